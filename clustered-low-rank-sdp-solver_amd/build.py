@@ -1,0 +1,35 @@
+"""Build libclrsdp.so in-tree with hipcc for gfx950 (no CMake; one translation unit)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "clrsdp.hip")
+OUT = os.path.join(HERE, "libclrsdp.so")
+DEPS = [SRC, os.path.join(HERE, "csrc", "kernels.h"), os.path.join(HERE, "csrc", "mwfloat.h"),
+        os.path.join(HERE, "..", "include", "clrsdp.h")]
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               # keep MFMA accumulators in the unified VGPR file (otherwise hipcc shuttles them
+               # through AGPRs every k-step: 46.7 vs 72.4 TF/s fp64, profiles/r01_f64_mfma_probe.log)
+               "-mllvm", "-amdgpu-mfma-vgpr-form"]
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and os.path.exists(OUT):
+        t = os.path.getmtime(OUT)
+        if all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d)):
+            return OUT
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc] + HIPCC_FLAGS + ["-o", OUT + ".tmp", SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,1077 @@
+// clrsdp.hip -- device-resident interior-point iteration behind the C ABI of include/clrsdp.h.
+//
+// One process drives one GPU.  The handle owns every device buffer; constraint data is uploaded
+// once and stays resident.  A loop body of solverank1sdp (MPMP.jl:755-887) is a fixed sequence
+// of batched launches on one stream (see DESIGN.md for the stage -> kernel table); the only
+// host synchronisation is the final read-back of the iteration statistics.  With
+// world_size > 1 each rank owns a subset of clusters and the few cross-cluster quantities (Q,
+// the n_y-vectors p and sum_j B_j^T S_j^-1 r_j, and ~10 scalars) are all-gathered through the
+// registered exchange and reduced in rank order, so every rank computes identical y, dy, alpha.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/clrsdp.h"
+#include "kernels.h"
+
+using namespace clrsdp;
+using mw::dd;
+using mw::Num;
+
+namespace {
+
+std::string g_last_error;
+
+struct ClrsdpError {
+  int code;
+  std::string msg;
+};
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess)                                                           \
+      throw ClrsdpError{CLRSDP_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+template <class X>
+X* dmalloc(size_t n) {
+  if (n == 0) n = 1;
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, n * sizeof(X)));
+  HIPCHK(hipMemset(p, 0, n * sizeof(X)));
+  return reinterpret_cast<X*>(p);
+}
+
+template <class X>
+X* upload_vec(const std::vector<X>& v) {
+  X* p = dmalloc<X>(v.size());
+  if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(X), hipMemcpyHostToDevice));
+  return p;
+}
+
+inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
+// --------------------------------------------------------------------------------------------
+// launch plans: descriptor arrays built once at creation, replayed every iteration
+// --------------------------------------------------------------------------------------------
+template <class T>
+struct GemmPlan {
+  bool ta = false, tb = false;
+  std::vector<GemmDesc<T>> h;
+  std::vector<int> t2d;
+  GemmDesc<T>* d = nullptr;
+  int* dt = nullptr;
+  static constexpr int TILE = std::is_same<T, double>::value ? 64 : 32;
+
+  void add(const T* A, int lda, const T* B, int ldb, const T* Cin, int ldcin, T* C, int ldc, int M,
+           int N, int K) {
+    if (M <= 0 || N <= 0) return;
+    GemmDesc<T> g;
+    g.A = A; g.B = B; g.Cin = Cin; g.C = C;
+    g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldcin = ldcin; g.ldc = ldc;
+    g.tn = cdiv(N, TILE);
+    g.tile0 = (int)t2d.size();
+    g.pad = 0;
+    const int nt = cdiv(M, TILE) * g.tn;
+    for (int i = 0; i < nt; ++i) t2d.push_back((int)h.size());
+    h.push_back(g);
+  }
+  void finalize() {
+    if (h.empty()) return;
+    d = upload_vec(h);
+    dt = upload_vec(t2d);
+  }
+  void launch(hipStream_t s, double alpha, double beta) const {
+    if (h.empty()) return;
+    const unsigned grid = (unsigned)t2d.size();
+    if constexpr (std::is_same<T, double>::value) {
+      if (!ta && !tb) gemm_f64_mfma<false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (ta && !tb) gemm_f64_mfma<true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (!ta && tb) gemm_f64_mfma<false, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else gemm_f64_mfma<true, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+    } else {
+      if (!ta && !tb) gemm_valu<T, false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (ta && !tb) gemm_valu<T, true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (!ta && tb) gemm_valu<T, false, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else gemm_valu<T, true, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+    }
+    HIPCHK(hipGetLastError());
+  }
+};
+
+template <class T>
+struct TrsmPlan {
+  static constexpr int NB = 16, NC = 64;
+  std::vector<TrsmDesc<T>> h;
+  std::vector<int> t2d;
+  TrsmDesc<T>* d = nullptr;
+  int* dt = nullptr;
+  int nmax = 0;
+  void add(const T* L, int ldl, T* B, int ldb, int n, int nrhs) {
+    if (n <= 0 || nrhs <= 0) return;
+    TrsmDesc<T> t;
+    t.L = L; t.B = B; t.n = n; t.nrhs = nrhs; t.ldl = ldl; t.ldb = ldb;
+    t.tile0 = (int)t2d.size();
+    t.pad = 0;
+    for (int i = 0; i < (int)cdiv(nrhs, NC); ++i) t2d.push_back((int)h.size());
+    h.push_back(t);
+    nmax = std::max(nmax, n);
+  }
+  void finalize() {
+    if (h.empty()) return;
+    d = upload_vec(h);
+    dt = upload_vec(t2d);
+  }
+  void launch(hipStream_t s, bool trans) const {
+    if (h.empty()) return;
+    const size_t lds = sizeof(T) * ((size_t)NB * NB + (size_t)NB * NC + (size_t)NB * nmax);
+    const unsigned grid = (unsigned)t2d.size();
+    if (trans) trsm_batched<T, true, NB, NC><<<grid, 256, lds, s>>>(d, dt);
+    else trsm_batched<T, false, NB, NC><<<grid, 256, lds, s>>>(d, dt);
+    HIPCHK(hipGetLastError());
+  }
+};
+
+template <class T>
+struct MatPlan {  // potrf / eigmin
+  static constexpr int NB = 16;
+  std::vector<MatDesc<T>> h;
+  MatDesc<T>* d = nullptr;
+  int nmax = 0;
+  void add(T* A, int n, int lda) {
+    MatDesc<T> m;
+    m.A = A; m.n = n; m.lda = lda;
+    h.push_back(m);
+    nmax = std::max(nmax, n);
+  }
+  void finalize() {
+    if (!h.empty()) d = upload_vec(h);
+  }
+  void potrf(hipStream_t s, int* info) const {
+    if (h.empty()) return;
+    const size_t lds = sizeof(T) * ((size_t)NB * NB + (size_t)NB * nmax);
+    potrf_batched<T, NB><<<(unsigned)h.size(), 256, lds, s>>>(d, info);
+    HIPCHK(hipGetLastError());
+  }
+  void eigmin(hipStream_t s, T* out) const {
+    if (h.empty()) return;
+    const size_t lds = sizeof(T) * (4 * (size_t)nmax + 256);
+    eigmin_batched<T><<<(unsigned)h.size(), 256, lds, s>>>(d, out);
+    HIPCHK(hipGetLastError());
+  }
+};
+
+struct HandleBase {
+  std::string err;
+  virtual ~HandleBase() {}
+  virtual void upload(const double* V, const double* lam, const double* B, const double* c,
+                      const double* b, const double* C) = 0;
+  virtual void set_state(const double* x, const double* X, const double* y, const double* Y) = 0;
+  virtual void get_state(double* x, double* X, double* y, double* Y) = 0;
+  virtual int initial(const clrsdp_params* prm, clrsdp_iter_stats* st) = 0;
+  virtual int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) = 0;
+  virtual int run_stage(int stage, const clrsdp_params* prm, int pd_feas) = 0;
+  virtual void get_buffer(int buf, double* host, int64_t* count) = 0;
+  virtual int64_t exchange_bytes() const = 0;
+  virtual void set_exchange(clrsdp_exchange_fn fn, void* ctx, void* send, void* recv) = 0;
+  virtual void set_stream(void* s) = 0;
+  virtual void* get_stream() const = 0;
+  virtual void synchronize() = 0;
+};
+
+template <class T>
+struct Solver final : HandleBase {
+  // ---------------- configuration / global description
+  int rank = 0, world = 1, timing = 0, W = Num<T>::W;
+  int64_t J = 0, n_y = 0;
+  std::vector<int64_t> m, Lc, Ns, Ds, xoff_g;    // per cluster
+  std::vector<int64_t> jl_first;                 // first (j,l) index of cluster j
+  std::vector<int64_t> delta, Kb, nb_g, blkoff_g, voff_g, koff_g;  // per (j,l)
+  std::vector<int64_t> rkoff_g;                  // offset into ranks[] of (j,l)
+  std::vector<int64_t> ranks_all;
+  std::vector<int64_t> Boff_g;                   // per cluster offset in global B
+  int64_t tot_x = 0, tot_blk = 0, tot_V = 0, tot_K = 0, tot_B = 0;
+  double dimtot = 0;
+
+  // ---------------- local (owned) layout
+  std::vector<int> oc;                       // owned clusters (global ids)
+  struct LBlk { int c, l; int64_t gjl; int n, del, K, m, N; int64_t off, voff, koff, toff, boff, ayoff, rsoff; };
+  std::vector<LBlk> lb;
+  std::vector<int64_t> c_xoff, c_Soff, c_Boff;   // per local cluster
+  int64_t nx = 0, nblk_el = 0, nV = 0, nK = 0, nT = 0, nBX = 0, nAY = 0, nS = 0, nB = 0, nRS = 0;
+  bool anyMgt1 = false, hasC = false;
+
+  // ---------------- device memory
+  hipStream_t own_stream = nullptr, stream = nullptr;
+  T *X, *Y, *Xinv, *LX, *LY, *R, *P, *dX, *dY, *Z, *tA, *tB, *Cm;
+  T *V, *lam, *TX, *TY, *BX, *BY, *AY, *tval, *S, *Wm, *Bm, *Qslab, *Q, *Qf;
+  T *cvec, *x, *dx, *dvec, *rhs, *tvec, *tmpv, *pslab, *y, *bvec, *dyv, *pvec, *uvec;
+  T *sc, *bpart, *eigX, *eigY, *tmpsc;
+  int *ksamp, *rsums, *info;
+  T *xsend = nullptr, *xrecv = nullptr, *own_send = nullptr;
+  int64_t xcap = 0;  // exchange capacity in T values
+  clrsdp_exchange_fn xfn = nullptr;
+  void* xctx = nullptr;
+  bool uploaded = false;
+  int info_count = 0, info_S0 = 0, info_Q0 = 0, info_Y0 = 0;
+
+  // ---------------- plans
+  GemmPlan<T> p_XY, p_dXdY, p_xinv, p_s1x, p_s1y, p_s2x, p_s2y, p_Q, p_wA_P, p_wA_dX, p_trU_Z,
+      p_trU_Y, p_By, p_Btx, p_Wt, p_Wdy, p_PY, p_Z, p_dXY, p_dY;
+  TrsmPlan<T> t_Linv, t_W, t_t, t_Q, t_sX1, t_sX2, t_sY1, t_sY2;
+  MatPlan<T> f_X, f_Y, f_S, f_Q, e_X, e_Y;
+  BlkDesc* d_blk = nullptr;      // all local blocks
+  BlkDesc* d_blk_m = nullptr;    // local blocks with m > 1
+  int n_blk_m = 0;
+  SchurClusterDesc* d_scd = nullptr;
+  SchurBlockDesc* d_sbd = nullptr;
+  long long n_pairs = 0;
+  AYDesc* d_ayd = nullptr;
+  PairDesc* d_pair = nullptr;
+  int n_pair = 0, max_K = 0;
+  ScaleDesc* d_scale = nullptr;
+  TupleDesc* d_td = nullptr;
+  TupleBlock* d_tb = nullptr;
+  hipEvent_t ev[CLRSDP_NUM_STAGES + 1];
+  float phase_ms[CLRSDP_NUM_STAGES];
+
+  int nb() const { return (int)lb.size(); }
+  int nc() const { return (int)oc.size(); }
+
+  Solver(const clrsdp_desc* desc, const clrsdp_config* cfg) {
+    rank = cfg->rank;
+    world = std::max(1, (int)cfg->world_size);
+    timing = cfg->timing;
+    HIPCHK(hipSetDevice(cfg->device));
+    J = desc->J;
+    n_y = desc->n_y;
+    if (J <= 0 || n_y <= 0) throw ClrsdpError{CLRSDP_E_ARG, "J and n_y must be positive"};
+    m.assign(desc->m, desc->m + J);
+    Lc.assign(desc->L, desc->L + J);
+    Ns.assign(desc->n_samples, desc->n_samples + J);
+    int64_t njl = 0;
+    for (int64_t j = 0; j < J; ++j) {
+      if (m[j] <= 0 || Lc[j] <= 0 || Ns[j] <= 0) throw ClrsdpError{CLRSDP_E_ARG, "bad m/L/N"};
+      Ds.push_back(m[j] * (m[j] + 1) / 2 * Ns[j]);
+      xoff_g.push_back(tot_x);
+      tot_x += Ds[j];
+      jl_first.push_back(njl);
+      njl += Lc[j];
+      Boff_g.push_back(tot_B);
+      tot_B += Ds[j] * n_y;
+    }
+    jl_first.push_back(njl);
+    int64_t rk = 0;
+    for (int64_t j = 0; j < J; ++j)
+      for (int64_t l = 0; l < Lc[j]; ++l) {
+        const int64_t g = jl_first[j] + l;
+        const int64_t del = desc->delta[g];
+        if (del <= 0) throw ClrsdpError{CLRSDP_E_ARG, "bad delta"};
+        delta.push_back(del);
+        rkoff_g.push_back(rk);
+        int64_t K = 0;
+        for (int64_t k = 0; k < Ns[j]; ++k) {
+          if (desc->ranks[rk + k] < 0) throw ClrsdpError{CLRSDP_E_ARG, "negative rank"};
+          K += desc->ranks[rk + k];
+          ranks_all.push_back(desc->ranks[rk + k]);
+        }
+        rk += Ns[j];
+        if (K <= 0) throw ClrsdpError{CLRSDP_E_ARG, "block without vectors"};
+        Kb.push_back(K);
+        const int64_t n = m[j] * del;
+        nb_g.push_back(n);
+        blkoff_g.push_back(tot_blk);
+        tot_blk += n * n;
+        voff_g.push_back(tot_V);
+        tot_V += del * K;
+        koff_g.push_back(tot_K);
+        tot_K += K;
+        dimtot += (double)n;
+      }
+    // owned clusters
+    if (cfg->owned && cfg->n_owned > 0) {
+      for (int i = 0; i < cfg->n_owned; ++i) {
+        if (cfg->owned[i] < 0 || cfg->owned[i] >= J) throw ClrsdpError{CLRSDP_E_ARG, "bad owned id"};
+        oc.push_back(cfg->owned[i]);
+      }
+      std::sort(oc.begin(), oc.end());
+    } else if (world == 1) {
+      for (int j = 0; j < J; ++j) oc.push_back(j);
+    }
+    // local layout
+    for (int c = 0; c < (int)oc.size(); ++c) {
+      const int j = oc[c];
+      c_xoff.push_back(nx);
+      nx += Ds[j];
+      c_Soff.push_back(nS);
+      nS += Ds[j] * Ds[j];
+      c_Boff.push_back(nB);
+      nB += Ds[j] * n_y;
+      if (m[j] > 1) anyMgt1 = true;
+      for (int l = 0; l < Lc[j]; ++l) {
+        LBlk b;
+        b.c = c; b.l = l; b.gjl = jl_first[j] + l;
+        b.n = (int)nb_g[b.gjl]; b.del = (int)delta[b.gjl]; b.K = (int)Kb[b.gjl];
+        b.m = (int)m[j]; b.N = (int)Ns[j];
+        b.off = nblk_el; nblk_el += (int64_t)b.n * b.n;
+        b.voff = nV; nV += (int64_t)b.del * b.K;
+        b.koff = nK; nK += b.K;
+        b.toff = nT; nT += (int64_t)b.n * b.m * b.K;
+        b.boff = nBX; nBX += (int64_t)b.m * b.K * b.m * b.K;
+        b.ayoff = nAY; nAY += (int64_t)b.m * (b.m + 1) / 2 * b.K;
+        b.rsoff = nRS; nRS += b.N + 1;
+        max_K = std::max(max_K, b.K);
+        lb.push_back(b);
+      }
+    }
+    HIPCHK(hipStreamCreateWithFlags(&own_stream, hipStreamNonBlocking));
+    stream = own_stream;
+    for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    allocate();
+    build_plans();
+  }
+
+  ~Solver() override {
+    // device memory is released with the process / hipDeviceReset; free what we own explicitly
+    T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, BX, BY, AY,
+                 tval, S, Wm, Bm, Qslab, Q, Qf, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
+                 bvec, dyv, pvec, uvec, sc, bpart, eigX, eigY, tmpsc, own_send};
+    for (T* p : bufs)
+      if (p) (void)hipFree(p);
+    (void)hipFree(ksamp);
+    (void)hipFree(rsums);
+    (void)hipFree(info);
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    if (own_stream) (void)hipStreamDestroy(own_stream);
+  }
+
+  void allocate() {
+    const int64_t B = std::max<int64_t>(nblk_el, 1);
+    X = dmalloc<T>(B); Y = dmalloc<T>(B); Xinv = dmalloc<T>(B); LX = dmalloc<T>(B);
+    LY = dmalloc<T>(B); R = dmalloc<T>(B); P = dmalloc<T>(B); dX = dmalloc<T>(B);
+    dY = dmalloc<T>(B); Z = dmalloc<T>(B); tA = dmalloc<T>(B); tB = dmalloc<T>(B);
+    Cm = dmalloc<T>(B);
+    V = dmalloc<T>(nV); lam = dmalloc<T>(nK);
+    // TX / TY also hold the trace_A products U (m(m+1)/2 * delta*K <= (m delta)(m K)) and the
+    // scaled vectors of compute_weighted_A
+    TX = dmalloc<T>(nT); TY = dmalloc<T>(nT);
+    BX = dmalloc<T>(nBX); BY = dmalloc<T>(nBX);
+    AY = dmalloc<T>(nAY); tval = dmalloc<T>(nAY);
+    S = dmalloc<T>(nS); Wm = dmalloc<T>(nB); Bm = dmalloc<T>(nB);
+    Qslab = dmalloc<T>((size_t)std::max(nc(), 1) * n_y * n_y);
+    Q = dmalloc<T>(n_y * n_y); Qf = dmalloc<T>(n_y * n_y);
+    cvec = dmalloc<T>(nx); x = dmalloc<T>(nx); dx = dmalloc<T>(nx); dvec = dmalloc<T>(nx);
+    rhs = dmalloc<T>(nx); tvec = dmalloc<T>(nx); tmpv = dmalloc<T>(nx);
+    pslab = dmalloc<T>((size_t)std::max(nc(), 1) * n_y);
+    y = dmalloc<T>(n_y); bvec = dmalloc<T>(n_y); dyv = dmalloc<T>(n_y); pvec = dmalloc<T>(n_y);
+    uvec = dmalloc<T>(n_y);
+    sc = dmalloc<T>(SC_COUNT);
+    bpart = dmalloc<T>(std::max(nb(), 1));
+    eigX = dmalloc<T>(std::max(nb(), 1));
+    eigY = dmalloc<T>(std::max(nb(), 1));
+    tmpsc = dmalloc<T>(8);
+    ksamp = dmalloc<int>(nK);
+    rsums = dmalloc<int>(nRS);
+    info_count = nb() + nc() + 1 + nb();
+    info_S0 = nb();
+    info_Q0 = nb() + nc();
+    info_Y0 = nb() + nc() + 1;
+    info = dmalloc<int>(info_count);
+    xcap = n_y * n_y + n_y + 16;
+    own_send = dmalloc<T>(xcap);
+    xsend = own_send;
+    xrecv = own_send;
+    // sample index of every vector column and the rank prefix sums, per local block
+    std::vector<int> ks(nK), rs(nRS);
+    for (const LBlk& b : lb) {
+      const int64_t r0 = rkoff_g[b.gjl];
+      int acc = 0, col = 0;
+      for (int k = 0; k < b.N; ++k) {
+        rs[b.rsoff + k] = acc;
+        for (int q = 0; q < ranks_all[r0 + k]; ++q) ks[b.koff + col++] = k;
+        acc += (int)ranks_all[r0 + k];
+      }
+      rs[b.rsoff + b.N] = acc;
+    }
+    if (nK) HIPCHK(hipMemcpy(ksamp, ks.data(), nK * sizeof(int), hipMemcpyHostToDevice));
+    if (nRS) HIPCHK(hipMemcpy(rsums, rs.data(), nRS * sizeof(int), hipMemcpyHostToDevice));
+  }
+
+  void build_plans() {
+    p_xinv.ta = true;
+    p_s2x.ta = p_s2y.ta = true;
+    p_Q.ta = true;
+    p_wA_P.tb = p_wA_dX.tb = true;
+    p_Btx.ta = true;
+    p_Wt.ta = true;
+    std::vector<BlkDesc> bd, bdm;
+    std::vector<AYDesc> ayd;
+    std::vector<PairDesc> pd;
+    std::vector<ScaleDesc> sd;
+    for (const LBlk& b : lb) {
+      const int n = b.n, del = b.del, K = b.K, mm = b.m;
+      BlkDesc d{b.off, n, 0};
+      bd.push_back(d);
+      if (mm > 1) bdm.push_back(d);
+      p_XY.add(X + b.off, n, Y + b.off, n, nullptr, n, R + b.off, n, n, n, n);
+      p_dXdY.add(dX + b.off, n, dY + b.off, n, R + b.off, n, R + b.off, n, n, n, n);
+      p_xinv.add(tA + b.off, n, tA + b.off, n, nullptr, n, Xinv + b.off, n, n, n, n);
+      p_PY.add(P + b.off, n, Y + b.off, n, R + b.off, n, tA + b.off, n, n, n, n);
+      p_Z.add(Xinv + b.off, n, tA + b.off, n, nullptr, n, Z + b.off, n, n, n, n);
+      p_dXY.add(dX + b.off, n, Y + b.off, n, R + b.off, n, tA + b.off, n, n, n, n);
+      p_dY.add(Xinv + b.off, n, tA + b.off, n, nullptr, n, dY + b.off, n, n, n, n);
+      t_Linv.add(LX + b.off, n, tA + b.off, n, n, n);
+      t_sX1.add(LX + b.off, n, tA + b.off, n, n, n);
+      t_sX2.add(LX + b.off, n, tB + b.off, n, n, n);
+      t_sY1.add(LY + b.off, n, tA + b.off, n, n, n);
+      t_sY2.add(LY + b.off, n, tB + b.off, n, n, n);
+      f_X.add(LX + b.off, n, n);
+      f_Y.add(LY + b.off, n, n);
+      e_X.add(tB + b.off, n, n);
+      e_Y.add(tB + b.off, n, n);
+      const int ldT = n;           // TX_b is (m delta) x (m K)
+      const int ldBX = mm * K;     // BX_b is (m K) x (m K)
+      for (int s = 0; s < mm; ++s) {
+        p_s1x.add(Xinv + b.off + (int64_t)s * del * n, n, V + b.voff, del, nullptr, 0,
+                  TX + b.toff + (int64_t)s * K * ldT, ldT, n, K, del);
+        p_s1y.add(Y + b.off + (int64_t)s * del * n, n, V + b.voff, del, nullptr, 0,
+                  TY + b.toff + (int64_t)s * K * ldT, ldT, n, K, del);
+        for (int r = 0; r < mm; ++r) {
+          p_s2x.add(V + b.voff, del, TX + b.toff + r * del + (int64_t)s * K * ldT, ldT, nullptr, 0,
+                    BX + b.boff + r * K + (int64_t)s * K * ldBX, ldBX, K, K, del);
+          p_s2y.add(V + b.voff, del, TY + b.toff + r * del + (int64_t)s * K * ldT, ldT, nullptr, 0,
+                    BY + b.boff + r * K + (int64_t)s * K * ldBX, ldBX, K, K, del);
+        }
+      }
+      ayd.push_back(AYDesc{b.boff, b.ayoff, K, mm});
+      const int64_t xo = c_xoff[b.c];
+      for (int r = 0; r < mm; ++r)
+        for (int s = 0; s <= r; ++s) {
+          const int rsi = s + r * (r + 1) / 2;
+          const int64_t uoff = b.toff + (int64_t)rsi * del * K;  // U / Vs slot in TX / TY
+          // trace_A: U = Z[r,s] V   (Z block rows r, cols s)
+          p_trU_Z.add(Z + b.off + r * del + (int64_t)s * del * n, n, V + b.voff, del, nullptr, 0,
+                      TX + uoff, del, del, K, del);
+          p_trU_Y.add(Y + b.off + r * del + (int64_t)s * del * n, n, V + b.voff, del, nullptr, 0,
+                      TX + uoff, del, del, K, del);
+          pd.push_back(PairDesc{uoff, b.voff, b.ayoff + (int64_t)rsi * K, del, K});
+          // weighted A: block (s, r) = Vs V^T  (MPMP.jl:1659-1667)
+          ScaleDesc s_;
+          s_.v_off = b.voff; s_.vs_off = uoff; s_.delta = del; s_.K = K;
+          s_.ks_off = (int)b.koff; s_.lam_off = (int)b.koff;
+          s_.a_off = (int)(xo + (int64_t)rsi * b.N);
+          s_.scale = (r != s) ? 0.5 : 1.0;
+          sd.push_back(s_);
+          p_wA_P.add(TY + uoff, del, V + b.voff, del, nullptr, 0,
+                     P + b.off + s * del + (int64_t)r * del * n, n, del, del, K);
+          p_wA_dX.add(TY + uoff, del, V + b.voff, del, nullptr, 0,
+                      dX + b.off + s * del + (int64_t)r * del * n, n, del, del, K);
+        }
+    }
+    n_blk_m = (int)bdm.size();
+    d_blk = upload_vec(bd);
+    if (n_blk_m) d_blk_m = upload_vec(bdm);
+    d_ayd = upload_vec(ayd);
+    n_pair = (int)pd.size();
+    d_pair = upload_vec(pd);
+    d_scale = upload_vec(sd);
+    // per cluster plans
+    std::vector<SchurClusterDesc> scd;
+    std::vector<SchurBlockDesc> sbd;
+    std::vector<TupleDesc> td;
+    std::vector<TupleBlock> tbk;
+    int bi = 0;
+    for (int c = 0; c < nc(); ++c) {
+      const int j = oc[c];
+      const int D = (int)Ds[j];
+      T* Sc = S + c_Soff[c];
+      T* Wc = Wm + c_Boff[c];
+      T* Bc = Bm + c_Boff[c];
+      const int64_t xo = c_xoff[c];
+      f_S.add(Sc, D, D);
+      t_W.add(Sc, D, Wc, D, D, (int)n_y);
+      t_t.add(Sc, D, tvec + xo, D, D, 1);
+      p_Q.add(Wc, D, Wc, D, nullptr, 0, Qslab + (int64_t)c * n_y * n_y, (int)n_y, (int)n_y, (int)n_y, D);
+      p_By.add(Bc, D, y, (int)n_y, nullptr, 0, tmpv + xo, D, D, 1, (int)n_y);
+      p_Btx.add(Bc, D, x + xo, D, nullptr, 0, pslab + (int64_t)c * n_y, (int)n_y, (int)n_y, 1, D);
+      p_Wt.add(Wc, D, tvec + xo, D, nullptr, 0, pslab + (int64_t)c * n_y, (int)n_y, (int)n_y, 1, D);
+      p_Wdy.add(Wc, D, dyv, (int)n_y, tvec + xo, D, dx + xo, D, D, 1, (int)n_y);
+      SchurClusterDesc cdsc;
+      cdsc.m = (int)m[j]; cdsc.N = (int)Ns[j]; cdsc.D = D;
+      cdsc.blk0 = bi; cdsc.nblk = (int)Lc[j];
+      cdsc.pair0 = (int)n_pairs;
+      cdsc.S_off = c_Soff[c];
+      scd.push_back(cdsc);
+      n_pairs += (long long)D * (D + 1) / 2;
+      TupleDesc tdc;
+      tdc.x_off = (int)xo; tdc.N = (int)Ns[j]; tdc.m = (int)m[j];
+      tdc.blk0 = bi; tdc.nblk = (int)Lc[j]; tdc.t0 = (int)xo;
+      td.push_back(tdc);
+      for (int l = 0; l < Lc[j]; ++l, ++bi) {
+        const LBlk& b = lb[bi];
+        SchurBlockDesc s;
+        s.bx_off = b.boff; s.K = b.K; s.rs_off = (int)b.rsoff; s.lam_off = (int)b.koff; s.pad = 0;
+        sbd.push_back(s);
+        TupleBlock t;
+        t.val_off = b.ayoff; t.K = b.K; t.rs_off = (int)b.rsoff; t.lam_off = (int)b.koff; t.pad = 0;
+        tbk.push_back(t);
+      }
+    }
+    t_Q.add(Qf, (int)n_y, dyv, (int)n_y, (int)n_y, 1);
+    t_dxadd_init();
+    f_Q.add(Qf, (int)n_y, (int)n_y);
+    if (nc()) {
+      d_scd = upload_vec(scd);
+      d_sbd = upload_vec(sbd);
+      d_td = upload_vec(td);
+      d_tb = upload_vec(tbk);
+    }
+    for (GemmPlan<T>* g : {&p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
+                           &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
+                           &p_Z, &p_dXY, &p_dY})
+      g->finalize();
+    for (TrsmPlan<T>* t : {&t_Linv, &t_W, &t_t, &t_Q, &t_sX1, &t_sX2, &t_sY1, &t_sY2, &t_dx})
+      t->finalize();
+    for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q, &e_X, &e_Y}) f->finalize();
+  }
+
+  TrsmPlan<T> t_dx;
+  void t_dxadd_init() {
+    for (int c = 0; c < nc(); ++c) {
+      const int D = (int)Ds[oc[c]];
+      t_dx.add(S + c_Soff[c], D, dx + c_xoff[c], D, D, 1);
+    }
+  }
+
+  // ---------------- host <-> device conversion
+  void put(T* dst, const double* planes, int64_t nplane, int64_t first, int64_t count) {
+    if (count <= 0) return;
+    std::vector<T> tmp(count);
+    for (int64_t i = 0; i < count; ++i) Num<T>::pack(planes, nplane, first + i, &tmp[i]);
+    HIPCHK(hipMemcpyAsync(dst, tmp.data(), count * sizeof(T), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+  void get(const T* src, double* planes, int64_t nplane, int64_t first, int64_t count) {
+    if (count <= 0) return;
+    std::vector<T> tmp(count);
+    HIPCHK(hipMemcpyAsync(tmp.data(), src, count * sizeof(T), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    for (int64_t i = 0; i < count; ++i) Num<T>::unpack(tmp[i], planes, nplane, first + i);
+  }
+
+  void upload(const double* Vh, const double* lamh, const double* Bh, const double* ch,
+              const double* bh, const double* Ch) override {
+    for (const LBlk& b : lb) {
+      put(V + b.voff, Vh, tot_V, voff_g[b.gjl], (int64_t)b.del * b.K);
+      put(lam + b.koff, lamh, tot_K, koff_g[b.gjl], b.K);
+    }
+    for (int c = 0; c < nc(); ++c) {
+      const int j = oc[c];
+      put(Bm + c_Boff[c], Bh, tot_B, Boff_g[j], Ds[j] * n_y);
+      put(cvec + c_xoff[c], ch, tot_x, xoff_g[j], Ds[j]);
+    }
+    put(bvec, bh, n_y, 0, n_y);
+    hasC = (Ch != nullptr);
+    if (hasC)
+      for (const LBlk& b : lb) put(Cm + b.off, Ch, tot_blk, blkoff_g[b.gjl], (int64_t)b.n * b.n);
+    uploaded = true;
+  }
+
+  void set_state(const double* xh, const double* Xh, const double* yh, const double* Yh) override {
+    for (int c = 0; c < nc(); ++c) put(x + c_xoff[c], xh, tot_x, xoff_g[oc[c]], Ds[oc[c]]);
+    for (const LBlk& b : lb) {
+      put(X + b.off, Xh, tot_blk, blkoff_g[b.gjl], (int64_t)b.n * b.n);
+      put(Y + b.off, Yh, tot_blk, blkoff_g[b.gjl], (int64_t)b.n * b.n);
+    }
+    put(y, yh, n_y, 0, n_y);
+  }
+  void get_state(double* xh, double* Xh, double* yh, double* Yh) override {
+    if (xh)
+      for (int c = 0; c < nc(); ++c) get(x + c_xoff[c], xh, tot_x, xoff_g[oc[c]], Ds[oc[c]]);
+    for (const LBlk& b : lb) {
+      if (Xh) get(X + b.off, Xh, tot_blk, blkoff_g[b.gjl], (int64_t)b.n * b.n);
+      if (Yh) get(Y + b.off, Yh, tot_blk, blkoff_g[b.gjl], (int64_t)b.n * b.n);
+    }
+    if (yh) get(y, yh, n_y, 0, n_y);
+  }
+
+  // ---------------- exchange
+  // Partials are written to xsend[0..cnt); after the exchange rank r's copy is at
+  // xrecv[r*cnt..].  world == 1: xrecv == xsend, nothing to do.
+  void exchange(int tag, int64_t cnt) {
+    if (world == 1) return;
+    if (!xfn) throw ClrsdpError{CLRSDP_E_EXCHANGE, "world_size > 1 but no exchange registered"};
+    const int rc = xfn(xctx, tag, cnt * (int64_t)sizeof(T), (void*)stream);
+    if (rc != 0) throw ClrsdpError{CLRSDP_E_EXCHANGE, "exchange callback failed"};
+  }
+  // reduce slot `slot` of every rank's partial vector (length cnt) in rank order into dst
+  void reduce_ranks(int64_t cnt, int64_t slot, int op, T* dst) {
+    ordered_reduce<T><<<1, 1, 0, stream>>>(xrecv + slot, world, cnt, op, dst);
+  }
+
+  // ---------------- kernels shorthands
+  void blk_lin(T* out, const T* A, double a, const T* B_, double b, const T* scal = nullptr,
+               double sm = 1.0) {
+    if (nb()) blk_axpby<T><<<nb(), 256, 0, stream>>>(d_blk, out, A, B_, a, b, scal, sm);
+  }
+  void vlin(T* out, const T* a_, double ca, const T* b_, double cb, const T* c_, double cc,
+            int64_t n) {
+    if (n > 0) vec_lin<T><<<cdiv(n, 256), 256, 0, stream>>>(out, a_, ca, b_, cb, c_, cc, n);
+  }
+  void fill(T* out, double v, int64_t n) {
+    if (n > 0) vec_fill<T><<<cdiv(n, 256), 256, 0, stream>>>(out, v, n);
+  }
+  void sym(T* out, const T* Zm, int mode, bool only_m = false) {
+    if (only_m) {
+      if (n_blk_m) blk_sym<T><<<n_blk_m, 256, 0, stream>>>(d_blk_m, out, Zm, mode);
+    } else if (nb()) {
+      blk_sym<T><<<nb(), 256, 0, stream>>>(d_blk, out, Zm, mode);
+    }
+  }
+  ScalarParams<T> sparams(const clrsdp_params* prm, int pd_feas) {
+    ScalarParams<T> p;
+    auto lim = [](const double* l) {
+      T v = T(l[0]);
+      for (int i = 1; i < Num<T>::W && i < 4; ++i) v += T(l[i]);
+      return v;
+    };
+    p.beta_inf = lim(prm->beta_infeasible);
+    p.beta_feas = lim(prm->beta_feasible);
+    p.gamma = lim(prm->gamma);
+    p.b0 = lim(prm->b0);
+    p.dim = dimtot;
+    p.pd_feas = pd_feas;
+    return p;
+  }
+  void scalars(const clrsdp_params* prm, int pd_feas, int which) {
+    scalar_kernel<T><<<1, 1, 0, stream>>>(sc, sparams(prm, pd_feas), which);
+  }
+  // local block-sum (op 0/1) or block-max (op 2) into *dst
+  void local_blk_reduce(const T* A, const T* B_, const T* dA, const T* dB, int op, T* dst) {
+    if (nb()) {
+      blk_reduce<T><<<nb(), 256, 0, stream>>>(d_blk, A, B_, dA, dB, op, bpart);
+      ordered_reduce<T><<<1, 1, 0, stream>>>(bpart, nb(), 1, op, dst);
+    } else {
+      fill(dst, 0.0, 1);
+    }
+  }
+
+  // trace_A with the products U already in TX -> val (tval) -> aggregate
+  void trace_aggregate(const T* val, const T* in, double c_in, const T* in2, double c_in2,
+                       double c_agg, T* out) {
+    if (nx > 0)
+      tuple_aggregate<T><<<cdiv(nx, 256), 256, 0, stream>>>(d_td, nc(), d_tb, rsums, lam, val, in,
+                                                            c_in, in2, c_in2, c_agg, out, nx);
+  }
+  void colsums() {
+    if (n_pair) {
+      dim3 g(cdiv(max_K, 4), n_pair);
+      colsum_dot<T><<<g, 256, 0, stream>>>(d_pair, TX, V, tval);
+    }
+  }
+  void weighted_A(const T* a, const GemmPlan<T>& plan, T* out) {
+    if (n_pair) {
+      dim3 g(64, n_pair);
+      scale_cols<T><<<g, 256, 0, stream>>>(d_scale, V, lam, ksamp, a, TY);
+    }
+    plan.launch(stream, 1.0, 0.0);
+    if (anyMgt1) sym(out, out, 1, true);  // Symmetric(.) on blocks with m != 1 (MPMP.jl:1671-1674)
+  }
+
+  // ---------------- stages
+  void st_mu_r(const clrsdp_params* prm, int pd_feas) {
+    local_blk_reduce(X, Y, nullptr, nullptr, 0, xsend);
+    exchange(1, 1);
+    reduce_ranks(1, 0, 0, sc + SC_DOT_XY);
+    scalars(prm, pd_feas, 0);
+    p_XY.launch(stream, -1.0, 0.0);             // R = -XY
+    blk_lin(R, R, 1.0, nullptr, 0.0, sc + SC_MU_P);  // R += mu_p I
+  }
+  void st_xinv() {
+    blk_lin(LX, X, 1.0, nullptr, 0.0);
+    f_X.potrf(stream, info);
+    if (nb()) blk_identity<T><<<nb(), 256, 0, stream>>>(d_blk, tA);
+    t_Linv.launch(stream, false);             // tA = L^-1
+    p_xinv.launch(stream, 1.0, 0.0);          // X^-1 = L^-T L^-1
+  }
+  void st_schur() {
+    p_s1x.launch(stream, 1.0, 0.0);
+    p_s1y.launch(stream, 1.0, 0.0);
+    p_s2x.launch(stream, 1.0, 0.0);
+    p_s2y.launch(stream, 1.0, 0.0);
+    if (nb()) extract_AY<T><<<nb(), 256, 0, stream>>>(d_ayd, BY, AY);
+    if (n_pairs)
+      schur_assemble<T><<<cdiv(n_pairs, 256), 256, 0, stream>>>(d_scd, nc(), d_sbd, rsums, lam, BX,
+                                                                 BY, S, n_pairs);
+  }
+  void st_factor() {
+    f_S.potrf(stream, info + info_S0);
+    vlin(Wm, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
+    t_W.launch(stream, false);                // W_j = L_j^-1 B_j
+    p_Q.launch(stream, 1.0, 0.0);             // slab_j = W_j^T W_j
+    const int64_t q2 = n_y * n_y;
+    if (nc()) slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(Qslab, nc(), q2, q2, xsend);
+    else fill(xsend, 0.0, q2);
+    exchange(2, q2);
+    slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(xrecv, world, q2, q2, Q);
+    vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
+    f_Q.potrf(stream, info + info_Q0);
+  }
+  void st_residuals(bool use_AY) {
+    // P = sum_i x_i A_i - X - C
+    weighted_A(x, p_wA_P, P);
+    blk_lin(P, P, 1.0, X, -1.0);
+    if (hasC) blk_lin(P, P, 1.0, Cm, -1.0);
+    // d = c - B y - Tr(A_* Y)
+    p_By.launch(stream, 1.0, 0.0);
+    if (!use_AY) {
+      p_trU_Y.launch(stream, 1.0, 0.0);
+      colsums();
+    }
+    trace_aggregate(use_AY ? AY : tval, cvec, 1.0, tmpv, -1.0, -1.0, dvec);
+    // p partial = sum_j B_j^T x_j ; errors
+    p_Btx.launch(stream, 1.0, 0.0);
+    const int64_t k = n_y + 2;
+    if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+    else fill(xsend, 0.0, n_y);
+    local_blk_reduce(P, nullptr, nullptr, nullptr, 2, xsend + n_y);
+    if (nx > 0) vec_reduce<T><<<1, 256, 0, stream>>>(dvec, nullptr, nx, 2, xsend + n_y + 1);
+    else fill(xsend + n_y + 1, 0.0, 1);
+    exchange(3, k);
+    slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, k, n_y, uvec);
+    vlin(pvec, bvec, 1.0, uvec, -1.0, nullptr, 0, n_y);      // p = b - sum B^T x
+    reduce_ranks(k, n_y, 2, sc + SC_ERR_PMAT);
+    reduce_ranks(k, n_y + 1, 2, sc + SC_ERR_DVEC);
+    vec_reduce<T><<<1, 256, 0, stream>>>(pvec, nullptr, n_y, 2, sc + SC_ERR_PVEC);
+  }
+  void st_direction(int tag) {
+    // Z = sym(X^-1 (P Y - R))
+    p_PY.launch(stream, 1.0, -1.0);
+    p_Z.launch(stream, 1.0, 0.0);
+    sym(Z, Z, 0);
+    // rhs_x = -d - Tr(A_* Z)
+    p_trU_Z.launch(stream, 1.0, 0.0);
+    colsums();
+    trace_aggregate(tval, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
+    // t_j = L_j^-1 rhs_j ;  u = sum_j W_j^T t_j ;  dy = Q^-1 (p - u)
+    vlin(tvec, rhs, 1.0, nullptr, 0, nullptr, 0, nx);
+    t_t.launch(stream, false);
+    p_Wt.launch(stream, 1.0, 0.0);
+    if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+    else fill(xsend, 0.0, n_y);
+    exchange(tag, n_y);
+    slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec);
+    vlin(dyv, pvec, 1.0, uvec, -1.0, nullptr, 0, n_y);
+    t_Q.launch(stream, false);
+    t_Q.launch(stream, true);
+    // dx_j = L_j^-T (t_j + W_j dy)
+    p_Wdy.launch(stream, 1.0, 1.0);
+    t_dx.launch(stream, true);
+    // dX = P + sum_i dx_i A_i
+    weighted_A(dx, p_wA_dX, dX);
+    blk_lin(dX, dX, 1.0, P, 1.0);
+    // dY = sym(X^-1 (R - dX Y))
+    p_dXY.launch(stream, -1.0, 1.0);
+    p_dY.launch(stream, 1.0, 0.0);
+    sym(dY, dY, 0);
+  }
+  void st_corrector_r(const clrsdp_params* prm, int pd_feas) {
+    local_blk_reduce(X, Y, dX, dY, 1, xsend);
+    exchange(5, 1);
+    reduce_ranks(1, 0, 0, sc + SC_DOT_XDY);
+    scalars(prm, pd_feas, 1);
+    p_XY.launch(stream, -1.0, 0.0);
+    p_dXdY.launch(stream, -1.0, 1.0);
+    blk_lin(R, R, 1.0, nullptr, 0.0, sc + SC_MU_C);
+  }
+  void st_step(const clrsdp_params* prm, int pd_feas) {
+    // X: L_X from the X^-1 stage
+    blk_lin(tA, dX, 1.0, nullptr, 0.0);
+    t_sX1.launch(stream, false);
+    sym(tB, tA, 2);
+    t_sX2.launch(stream, false);
+    e_X.eigmin(stream, eigX);
+    // Y
+    blk_lin(LY, Y, 1.0, nullptr, 0.0);
+    f_Y.potrf(stream, info + info_Y0);
+    blk_lin(tA, dY, 1.0, nullptr, 0.0);
+    t_sY1.launch(stream, false);
+    sym(tB, tA, 2);
+    t_sY2.launch(stream, false);
+    e_Y.eigmin(stream, eigY);
+    if (nb()) {
+      ordered_reduce<T><<<1, 1, 0, stream>>>(eigX, nb(), 1, 3, xsend);
+      ordered_reduce<T><<<1, 1, 0, stream>>>(eigY, nb(), 1, 3, xsend + 1);
+    } else {
+      fill(xsend, 1e300, 2);  // no local blocks: neutral element of min
+    }
+    exchange(8, 2);
+    reduce_ranks(2, 0, 3, sc + SC_MINEIG_X);
+    reduce_ranks(2, 1, 3, sc + SC_MINEIG_Y);
+    scalars(prm, pd_feas, 2);
+  }
+  void objectives(const clrsdp_params* prm, int pd_feas) {
+    if (nx > 0) vec_reduce<T><<<1, 256, 0, stream>>>(cvec, x, nx, 0, xsend);
+    else fill(xsend, 0.0, 1);
+    if (hasC) local_blk_reduce(Cm, Y, nullptr, nullptr, 0, xsend + 1);
+    else fill(xsend + 1, 0.0, 1);
+    exchange(9, 2);
+    reduce_ranks(2, 0, 0, sc + SC_DOT_CX);
+    reduce_ranks(2, 1, 0, sc + SC_DOT_CY);
+    vec_reduce<T><<<1, 256, 0, stream>>>(bvec, y, n_y, 0, sc + SC_DOT_BY);
+    scalars(prm, pd_feas, 3);
+  }
+  void st_update(const clrsdp_params* prm, int pd_feas) {
+    if (nx > 0) vec_axpy_dev<T><<<cdiv(nx, 256), 256, 0, stream>>>(x, dx, sc + SC_ALPHA_P, nx);
+    vec_axpy_dev<T><<<cdiv(n_y, 256), 256, 0, stream>>>(y, dyv, sc + SC_ALPHA_D, n_y);
+    if (nb()) {
+      blk_axpy_dev<T><<<nb(), 256, 0, stream>>>(d_blk, X, dX, sc + SC_ALPHA_P);
+      blk_axpy_dev<T><<<nb(), 256, 0, stream>>>(d_blk, Y, dY, sc + SC_ALPHA_D);
+    }
+    objectives(prm, pd_feas);
+  }
+
+  void stage(int s, const clrsdp_params* prm, int pd_feas) {
+    switch (s) {
+      case CLRSDP_STAGE_MU_R: st_mu_r(prm, pd_feas); break;
+      case CLRSDP_STAGE_XINV: st_xinv(); break;
+      case CLRSDP_STAGE_SCHUR: st_schur(); break;
+      case CLRSDP_STAGE_FACTOR: st_factor(); break;
+      case CLRSDP_STAGE_RESIDUALS: st_residuals(true); break;
+      case CLRSDP_STAGE_PREDICTOR: st_direction(4); break;
+      case CLRSDP_STAGE_CORRECTOR_R: st_corrector_r(prm, pd_feas); break;
+      case CLRSDP_STAGE_CORRECTOR: st_direction(6); break;
+      case CLRSDP_STAGE_STEP: st_step(prm, pd_feas); break;
+      case CLRSDP_STAGE_UPDATE: st_update(prm, pd_feas); break;
+      default: throw ClrsdpError{CLRSDP_E_ARG, "bad stage"};
+    }
+    HIPCHK(hipGetLastError());
+  }
+
+  int check_info() {
+    std::vector<int> h(info_count);
+    HIPCHK(hipMemcpyAsync(h.data(), info, info_count * sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    for (int i = 0; i < nb(); ++i)
+      if (h[i]) { err = "X block not positive definite (spd_inv! failed)"; return CLRSDP_E_NOT_PD_X; }
+    for (int i = 0; i < nc(); ++i)
+      if (h[info_S0 + i]) { err = "S was not decomposed succesfully, try again with higher precision"; return CLRSDP_E_NOT_PD_S; }
+    if (h[info_Q0]) { err = "Q was not decomposed correctly. Try restarting with a higher precision."; return CLRSDP_E_NOT_PD_Q; }
+    for (int i = 0; i < nb(); ++i)
+      if (h[info_Y0 + i]) { err = "The step length could not be calculated correctly (Y not PD)."; return CLRSDP_E_STEP; }
+    return CLRSDP_OK;
+  }
+
+  void read_stats(clrsdp_iter_stats* st) {
+    std::vector<T> h(SC_COUNT);
+    HIPCHK(hipMemcpyAsync(h.data(), sc, SC_COUNT * sizeof(T), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    auto f = [&](int i) { return Num<T>::hi(h[i]); };
+    st->mu = f(SC_MU);
+    st->P_err = f(SC_ERR_PMAT);
+    st->p_err = f(SC_ERR_PVEC);
+    st->d_err = f(SC_ERR_DVEC);
+    st->alpha_p = f(SC_ALPHA_P);
+    st->alpha_d = f(SC_ALPHA_D);
+    st->beta_c = f(SC_BETA_C);
+    st->p_obj = f(SC_POBJ);
+    st->d_obj = f(SC_DOBJ);
+  }
+
+  int initial(const clrsdp_params* prm, clrsdp_iter_stats* st) override {
+    if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
+    std::memset(st, 0, sizeof(*st));
+    st_residuals(false);
+    objectives(prm, 0);
+    read_stats(st);
+    return CLRSDP_OK;
+  }
+
+  int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
+    if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
+    HIPCHK(hipMemsetAsync(info, 0, info_count * sizeof(int), stream));
+    for (int s = 0; s < CLRSDP_NUM_STAGES; ++s) {
+      if (timing) HIPCHK(hipEventRecord(ev[s], stream));
+      stage(s, prm, pd_feas);
+    }
+    if (timing) HIPCHK(hipEventRecord(ev[CLRSDP_NUM_STAGES], stream));
+    std::memset(st, 0, sizeof(*st));
+    read_stats(st);
+    if (timing)
+      for (int s = 0; s < CLRSDP_NUM_STAGES; ++s) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ev[s], ev[s + 1]));
+        st->phase_ms[s] = ms;
+      }
+    const int rc = check_info();
+    st->status = rc;
+    return rc;
+  }
+
+  int run_stage(int s, const clrsdp_params* prm, int pd_feas) override {
+    if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
+    if (s == 0) HIPCHK(hipMemsetAsync(info, 0, info_count * sizeof(int), stream));
+    stage(s, prm, pd_feas);
+    HIPCHK(hipStreamSynchronize(stream));
+    return check_info();
+  }
+
+  void get_buffer(int buf, double* host, int64_t* count) override {
+    const T* src = nullptr;
+    int64_t n = 0;
+    switch (buf) {
+      case CLRSDP_BUF_X: src = X; n = nblk_el; break;
+      case CLRSDP_BUF_Y: src = Y; n = nblk_el; break;
+      case CLRSDP_BUF_XINV: src = Xinv; n = nblk_el; break;
+      case CLRSDP_BUF_R: src = R; n = nblk_el; break;
+      case CLRSDP_BUF_S: src = S; n = nS; break;
+      case CLRSDP_BUF_AY: src = AY; n = nAY; break;
+      case CLRSDP_BUF_Q: src = Q; n = n_y * n_y; break;
+      case CLRSDP_BUF_P: src = P; n = nblk_el; break;
+      case CLRSDP_BUF_PVEC: src = pvec; n = n_y; break;
+      case CLRSDP_BUF_DVEC: src = dvec; n = nx; break;
+      case CLRSDP_BUF_DX: src = dx; n = nx; break;
+      case CLRSDP_BUF_DXMAT: src = dX; n = nblk_el; break;
+      case CLRSDP_BUF_DY: src = dyv; n = n_y; break;
+      case CLRSDP_BUF_DYMAT: src = dY; n = nblk_el; break;
+      case CLRSDP_BUF_XVEC: src = x; n = nx; break;
+      case CLRSDP_BUF_YVEC: src = y; n = n_y; break;
+      case CLRSDP_BUF_SCALARS: src = sc; n = SC_COUNT; break;
+      default: throw ClrsdpError{CLRSDP_E_ARG, "bad buffer id"};
+    }
+    if (count) *count = n;
+    if (host) get(src, host, n, 0, n);
+  }
+
+  int64_t exchange_bytes() const override { return xcap * (int64_t)sizeof(T); }
+  void set_exchange(clrsdp_exchange_fn fn, void* ctx, void* send, void* recv) override {
+    xfn = fn;
+    xctx = ctx;
+    if (send && recv) {
+      xsend = reinterpret_cast<T*>(send);
+      xrecv = reinterpret_cast<T*>(recv);
+    } else {
+      xsend = xrecv = own_send;
+    }
+  }
+  void set_stream(void* s) override { stream = s ? reinterpret_cast<hipStream_t>(s) : own_stream; }
+  void* get_stream() const override { return (void*)stream; }
+  void synchronize() override { HIPCHK(hipStreamSynchronize(stream)); }
+};
+
+}  // namespace
+
+struct clrsdp_handle {
+  std::unique_ptr<HandleBase> impl;
+};
+
+#define GUARD(h, body)                                          \
+  try {                                                         \
+    body                                                        \
+  } catch (const ClrsdpError& e) {                              \
+    g_last_error = e.msg;                                       \
+    if (h) (h)->impl->err = e.msg;                              \
+    return e.code;                                              \
+  } catch (const std::exception& e) {                           \
+    g_last_error = e.what();                                    \
+    if (h) (h)->impl->err = e.what();                           \
+    return CLRSDP_E_HIP;                                        \
+  }
+
+extern "C" {
+
+int32_t clrsdp_version(void) { return 100; }
+
+const char* clrsdp_last_error(const clrsdp_handle* h) {
+  if (h && !h->impl->err.empty()) return h->impl->err.c_str();
+  return g_last_error.c_str();
+}
+
+int32_t clrsdp_create(const clrsdp_desc* desc, const clrsdp_config* cfg, clrsdp_handle** out) {
+  clrsdp_handle* h = nullptr;
+  if (!desc || !cfg || !out) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, {
+    auto* hh = new clrsdp_handle();
+    if (cfg->precision_words == 1) hh->impl.reset(new Solver<double>(desc, cfg));
+    else if (cfg->precision_words == 2) hh->impl.reset(new Solver<dd>(desc, cfg));
+    else { delete hh; g_last_error = "precision_words must be 1 or 2"; return CLRSDP_E_ARG; }
+    *out = hh;
+    return CLRSDP_OK;
+  })
+}
+
+int32_t clrsdp_upload_constraints(clrsdp_handle* h, const double* V, const double* lambda,
+                                  const double* B, const double* c, const double* b,
+                                  const double* C) {
+  if (!h || !V || !lambda || !B || !c || !b) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->upload(V, lambda, B, c, b, C); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_set_state(clrsdp_handle* h, const double* x, const double* X, const double* y,
+                         const double* Y) {
+  if (!h || !x || !X || !y || !Y) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->set_state(x, X, y, Y); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_get_state(clrsdp_handle* h, double* x, double* X, double* y, double* Y) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->get_state(x, X, y, Y); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_initial_residuals(clrsdp_handle* h, const clrsdp_params* prm, clrsdp_iter_stats* st) {
+  if (!h || !prm || !st) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, { return h->impl->initial(prm, st); })
+}
+
+int32_t clrsdp_iterate(clrsdp_handle* h, const clrsdp_params* prm, int32_t pd_feas,
+                       clrsdp_iter_stats* st) {
+  if (!h || !prm || !st) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, { return h->impl->iterate(prm, pd_feas, st); })
+}
+
+int32_t clrsdp_run_stage(clrsdp_handle* h, int32_t stage, const clrsdp_params* prm, int32_t pd_feas) {
+  if (!h || !prm) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, { return h->impl->run_stage(stage, prm, pd_feas); })
+}
+
+int32_t clrsdp_get_buffer(clrsdp_handle* h, int32_t buf, double* host, int64_t* count) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->get_buffer(buf, host, count); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_exchange_bytes(const clrsdp_handle* h, int64_t* bytes) {
+  if (!h || !bytes) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  *bytes = h->impl->exchange_bytes();
+  return CLRSDP_OK;
+}
+
+int32_t clrsdp_set_exchange(clrsdp_handle* h, clrsdp_exchange_fn fn, void* ctx, void* send_dev,
+                            void* recv_dev) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->set_exchange(fn, ctx, send_dev, recv_dev); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_set_stream(clrsdp_handle* h, void* stream) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->set_stream(stream); return CLRSDP_OK; })
+}
+
+void* clrsdp_get_stream(const clrsdp_handle* h) { return h ? h->impl->get_stream() : nullptr; }
+
+int32_t clrsdp_synchronize(clrsdp_handle* h) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->synchronize(); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_destroy(clrsdp_handle* h) {
+  if (!h) return CLRSDP_OK;
+  GUARD(h, { delete h; return CLRSDP_OK; })
+}
+
+}  // extern "C"

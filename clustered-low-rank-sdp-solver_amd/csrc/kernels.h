@@ -1,0 +1,931 @@
+// kernels.h -- gfx950 kernels of one interior-point iteration, templated on the word type T.
+//
+// Every kernel is *batched over a descriptor array*: one launch covers all (j,l) blocks (or
+// all clusters) of a phase, whatever their sizes -- the reference's `Threads.@threads for
+// (j,l) in jl_pairs` loops become the grid.  Layout in HBM: every matrix
+// column-major; block matrices of X, Y, ... concatenated in (j,l) order.
+//
+//   gemm_f64_mfma   C = alpha op(A) op(B) + beta Cin     fp64 matrix cores (v_mfma_f64_16x16x4)
+//   gemm_valu       same for multi-word T                VALU
+//   potrf_batched   in-place lower Cholesky              (spd_inv!/cho!/approx_lu! replacements)
+//   trsm_batched    B <- L^-1 B  or  L^-T B              (approx_solve_tril!/triu!)
+//   eigmin_batched  lambda_min of a symmetric block      (approx_eig_qr! replacement)
+//   schur_assemble  S_j from the pairings BX, BY         (MPMP.jl:1335-1409)
+//   + small elementwise / reduction kernels
+#pragma once
+#include <hip/hip_runtime.h>
+#include "mwfloat.h"
+
+namespace clrsdp {
+
+using mw::Num;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+template <class T> struct GemmDesc {
+  const T* A;
+  const T* B;
+  const T* Cin;
+  T* C;
+  int M, N, K, lda, ldb, ldcin, ldc;
+  int tn;     // tiles along N
+  int tile0;  // first tile index of this problem in the launch
+  int pad;
+};
+
+template <class T> struct MatDesc {
+  T* A;
+  int n, lda;
+};
+
+template <class T> struct TrsmDesc {
+  const T* L;
+  T* B;
+  int n, nrhs, ldl, ldb;
+  int tile0;  // first column-tile index of this problem in the launch
+  int pad;
+};
+
+// ------------------------------------------------------------------------------------------
+// GEMM, fp64 matrix cores.  64x64 output tile per 256-thread workgroup (4 waves as 2x2, each
+// wave 32x32 = 2x2 MFMA tiles of 16x16), K-step 16 staged through LDS.
+// v_mfma_f64_16x16x4_f64 lane maps (checked by tools/micro/f64_mfma_probe.hip):
+//   A: lane l holds A[i = l&15][k = l>>4];  B: B[k = l>>4][j = l&15];
+//   C/D: 4 results per lane, reg r at (row = (l>>4) + 4r, col = l&15).
+// LDS rows are padded to 80 doubles so the two 16-lane halves of a ds_read_b64 group land on
+// disjoint banks.
+// ------------------------------------------------------------------------------------------
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_f64_mfma(const GemmDesc<double>* __restrict__ descs,
+                                                     const int* __restrict__ t2d, double alpha,
+                                                     double beta) {
+  constexpr int BM = 64, BN = 64, BK = 16, LS = 80;
+  __shared__ double As[BK * LS];
+  __shared__ double Bs[BK * LS];
+  const GemmDesc<double> d = descs[t2d[blockIdx.x]];
+  const int t = blockIdx.x - d.tile0;
+  const int m0 = (t / d.tn) * BM, n0 = (t % d.tn) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const double* __restrict__ A = d.A;
+  const double* __restrict__ B = d.B;
+  d4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+
+  for (int k0 = 0; k0 < d.K; k0 += BK) {
+    // ---- stage A tile (rows m0..m0+63, k0..k0+15) as As[k][i]
+    if (!TA) {
+      const int k = tid >> 4, i = (tid & 15) * 4, gk = k0 + k;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gi = m0 + i + q;
+        As[k * LS + i + q] = (gi < d.M && gk < d.K) ? A[gi + (size_t)gk * d.lda] : 0.0;
+      }
+    } else {
+      const int i = tid >> 2, k = (tid & 3) * 4, gi = m0 + i;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gk = k0 + k + q;
+        As[(k + q) * LS + i] = (gi < d.M && gk < d.K) ? A[gk + (size_t)gi * d.lda] : 0.0;
+      }
+    }
+    // ---- stage B tile (k0..k0+15, cols n0..n0+63) as Bs[k][j]
+    if (!TB) {
+      const int j = tid >> 2, k = (tid & 3) * 4, gj = n0 + j;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gk = k0 + k + q;
+        Bs[(k + q) * LS + j] = (gj < d.N && gk < d.K) ? B[gk + (size_t)gj * d.ldb] : 0.0;
+      }
+    } else {
+      const int k = tid >> 4, j = (tid & 15) * 4, gk = k0 + k;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gj = n0 + j + q;
+        Bs[k * LS + j + q] = (gj < d.N && gk < d.K) ? B[gj + (size_t)gk * d.ldb] : 0.0;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const int kr = (kk + (lane >> 4)) * LS;
+      const double a0 = As[kr + wm * 32 + (lane & 15)];
+      const double a1 = As[kr + wm * 32 + 16 + (lane & 15)];
+      const double b0 = Bs[kr + wn * 32 + (lane & 15)];
+      const double b1 = Bs[kr + wn * 32 + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + mi * 16 + (lane >> 4) + 4 * r;
+        const int col = n0 + wn * 32 + ni * 16 + (lane & 15);
+        if (row < d.M && col < d.N) {
+          double v = alpha * acc[mi][ni][r];
+          if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];
+          d.C[row + (size_t)col * d.ldc] = v;
+        }
+      }
+}
+
+// ------------------------------------------------------------------------------------------
+// GEMM on the VALU for multi-word T: 32x32 tile, 256 threads, 2x2 outputs per thread.
+// ------------------------------------------------------------------------------------------
+template <class T, bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__ descs,
+                                                 const int* __restrict__ t2d, double alpha,
+                                                 double beta) {
+  constexpr int BM = 32, BN = 32, BK = 8;
+  __shared__ T As[BK][BM + 1];
+  __shared__ T Bs[BK][BN + 1];
+  const GemmDesc<T> d = descs[t2d[blockIdx.x]];
+  const int t = blockIdx.x - d.tile0;
+  const int m0 = (t / d.tn) * BM, n0 = (t % d.tn) * BN;
+  const int tid = threadIdx.x;
+  const int ti = (tid & 15) * 2, tj = (tid >> 4) * 2;
+  T acc[2][2];
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) acc[a][b] = T(0.0);
+  for (int k0 = 0; k0 < d.K; k0 += BK) {
+    {  // A tile 32 x 8 = 256 elements
+      const int i = TA ? (tid >> 3) : (tid & 31), k = TA ? (tid & 7) : (tid >> 5);
+      const int gi = m0 + i, gk = k0 + k;
+      T v = T(0.0);
+      if (gi < d.M && gk < d.K) v = TA ? d.A[gk + (size_t)gi * d.lda] : d.A[gi + (size_t)gk * d.lda];
+      As[k][i] = v;
+    }
+    {  // B tile 8 x 32
+      const int j = TB ? (tid & 31) : (tid >> 3), k = TB ? (tid >> 5) : (tid & 7);
+      const int gj = n0 + j, gk = k0 + k;
+      T v = T(0.0);
+      if (gj < d.N && gk < d.K) v = TB ? d.B[gj + (size_t)gk * d.ldb] : d.B[gk + (size_t)gj * d.ldb];
+      Bs[k][j] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < BK; ++k) {
+      const T a0 = As[k][ti], a1 = As[k][ti + 1], b0 = Bs[k][tj], b1 = Bs[k][tj + 1];
+      acc[0][0] += a0 * b0;
+      acc[0][1] += a0 * b1;
+      acc[1][0] += a1 * b0;
+      acc[1][1] += a1 * b1;
+    }
+    __syncthreads();
+  }
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      const int row = m0 + ti + a, col = n0 + tj + b;
+      if (row < d.M && col < d.N) {
+        T v = acc[a][b] * T(alpha);
+        if (beta != 0.0) v += d.Cin[row + (size_t)col * d.ldcin] * T(beta);
+        d.C[row + (size_t)col * d.ldc] = v;
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Block reductions (deterministic: fixed tree over a fixed thread->element map)
+// ------------------------------------------------------------------------------------------
+template <class T>
+__device__ T block_sum(T v, T* red) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (tid < s) red[tid] = red[tid] + red[tid + s];
+    __syncthreads();
+  }
+  T r = red[0];
+  __syncthreads();
+  return r;
+}
+template <class T>
+__device__ T block_max(T v, T* red) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (tid < s) red[tid] = (red[tid + s] > red[tid]) ? red[tid + s] : red[tid];
+    __syncthreads();
+  }
+  T r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------
+// Cholesky A = L L^T in place (lower triangle), one 256-thread workgroup per matrix, blocked
+// right-looking with NB-column panels; the panel lives in LDS, the trailing matrix in global
+// memory (L2-resident at the sizes of this solver).  info[b] = 0 on success, else the 1-based
+// column at which a non-positive pivot appeared (the reference's status 0 of spd_inv!/cho!).
+// ------------------------------------------------------------------------------------------
+template <class T, int NB>
+__global__ __launch_bounds__(256) void potrf_batched(const MatDesc<T>* __restrict__ descs,
+                                                     int* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* D = reinterpret_cast<T*>(smem_raw);  // NB x NB diagonal block (column-major)
+  T* P = D + NB * NB;                      // panel: P[q * pm + i]
+  __shared__ int fail;
+  const MatDesc<T> d = descs[blockIdx.x];
+  T* A = d.A;
+  const int n = d.n, lda = d.lda, tid = threadIdx.x;
+  if (tid == 0) fail = 0;
+  __syncthreads();
+  for (int k0 = 0; k0 < n; k0 += NB) {
+    const int nb = min(NB, n - k0);
+    for (int e = tid; e < nb * nb; e += blockDim.x) {
+      const int i = e % nb, j = e / nb;
+      D[i + j * NB] = A[(k0 + i) + (size_t)(k0 + j) * lda];
+    }
+    __syncthreads();
+    for (int j = 0; j < nb; ++j) {
+      if (tid == 0) {
+        const T djj = D[j + j * NB];
+        if (!(djj > T(0.0))) {
+          fail = k0 + j + 1;
+        } else {
+          D[j + j * NB] = Num<T>::sqrt_(djj);
+        }
+      }
+      __syncthreads();
+      if (fail) break;
+      const T piv = D[j + j * NB];
+      for (int i = j + 1 + tid; i < nb; i += blockDim.x) D[i + j * NB] = D[i + j * NB] / piv;
+      __syncthreads();
+      const int r = nb - j - 1;
+      for (int e = tid; e < r * r; e += blockDim.x) {
+        const int i = j + 1 + e % r, c = j + 1 + e / r;
+        if (i >= c) D[i + c * NB] = D[i + c * NB] - D[i + j * NB] * D[c + j * NB];
+      }
+      __syncthreads();
+    }
+    if (fail) break;
+    for (int e = tid; e < nb * nb; e += blockDim.x) {
+      const int i = e % nb, j = e / nb;
+      if (i >= j) A[(k0 + i) + (size_t)(k0 + j) * lda] = D[i + j * NB];
+    }
+    const int k1 = k0 + nb, pm = n - k1;
+    if (pm <= 0) break;
+    // panel L21 = A21 L11^-T, one row per thread
+    for (int i = tid; i < pm; i += blockDim.x) {
+      T row[NB];
+      for (int q = 0; q < nb; ++q) {
+        T x = A[(k1 + i) + (size_t)(k0 + q) * lda];
+        for (int p = 0; p < q; ++p) x = x - row[p] * D[q + p * NB];
+        x = x / D[q + q * NB];
+        row[q] = x;
+        P[q * pm + i] = x;
+        A[(k1 + i) + (size_t)(k0 + q) * lda] = x;
+      }
+    }
+    __syncthreads();
+    // trailing update A22 -= L21 L21^T (lower triangle)
+    for (int e = tid; e < pm * pm; e += blockDim.x) {
+      const int i = e % pm, j = e / pm;
+      if (i >= j) {
+        T s = T(0.0);
+        for (int q = 0; q < nb; ++q) s += P[q * pm + i] * P[q * pm + j];
+        A[(k1 + i) + (size_t)(k1 + j) * lda] = A[(k1 + i) + (size_t)(k1 + j) * lda] - s;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) info[blockIdx.x] = fail;
+}
+
+// ------------------------------------------------------------------------------------------
+// Triangular solves with L from potrf (lower, non-unit), in place on B:
+//   TRANS = false:  B <- L^-1 B     (forward substitution)
+//   TRANS = true :  B <- L^-T B     (backward substitution)
+// One workgroup per (matrix, NC-column tile of B); NB-row blocks; L panel staged in LDS.
+// ------------------------------------------------------------------------------------------
+template <class T, bool TRANS, int NB, int NC>
+__global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restrict__ descs,
+                                                    const int* __restrict__ t2d) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* D = reinterpret_cast<T*>(smem_raw);  // NB x NB diagonal block of L (column-major)
+  T* Xs = D + NB * NB;                     // NB x NC solved rows
+  T* P = Xs + NB * NC;                     // panel NB x n
+  const TrsmDesc<T> d = descs[t2d[blockIdx.x]];
+  const int c0 = (blockIdx.x - d.tile0) * NC;
+  const int nc = min(NC, d.nrhs - c0);
+  const int n = d.n, tid = threadIdx.x;
+  const T* L = d.L;
+  T* B = d.B + (size_t)c0 * d.ldb;
+  const int nblk = (n + NB - 1) / NB;
+  for (int bi = 0; bi < nblk; ++bi) {
+    const int i0 = TRANS ? (nblk - 1 - bi) * NB : bi * NB;
+    const int nb = min(NB, n - i0);
+    for (int e = tid; e < nb * nb; e += blockDim.x) {
+      const int i = e % nb, j = e / nb;
+      D[i + j * NB] = L[(i0 + i) + (size_t)(i0 + j) * d.ldl];
+    }
+    // panel of the rows still to be updated
+    const int pr0 = TRANS ? 0 : i0 + nb;
+    const int pm = TRANS ? i0 : n - i0 - nb;
+    for (int e = tid; e < nb * pm; e += blockDim.x) {
+      const int i = e % pm, q = e / pm;
+      // non-trans: P[q][i] = L[pr0 + i, i0 + q];  trans: P[q][i] = L[i0 + q, i]
+      P[q * pm + i] = TRANS ? L[(i0 + q) + (size_t)i * d.ldl] : L[(pr0 + i) + (size_t)(i0 + q) * d.ldl];
+    }
+    __syncthreads();
+    if (tid < nc) {
+      T x[NB];
+      if (!TRANS) {
+        for (int r = 0; r < nb; ++r) {
+          T v = B[(i0 + r) + (size_t)tid * d.ldb];
+          for (int q = 0; q < r; ++q) v = v - D[r + q * NB] * x[q];
+          x[r] = v / D[r + r * NB];
+        }
+      } else {
+        for (int r = nb - 1; r >= 0; --r) {
+          T v = B[(i0 + r) + (size_t)tid * d.ldb];
+          for (int q = r + 1; q < nb; ++q) v = v - D[q + r * NB] * x[q];
+          x[r] = v / D[r + r * NB];
+        }
+      }
+      for (int r = 0; r < nb; ++r) {
+        B[(i0 + r) + (size_t)tid * d.ldb] = x[r];
+        Xs[r * NC + tid] = x[r];
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < pm * nc; e += blockDim.x) {
+      const int i = e % pm, c = e / pm;
+      T s = T(0.0);
+      for (int q = 0; q < nb; ++q) s += P[q * pm + i] * Xs[q * NC + c];
+      T* bp = B + (pr0 + i) + (size_t)c * d.ldb;
+      *bp = *bp - s;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Smallest eigenvalue of a symmetric matrix (destroys it): symmetrise, Householder
+// tridiagonalisation (full symmetric storage, one workgroup per matrix), then Sturm-count
+// multisection by one wave (64 shifts per round).  Replaces the complex QR eigen-solver of
+// compute_step_length (MPMP.jl:1857-1870), which returns the same spectrum for the
+// (mathematically symmetric) L^-1 dM L^-T.
+// ------------------------------------------------------------------------------------------
+template <class T>
+__device__ int sturm_count(const T* dg, const T* e2, int n, T sigma) {
+  int cnt = 0;
+  T q = dg[0] - sigma;
+  if (q < T(0.0)) ++cnt;
+  for (int i = 1; i < n; ++i) {
+    if (q == T(0.0)) q = T(1e-300);
+    q = dg[i] - sigma - e2[i - 1] / q;
+    if (q < T(0.0)) ++cnt;
+  }
+  return cnt;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void eigmin_batched(const MatDesc<T>* __restrict__ descs,
+                                                      T* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const MatDesc<T> d = descs[blockIdx.x];
+  const int n = d.n, lda = d.lda, tid = threadIdx.x;
+  T* v = reinterpret_cast<T*>(smem_raw);  // n
+  T* p = v + n;                            // n
+  T* dg = p + n;                           // n   diagonal
+  T* e2 = dg + n;                          // n   squared off-diagonal
+  T* red = e2 + n;                         // blockDim.x
+  T* A = d.A;
+  // symmetrise: A = (A + A^T) / 2
+  for (int e = tid; e < n * n; e += blockDim.x) {
+    const int i = e % n, j = e / n;
+    if (i > j) {
+      const T s = (A[i + (size_t)j * lda] + A[j + (size_t)i * lda]) * T(0.5);
+      A[i + (size_t)j * lda] = s;
+      A[j + (size_t)i * lda] = s;
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k + 2 < n; ++k) {
+    const int m = n - k - 1;
+    T* Ak = A + (k + 1) + (size_t)(k + 1) * lda;  // trailing m x m
+    for (int i = tid; i < m; i += blockDim.x) v[i] = A[(k + 1 + i) + (size_t)k * lda];
+    __syncthreads();
+    T s = T(0.0);
+    for (int i = tid; i < m; i += blockDim.x) s += v[i] * v[i];
+    s = block_sum(s, red);
+    const T x0 = v[0];
+    const T nrm = Num<T>::sqrt_(s);
+    const T alpha = (x0 > T(0.0)) ? -nrm : nrm;
+    if (tid == 0) dg[k] = A[k + (size_t)k * lda];
+    T tail = s - x0 * x0;
+    if (!(tail > T(0.0))) {  // already tridiagonal in this column
+      if (tid == 0) e2[k] = x0 * x0;
+      __syncthreads();
+      continue;
+    }
+    if (tid == 0) {
+      e2[k] = alpha * alpha;
+      v[0] = x0 - alpha;
+    }
+    __syncthreads();
+    // v^T v = tail + (x0 - alpha)^2
+    const T v0 = x0 - alpha;
+    const T beta = T(2.0) / (tail + v0 * v0);
+    // p = beta A' v
+    for (int i = tid; i < m; i += blockDim.x) {
+      T acc = T(0.0);
+      for (int j = 0; j < m; ++j) acc += Ak[i + (size_t)j * lda] * v[j];
+      p[i] = acc * beta;
+    }
+    __syncthreads();
+    T pv = T(0.0);
+    for (int i = tid; i < m; i += blockDim.x) pv += p[i] * v[i];
+    pv = block_sum(pv, red);
+    const T Kc = beta * pv * T(0.5);
+    for (int i = tid; i < m; i += blockDim.x) p[i] = p[i] - Kc * v[i];
+    __syncthreads();
+    for (int e = tid; e < m * m; e += blockDim.x) {
+      const int i = e % m, j = e / m;
+      Ak[i + (size_t)j * lda] = Ak[i + (size_t)j * lda] - (v[i] * p[j] + p[i] * v[j]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (n >= 2) {
+      dg[n - 2] = A[(n - 2) + (size_t)(n - 2) * lda];
+      dg[n - 1] = A[(n - 1) + (size_t)(n - 1) * lda];
+      const T e = A[(n - 1) + (size_t)(n - 2) * lda];
+      e2[n - 2] = e * e;
+    } else {
+      dg[0] = A[0];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    // Gershgorin interval
+    T lo = T(0.0), hi = T(0.0);
+    if (tid == 0) {
+      for (int i = 0; i < n; ++i) {
+        T r = T(0.0);
+        if (i > 0) r += Num<T>::sqrt_(e2[i - 1]);
+        if (i + 1 < n) r += Num<T>::sqrt_(e2[i]);
+        const T a = dg[i] - r, b = dg[i] + r;
+        if (i == 0 || a < lo) lo = a;
+        if (i == 0 || b > hi) hi = b;
+      }
+      red[0] = lo;
+      red[1] = hi;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    lo = red[0];
+    hi = red[1];
+    const T span = hi - lo;
+    lo = lo - span * T(1e-3) - T(1e-300);
+    hi = hi + span * T(1e-3) + T(1e-300);
+    const int rounds = Num<T>::BITS / 6 + 3;
+    for (int it = 0; it < rounds; ++it) {
+      const T width = hi - lo;
+      const T sigma = lo + width * T((double)(tid + 1) / 65.0);
+      const int c = sturm_count(dg, e2, n, sigma);
+      const unsigned long long mask = __ballot(c >= 1);
+      T nlo = lo, nhi = hi;
+      if (mask == 0ull) {
+        nlo = lo + width * T(64.0 / 65.0);
+      } else {
+        const int f = __ffsll((long long)mask) - 1;
+        nhi = lo + width * T((double)(f + 1) / 65.0);
+        if (f > 0) nlo = lo + width * T((double)f / 65.0);
+      }
+      lo = nlo;
+      hi = nhi;
+    }
+    if (tid == 0) out[blockIdx.x] = (lo + hi) * T(0.5);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Schur complement assembly from the pairings (MPMP.jl:1335-1409).  One thread per upper
+// entry (ver <= hor) of one cluster; sums the l blocks and rank pairs in the reference's order
+// and writes both triangles.
+//   BX_b, BY_b:  (m K) x (m K) pairings of block b (column-major, ld m K)
+//   S_c: D x D.   tuple t(r,s,k) = k + (s + r(r+1)/2) N
+// ------------------------------------------------------------------------------------------
+struct SchurClusterDesc {
+  int m, N, D;
+  int blk0, nblk;    // local blocks of this cluster
+  int pair0;         // first upper-pair index of this cluster in the launch
+  long long S_off;   // offset of S_c in the S arena
+};
+struct SchurBlockDesc {
+  long long bx_off;   // offset of BX_b / BY_b in the pairing arenas
+  int K;              // vectors of this block
+  int rs_off;         // offset of rank_sums of this block in the int arena (N + 1 entries)
+  int lam_off;        // offset of lambda_b
+  int pad;
+};
+
+template <class T>
+__global__ __launch_bounds__(256) void schur_assemble(const SchurClusterDesc* __restrict__ cd,
+                                                      int ncl, const SchurBlockDesc* __restrict__ bd,
+                                                      const int* __restrict__ rank_sums,
+                                                      const T* __restrict__ lam,
+                                                      const T* __restrict__ BX,
+                                                      const T* __restrict__ BY,
+                                                      T* __restrict__ S, long long npairs) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= npairs) return;
+  int lo = 0, hi = ncl - 1;  // find the cluster: last c with pair0 <= g
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (cd[mid].pair0 <= g) lo = mid; else hi = mid - 1;
+  }
+  const SchurClusterDesc c = cd[lo];
+  long long u = g - c.pair0;  // index into the upper triangle, column by column
+  // hor = column h, ver = row v <= h :  u = h(h+1)/2 + v
+  int h = (int)((sqrt(8.0 * (double)u + 1.0) - 1.0) * 0.5);
+  while ((long long)h * (h + 1) / 2 > u) --h;
+  while ((long long)(h + 1) * (h + 2) / 2 <= u) ++h;
+  const int v = (int)(u - (long long)h * (h + 1) / 2);
+  const int N = c.N;
+  // decode tuples: hor = (r1, s1, k1), ver = (r2, s2, k2)
+  const int k1 = h % N, rs1 = h / N, k2 = v % N, rs2 = v / N;
+  int r1 = 0;
+  while ((r1 + 1) * (r1 + 2) / 2 <= rs1) ++r1;
+  const int s1 = rs1 - r1 * (r1 + 1) / 2;
+  int r2 = 0;
+  while ((r2 + 1) * (r2 + 2) / 2 <= rs2) ++r2;
+  const int s2 = rs2 - r2 * (r2 + 1) / 2;
+  T tot = T(0.0);
+  for (int b = c.blk0; b < c.blk0 + c.nblk; ++b) {
+    const SchurBlockDesc B = bd[b];
+    const int K = B.K, ld = c.m * K;
+    const int* rsum = rank_sums + B.rs_off;
+    const T* bx = BX + B.bx_off;
+    const T* by = BY + B.bx_off;
+    const T* lb = lam + B.lam_off;
+    for (int p1 = rsum[k1]; p1 < rsum[k1 + 1]; ++p1) {
+      for (int p2 = rsum[k2]; p2 < rsum[k2 + 1]; ++p2) {
+        const int r1s = p1 + K * r1, s1s = p1 + K * s1, r2s = p2 + K * r2, s2s = p2 + K * s2;
+        T t = bx[s1s + (size_t)r2s * ld] * by[s2s + (size_t)r1s * ld];
+        t += bx[r1s + (size_t)r2s * ld] * by[s2s + (size_t)s1s * ld];
+        t += bx[s1s + (size_t)s2s * ld] * by[r2s + (size_t)r1s * ld];
+        t += bx[r1s + (size_t)s2s * ld] * by[r2s + (size_t)s1s * ld];
+        tot += t * lb[p1] * lb[p2] * T(0.25);
+      }
+    }
+  }
+  T* Sc = S + c.S_off;
+  Sc[v + (size_t)h * c.D] = tot;
+  Sc[h + (size_t)v * c.D] = tot;
+}
+
+// ------------------------------------------------------------------------------------------
+// small batched elementwise kernels over block matrices (one workgroup per block)
+// ------------------------------------------------------------------------------------------
+struct BlkDesc {
+  long long off;  // offset in the block arena
+  int n;
+  int pad;
+};
+
+// out = a*X + b*Y (+ s*I with s = *sc if sc != nullptr)
+template <class T>
+__global__ void blk_axpby(const BlkDesc* __restrict__ bd, T* out, const T* X, const T* Y, double a,
+                          double b, const T* sc, double sc_mult) {
+  const BlkDesc B = bd[blockIdx.x];
+  const int nn = B.n * B.n;
+  const T s = sc ? (*sc) * T(sc_mult) : T(0.0);
+  for (int e = threadIdx.x; e < nn; e += blockDim.x) {
+    T v = T(0.0);
+    if (a != 0.0) v += X[B.off + e] * T(a);
+    if (b != 0.0) v += Y[B.off + e] * T(b);
+    if (sc && (e % B.n) == (e / B.n)) v += s;
+    out[B.off + e] = v;
+  }
+}
+
+// X += alpha * dX with alpha = *sc
+template <class T>
+__global__ void blk_axpy_dev(const BlkDesc* __restrict__ bd, T* X, const T* dX, const T* sc) {
+  const BlkDesc B = bd[blockIdx.x];
+  const int nn = B.n * B.n;
+  const T a = *sc;
+  for (int e = threadIdx.x; e < nn; e += blockDim.x) X[B.off + e] = X[B.off + e] + a * dX[B.off + e];
+}
+
+// identity
+template <class T>
+__global__ void blk_identity(const BlkDesc* __restrict__ bd, T* out) {
+  const BlkDesc B = bd[blockIdx.x];
+  const int nn = B.n * B.n;
+  for (int e = threadIdx.x; e < nn; e += blockDim.x)
+    out[B.off + e] = ((e % B.n) == (e / B.n)) ? T(1.0) : T(0.0);
+}
+
+// out = (Z + Z^T)/2   (mode 0);  out = upper triangle mirrored (mode 1, Symmetric(.)) ;
+// out = Z^T (mode 2)
+template <class T>
+__global__ void blk_sym(const BlkDesc* __restrict__ bd, T* out, const T* Z, int mode) {
+  const BlkDesc B = bd[blockIdx.x];
+  const int n = B.n;
+  const T* z = Z + B.off;
+  T* o = out + B.off;
+  if (mode == 2) {
+    for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+      const int i = e % n, j = e / n;
+      o[i + (size_t)j * n] = z[j + (size_t)i * n];
+    }
+    return;
+  }
+  // in-place safe: each unordered pair handled by one thread
+  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+    const int i = e % n, j = e / n;
+    if (i > j) {
+      T v;
+      if (mode == 0) v = (z[i + (size_t)j * n] + z[j + (size_t)i * n]) * T(0.5);
+      else v = z[j + (size_t)i * n];
+      o[i + (size_t)j * n] = v;
+      o[j + (size_t)i * n] = v;
+    } else if (i == j) {
+      o[i + (size_t)j * n] = z[i + (size_t)j * n];
+    }
+  }
+}
+
+// per-block reductions: op 0 = sum X.*Y, op 1 = sum (X+dX).*(Y+dY), op 2 = max |X|
+template <class T>
+__global__ __launch_bounds__(256) void blk_reduce(const BlkDesc* __restrict__ bd, const T* X,
+                                                  const T* Y, const T* dX, const T* dY, int op,
+                                                  T* __restrict__ partial) {
+  __shared__ T red[256];
+  const BlkDesc B = bd[blockIdx.x];
+  const int nn = B.n * B.n;
+  T acc = T(0.0);
+  for (int e = threadIdx.x; e < nn; e += blockDim.x) {
+    const size_t o = B.off + e;
+    if (op == 0) acc += X[o] * Y[o];
+    else if (op == 1) acc += (X[o] + dX[o]) * (Y[o] + dY[o]);
+    else {
+      const T a = Num<T>::abs_(X[o]);
+      if (a > acc) acc = a;
+    }
+  }
+  T r = (op == 2) ? block_max(acc, red) : block_sum(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = r;
+}
+
+// vector reductions over [0, n): op 0 = sum a.*b, op 2 = max |a|; single workgroup
+template <class T>
+__global__ __launch_bounds__(256) void vec_reduce(const T* a, const T* b, long long n, int op,
+                                                  T* __restrict__ out) {
+  __shared__ T red[256];
+  T acc = T(0.0);
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    if (op == 0) acc += a[e] * b[e];
+    else {
+      const T v = Num<T>::abs_(a[e]);
+      if (v > acc) acc = v;
+    }
+  }
+  T r = (op == 2) ? block_max(acc, red) : block_sum(acc, red);
+  if (threadIdx.x == 0) *out = r;
+}
+
+// sum or max of `cnt` values spaced `stride` apart (fixed order), single thread -> *out
+template <class T>
+__global__ void ordered_reduce(const T* in, int cnt, long long stride, int op, T* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  T acc = in[0];
+  for (int i = 1; i < cnt; ++i) {
+    const T v = in[(size_t)i * stride];
+    if (op == 0) acc += v;
+    else if (op == 2) acc = (v > acc) ? v : acc;
+    else acc = (v < acc) ? v : acc;  // op 3: min
+  }
+  *out = acc;
+}
+
+// out[e] = sum_{i<cnt} in[i*stride + e]  (fixed order), e < n
+template <class T>
+__global__ void slab_sum(const T* in, int cnt, long long stride, long long n, T* out) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  T acc = in[e];
+  for (int i = 1; i < cnt; ++i) acc += in[(size_t)i * stride + e];
+  out[e] = acc;
+}
+
+// vector: out = a*x + b*y (+ c*z) over n
+template <class T>
+__global__ void vec_lin(T* out, const T* x, double a, const T* y, double b, const T* z, double c,
+                        long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  T v = x[e] * T(a);
+  if (y) v += y[e] * T(b);
+  if (z) v += z[e] * T(c);
+  out[e] = v;
+}
+
+// out[0..n) = v
+template <class T>
+__global__ void vec_fill(T* out, double v, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) out[e] = T(v);
+}
+
+// x += (*sc) * dx
+template <class T>
+__global__ void vec_axpy_dev(T* x, const T* dx, const T* sc, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  x[e] = x[e] + (*sc) * dx[e];
+}
+
+// ------------------------------------------------------------------------------------------
+// Low-rank operators
+// ------------------------------------------------------------------------------------------
+// Per (block, r>=s) pair: column dots val[p] = sum_i V[i,p] U[i,p]  (U = Z[r,s] V), one wave
+// per column (trace_A, MPMP.jl:1558-1560)
+struct PairDesc {
+  long long u_off;    // U_{b,rs} (delta x K, ld delta)
+  long long v_off;    // V_b
+  long long val_off;  // val_{b,rs} (K)
+  int delta, K;
+};
+template <class T>
+__global__ __launch_bounds__(256) void colsum_dot(const PairDesc* __restrict__ pd, const T* U,
+                                                  const T* V, T* val) {
+  const PairDesc P = pd[blockIdx.y];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = blockIdx.x * 4 + wave;
+  if (col >= P.K) return;
+  const T* u = U + P.u_off + (size_t)col * P.delta;
+  const T* v = V + P.v_off + (size_t)col * P.delta;
+  T acc = T(0.0);
+  for (int i = lane; i < P.delta; i += 64) acc += u[i] * v[i];
+  // fixed butterfly over the wave
+  for (int s = 32; s > 0; s >>= 1) {
+    if constexpr (sizeof(T) == 8) {
+      acc += __shfl_xor(acc, s);
+    } else {
+      T o;
+      double* od = reinterpret_cast<double*>(&o);
+      const double* ad = reinterpret_cast<const double*>(&acc);
+#pragma unroll
+      for (int q = 0; q < (int)(sizeof(T) / 8); ++q) od[q] = __shfl_xor(ad[q], s);
+      acc += o;
+    }
+  }
+  if (lane == 0) val[P.val_off + col] = acc;
+}
+
+// Per (block, r>=s): Vs[:,p] = V[:,p] * w_p with w_p = a[xoff + tuple(r,s,k(p))] * lambda_p * scale
+// (compute_weighted_A!, MPMP.jl:1654)
+struct ScaleDesc {
+  long long v_off, vs_off;
+  int delta, K;
+  int ks_off;     // sample index of each column
+  int lam_off;
+  int a_off;      // local x offset of the cluster + (s + r(r+1)/2) N
+  int pad;
+  double scale;   // 1/2 on off-diagonal (r != s) blocks, MPMP.jl:1661-1663
+};
+template <class T>
+__global__ void scale_cols(const ScaleDesc* __restrict__ sd, const T* V, const T* lam,
+                           const int* ksamp, const T* a, T* Vs) {
+  const ScaleDesc S = sd[blockIdx.y];
+  const long long tot = (long long)S.delta * S.K;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int p = (int)(e / S.delta);
+    const T w = a[S.a_off + ksamp[S.ks_off + p]] * lam[S.lam_off + p] * T(S.scale);
+    Vs[S.vs_off + e] = V[S.v_off + e] * w;
+  }
+}
+
+// Tuple aggregation (trace_A's sample sum, MPMP.jl:1563-1578 / 1592-1615):
+//   out[t] = c_in * in[t] + c_in2 * in2[t] + c_agg * sum_{l} sum_{p in k} lambda_p val_{b,rs}[p]
+// one thread per local tuple t = xoff_c + (s + r(r+1)/2) N + k
+struct TupleDesc {
+  int x_off;      // local x offset of this cluster
+  int N, m;
+  int blk0, nblk; // local blocks
+  int t0;         // first local tuple index (== x_off)
+};
+struct TupleBlock {
+  long long val_off;   // val of (b, rs=0); rs stride = K
+  int K;
+  int rs_off;          // rank_sums offset (N+1 entries)
+  int lam_off;
+  int pad;
+};
+template <class T>
+__global__ void tuple_aggregate(const TupleDesc* __restrict__ td, int ncl,
+                                const TupleBlock* __restrict__ tb, const int* rank_sums,
+                                const T* lam, const T* val, const T* in, double c_in,
+                                const T* in2, double c_in2, double c_agg, T* out, long long ntup) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ntup) return;
+  int lo = 0, hi = ncl - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (td[mid].t0 <= g) lo = mid; else hi = mid - 1;
+  }
+  const TupleDesc C = td[lo];
+  const int loc = (int)(g - C.t0);
+  const int k = loc % C.N, rs = loc / C.N;
+  T agg = T(0.0);
+  for (int b = C.blk0; b < C.blk0 + C.nblk; ++b) {
+    const TupleBlock B = tb[b];
+    const int* rsum = rank_sums + B.rs_off;
+    const T* vv = val + B.val_off + (size_t)rs * B.K;
+    for (int p = rsum[k]; p < rsum[k + 1]; ++p) agg += lam[B.lam_off + p] * vv[p];
+  }
+  T o = agg * T(c_agg);
+  if (in) o += in[g] * T(c_in);
+  if (in2) o += in2[g] * T(c_in2);
+  out[g] = o;
+}
+
+// A_Y extraction: val_{b,rs}[p] = BY_b[r K + p, s K + p]   (MPMP.jl:1320-1330)
+struct AYDesc {
+  long long by_off, ay_off;
+  int K, m;
+};
+template <class T>
+__global__ void extract_AY(const AYDesc* __restrict__ ad, const T* BY, T* AY) {
+  const AYDesc A = ad[blockIdx.x];
+  const int nrs = A.m * (A.m + 1) / 2;
+  const int ld = A.m * A.K;
+  for (int e = threadIdx.x; e < nrs * A.K; e += blockDim.x) {
+    const int p = e % A.K, rs = e / A.K;
+    int r = 0;
+    while ((r + 1) * (r + 2) / 2 <= rs) ++r;
+    const int s = rs - r * (r + 1) / 2;
+    AY[A.ay_off + e] = BY[A.by_off + (r * A.K + p) + (size_t)(s * A.K + p) * ld];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// scalar logic of the driver loop, on the device (MPMP.jl:755-756, 832-837, 871-874, 1893-1897)
+// ------------------------------------------------------------------------------------------
+enum { SC_MU = 0, SC_MU_P, SC_R, SC_BETA, SC_BETA_C, SC_MU_C, SC_ALPHA_P, SC_ALPHA_D, SC_MINEIG_X,
+       SC_MINEIG_Y, SC_POBJ, SC_DOBJ, SC_ERR_PMAT, SC_ERR_PVEC, SC_ERR_DVEC, SC_DOT_XY, SC_DOT_XDY,
+       SC_DOT_CX, SC_DOT_BY, SC_DOT_CY, SC_TMP0, SC_TMP1, SC_TMP2, SC_TMP3, SC_COUNT };
+
+template <class T> struct ScalarParams {
+  T beta_inf, beta_feas, gamma, b0;
+  double dim;
+  int pd_feas;
+};
+
+template <class T>
+__global__ void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
+  if (threadIdx.x != 0) return;
+  const T dim = T(p.dim);
+  if (which == 0) {  // mu, mu_p
+    sc[SC_MU] = sc[SC_DOT_XY] / dim;
+    sc[SC_MU_P] = p.pd_feas ? T(0.0) : p.beta_inf * sc[SC_MU];
+  } else if (which == 1) {  // r, beta, beta_c, mu_c
+    const T r = sc[SC_DOT_XDY] / (sc[SC_MU] * dim);
+    const T beta = (r < T(1.0)) ? r * r : r;
+    T bc;
+    if (p.pd_feas) {
+      bc = (p.beta_feas > beta) ? p.beta_feas : beta;
+      if (bc > T(1.0)) bc = T(1.0);
+    } else {
+      bc = (p.beta_inf > beta) ? p.beta_inf : beta;
+    }
+    sc[SC_R] = r;
+    sc[SC_BETA] = beta;
+    sc[SC_BETA_C] = bc;
+    sc[SC_MU_C] = bc * sc[SC_MU];
+  } else if (which == 2) {  // step lengths
+    const T g = p.gamma;
+    T ap = (sc[SC_MINEIG_X] > -g) ? T(1.0) : -g / sc[SC_MINEIG_X];
+    T ad = (sc[SC_MINEIG_Y] > -g) ? T(1.0) : -g / sc[SC_MINEIG_Y];
+    if (p.pd_feas) {
+      const T mn = (ad < ap) ? ad : ap;
+      ap = mn;
+      ad = mn;
+    }
+    sc[SC_ALPHA_P] = ap;
+    sc[SC_ALPHA_D] = ad;
+  } else if (which == 3) {  // objectives
+    sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;
+    sc[SC_DOBJ] = sc[SC_DOT_CY] + sc[SC_DOT_BY] + p.b0;
+  }
+}
+
+}  // namespace clrsdp

@@ -1,0 +1,311 @@
+"""Host mirror of ``solverank1sdp`` (MPMP.jl:595-1025) driving the MI355X library.
+
+The loop control, the termination test, the printed table and the returned 11-tuple follow
+the reference exactly; every loop body (MPMP.jl:755-887) is one ``clrsdp_iterate`` call that
+runs entirely on the GPU.  Numbers cross the boundary as planar limbs (``precision_words`` 1 =
+fp64, 2 = double-double).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .blockinfo import BlockInfo
+from .instance import Flat, blocks_to_flat, concat_colmajor, flat_to_blocks, flatten, to_planes
+
+DEFAULTS = dict(beta_infeasible="0.3", beta_feasible="0.1", gamma="0.7", omega_p="1e10",
+                omega_d="1e10", duality_gap_threshold="1e-15", primal_error_threshold="1e-30",
+                dual_error_threshold="1e-30")
+
+
+def limbs(v, words=4):
+    """A scalar (float, str, mpmath.mpf) as `words` limbs of an unevaluated sum."""
+    import mpmath
+    with mpmath.workprec(320):
+        r = mpmath.mpf(v) if not isinstance(v, float) else mpmath.mpf(v)
+        out = []
+        for _ in range(words):
+            h = float(r)
+            out.append(h)
+            r = r - h
+    return out
+
+
+def make_params(beta_infeasible, beta_feasible, gamma, b0) -> _lib.Params:
+    p = _lib.Params()
+    for name, v in (("beta_infeasible", beta_infeasible), ("beta_feasible", beta_feasible),
+                    ("gamma", gamma), ("b0", b0)):
+        arr = getattr(p, name)
+        for i, x in enumerate(limbs(v)):
+            arr[i] = x
+    return p
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_lib.P_f64)
+
+
+class DeviceSolver:
+    """One handle of libclrsdp: constraint data resident on one GPU (the clusters of this rank)."""
+
+    def __init__(self, constraints: Sequence, b, bi: BlockInfo, precision_words: int = 1,
+                 C_blocks=None, device: int = 0, rank: int = 0, world: int = 1,
+                 owned: Optional[Sequence[int]] = None, timing: bool = False):
+        self.L = _lib.lib()
+        self.bi = bi
+        self.w = int(precision_words)
+        self.rank, self.world = rank, world
+        flat = flatten(constraints, bi)
+        self.flat = flat
+        self._keep = []
+        desc = _lib.Desc()
+        desc.J = bi.J
+        desc.n_y = bi.n_y
+        for name in ("m", "L", "n_samples", "delta", "ranks"):
+            arr = np.ascontiguousarray(getattr(flat, name), dtype=np.int64)
+            self._keep.append(arr)
+            setattr(desc, name, arr.ctypes.data_as(_lib.P_i64))
+        cfg = _lib.Config()
+        cfg.precision_words = self.w
+        cfg.device = device
+        cfg.rank = rank
+        cfg.world_size = world
+        if owned is not None:
+            own = np.ascontiguousarray(sorted(owned), dtype=np.int32)
+            self._keep.append(own)
+            cfg.owned = own.ctypes.data_as(_lib.P_i32)
+            cfg.n_owned = len(own)
+        cfg.timing = 1 if timing else 0
+        h = C.c_void_p()
+        _lib.check(self.L.clrsdp_create(C.byref(desc), C.byref(cfg), C.byref(h)))
+        self.h = h
+        self.owned = sorted(owned) if owned is not None else list(range(bi.J))
+        w = self.w
+        Vp = to_planes(concat_colmajor(flat.V), w)
+        lp = to_planes(np.concatenate(flat.lam), w)
+        Bp = to_planes(concat_colmajor(flat.B), w)
+        cp = to_planes(np.concatenate(flat.c), w)
+        bp = to_planes(np.asarray(b), w)
+        Cp = to_planes(blocks_to_flat(C_blocks), w) if C_blocks is not None else None
+        self.check(self.L.clrsdp_upload_constraints(
+            self.h, _ptr(Vp), _ptr(lp), _ptr(Bp), _ptr(cp), _ptr(bp),
+            _ptr(Cp) if Cp is not None else None))
+        self.n_x = sum(bi.dim_S)
+        self.n_blk = sum(n * n for bj in bi.Y_blocksizes for n in bj)
+
+    # ------------------------------------------------------------------ plumbing
+    def check(self, rc):
+        _lib.check(rc, self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.clrsdp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _from_planes(self, planes: np.ndarray, n: int, exact=False):
+        if self.w == 1 or not exact:
+            return planes[:n].copy()
+        import mpmath
+        out = np.empty(n, dtype=object)
+        P = planes.reshape(self.w, n)
+        for i in range(n):
+            s = mpmath.mpf(0)
+            for q in range(self.w):
+                s += mpmath.mpf(P[q, i])
+            out[i] = s
+        return out
+
+    # ------------------------------------------------------------------ state
+    def set_state(self, x, X, y, Y):
+        w = self.w
+        xp = to_planes(np.asarray(x), w)
+        Xp = to_planes(blocks_to_flat(X), w)
+        yp = to_planes(np.asarray(y), w)
+        Yp = to_planes(blocks_to_flat(Y), w)
+        self.check(self.L.clrsdp_set_state(self.h, _ptr(xp), _ptr(Xp), _ptr(yp), _ptr(Yp)))
+
+    def get_state(self, exact=False):
+        w = self.w
+        xp = np.zeros(w * self.n_x)
+        Xp = np.zeros(w * self.n_blk)
+        yp = np.zeros(w * self.bi.n_y)
+        Yp = np.zeros(w * self.n_blk)
+        self.check(self.L.clrsdp_get_state(self.h, _ptr(xp), _ptr(Xp), _ptr(yp), _ptr(Yp)))
+        x = self._from_planes(xp, self.n_x, exact)
+        y = self._from_planes(yp, self.bi.n_y, exact)
+        X = flat_to_blocks(self._from_planes(Xp, self.n_blk, exact), self.bi)
+        Y = flat_to_blocks(self._from_planes(Yp, self.n_blk, exact), self.bi)
+        return x, X, y, Y
+
+    def buffer(self, buf: int, exact=False) -> np.ndarray:
+        cnt = C.c_int64()
+        self.check(self.L.clrsdp_get_buffer(self.h, buf, None, C.byref(cnt)))
+        n = cnt.value
+        out = np.zeros(self.w * max(n, 1))
+        self.check(self.L.clrsdp_get_buffer(self.h, buf, _ptr(out), C.byref(cnt)))
+        return self._from_planes(out, n, exact)
+
+    def scalar(self, name: str, exact=False):
+        return self.buffer(_lib.BUF_SCALARS, exact)[_lib.SC[name]]
+
+    # ------------------------------------------------------------------ iteration
+    def initial_residuals(self, prm: _lib.Params) -> _lib.IterStats:
+        st = _lib.IterStats()
+        self.check(self.L.clrsdp_initial_residuals(self.h, C.byref(prm), C.byref(st)))
+        return st
+
+    def iterate(self, prm: _lib.Params, pd_feas: bool) -> _lib.IterStats:
+        st = _lib.IterStats()
+        self.check(self.L.clrsdp_iterate(self.h, C.byref(prm), 1 if pd_feas else 0, C.byref(st)))
+        return st
+
+    def run_stage(self, stage: int, prm: _lib.Params, pd_feas: bool):
+        self.check(self.L.clrsdp_run_stage(self.h, stage, C.byref(prm), 1 if pd_feas else 0))
+
+    def synchronize(self):
+        self.check(self.L.clrsdp_synchronize(self.h))
+
+    def set_stream(self, stream_ptr: int):
+        self.check(self.L.clrsdp_set_stream(self.h, C.c_void_p(stream_ptr)))
+
+    def exchange_bytes(self) -> int:
+        b = C.c_int64()
+        self.check(self.L.clrsdp_exchange_bytes(self.h, C.byref(b)))
+        return b.value
+
+    def set_exchange(self, fn, send_ptr: int, recv_ptr: int):
+        self._xfn = _lib.EXCHANGE_FN(fn)
+        self.check(self.L.clrsdp_set_exchange(self.h, self._xfn, None, C.c_void_p(send_ptr),
+                                              C.c_void_p(recv_ptr)))
+
+
+def initial_point(bi: BlockInfo, omega_p, omega_d):
+    """x = 0, X = omega_p I, y = 0, Y = omega_d I (MPMP.jl:660-686)."""
+    x = np.zeros(sum(bi.dim_S))
+    X = [[float(omega_p) * np.eye(n) for n in bj] for bj in bi.Y_blocksizes]
+    y = np.zeros(bi.n_y)
+    Y = [[float(omega_d) * np.eye(n) for n in bj] for bj in bi.Y_blocksizes]
+    return x, X, y, Y
+
+
+def _terminate(gap, perr, derr, gthr, pthr, dthr, need_p, need_d, out):
+    """MPMP.jl:1147-1173."""
+    gap_opt, pf, df = gap < gthr, perr < pthr, derr < dthr
+    if need_p and pf:
+        out("Primal feasible solution found")
+        return True
+    if need_d and df:
+        out("Dual feasible solution found")
+        return True
+    if pf and df and gap_opt:
+        out("Optimal solution found")
+        return True
+    return False
+
+
+HEADER = "%5s %8s %11s %11s %11s %10s %10s %10s %10s %10s %10s %10s" % (
+    "iter", "time(s)", "μ", "P-obj", "D-obj", "gap", "P-error", "p-error", "d-error", "α_p",
+    "α_d", "beta")
+
+
+@dataclass
+class RunInfo:
+    iterations: int
+    log: list
+    phase_ms: np.ndarray
+    time_total: float
+    time_loop_after2: float
+    status: str
+
+
+def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterations=500,
+                  beta_infeasible=None, beta_feasible=None, gamma=None, omega_p=None,
+                  omega_d=None, duality_gap_threshold=None, primal_error_threshold=None,
+                  dual_error_threshold=None, need_primal_feasible=False, need_dual_feasible=False,
+                  testing=True, initial_solutions=(), precision_words=1, device=0, verbose=True,
+                  solver: Optional[DeviceSolver] = None, return_info=False):
+    """Solve the clustered low-rank SDP on the GPU; same signature/semantics as MPMP.jl:595-614.
+
+    Returns ``(x, X, y, Y, P, p, d, duality_gap, primal_objective, dual_objective, time)``
+    (MPMP.jl:1014-1024); with ``return_info`` a :class:`RunInfo` is appended.
+    """
+    kw = dict(beta_infeasible=beta_infeasible, beta_feasible=beta_feasible, gamma=gamma,
+              omega_p=omega_p, omega_d=omega_d, duality_gap_threshold=duality_gap_threshold,
+              primal_error_threshold=primal_error_threshold,
+              dual_error_threshold=dual_error_threshold)
+    prm_v = {k: (DEFAULTS[k] if v is None else v) for k, v in kw.items()}
+    out = print if verbose else (lambda *a, **k: None)
+    bi = blockinfo
+    dev = solver or DeviceSolver(constraints, b, bi, precision_words=precision_words, C_blocks=C,
+                                 device=device)
+    prm = make_params(prm_v["beta_infeasible"], prm_v["beta_feasible"], prm_v["gamma"], b0)
+    gthr = float(prm_v["duality_gap_threshold"])
+    pthr = float(prm_v["primal_error_threshold"])
+    dthr = float(prm_v["dual_error_threshold"])
+    if initial_solutions is not None and len(initial_solutions) == 4:
+        x, X, y, Y = initial_solutions
+    else:
+        x, X, y, Y = initial_point(bi, float(prm_v["omega_p"]), float(prm_v["omega_d"]))
+    dev.set_state(x, X, y, Y)
+    b0f = float(b0)
+    out(HEADER)
+    st = dev.initial_residuals(prm)
+    p_obj, d_obj = st.p_obj, st.d_obj
+    # compute_duality_gap(constraints, x, y, Y, C, b) excludes b0 (MPMP.jl:725, 1067-1074)
+    dual_gap = abs((p_obj - b0f) - (d_obj - b0f)) / max(1.0, abs((p_obj - b0f) + (d_obj - b0f)))
+    perr = max(st.p_err, st.P_err)
+    derr = st.d_err
+    pd_feas = perr < pthr and derr < dthr
+    it = 1
+    log = []
+    phase = np.zeros(_lib.NUM_STAGES)
+    t_start = time.time()
+    t_after2 = None
+    status = "maxiterations"
+    while True:
+        if _terminate(dual_gap, perr, derr, gthr, pthr, dthr, need_primal_feasible,
+                      need_dual_feasible, out):
+            status = "terminated"
+            break
+        if not it < maxiterations:
+            break
+        if it == 3:
+            t_after2 = time.time()
+        st = dev.iterate(prm, pd_feas)
+        if it > 2:
+            phase += np.array(st.phase_ms[:])
+        row = (it, time.time() - t_start, st.mu, p_obj, d_obj, dual_gap, st.P_err, st.p_err,
+               st.d_err, st.alpha_p, st.alpha_d, st.beta_c)
+        log.append(row)
+        out("%5d %8.1f %11.3e %11.3e %11.3e %10.2e %10.2e %10.2e %10.2e %10.2e %10.2e %10.2e" % row)
+        p_obj, d_obj = st.p_obj, st.d_obj
+        dual_gap = abs(p_obj - d_obj) / max(1.0, abs(p_obj + d_obj))          # MPMP.jl:942
+        perr = max(st.p_err, st.P_err)                                         # MPMP.jl:943
+        derr = st.d_err
+        it += 1
+        pd_feas = perr < pthr and derr < dthr
+    t_total = time.time() - t_start
+    out(HEADER)
+    xf, Xf, yf, Yf = dev.get_state()
+    P = flat_to_blocks(dev.buffer(_lib.BUF_P), bi)
+    p = dev.buffer(_lib.BUF_PVEC)
+    d = dev.buffer(_lib.BUF_DVEC)
+    gap_nob0 = abs((p_obj - b0f) - (d_obj - b0f)) / max(1.0, abs((p_obj - b0f) + (d_obj - b0f)))
+    res = (xf, Xf, yf, Yf, P, p, d, gap_nob0, p_obj, d_obj, t_total)
+    if return_info:
+        res = res + (RunInfo(it - 1, log, phase, t_total,
+                             (time.time() - t_after2) if t_after2 else 0.0, status),)
+    if solver is None:
+        dev.close()
+    return res
