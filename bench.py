@@ -1,0 +1,183 @@
+"""Benchmark: interior-point iterations/s of solverank1sdp's loop body on MI355X.
+
+Workload (BASELINE.json configs[2], the north-star instance): synthetic clustered low-rank SDP,
+64 clusters x 128x128 blocks (m = 1, L = 1, delta = 128), rank-1 constraints, N = 255 samples per
+cluster, n_y = 128, fp64 -- SURVEY.md §8d "C3".  One step = one full predictor-corrector
+iteration (MPMP.jl:755-887) on device-resident data.  With --gpus N the clusters are sharded
+over N ranks (one process per GPU, cluster-balanced as MPMP.jl:425-465) and the cross-cluster
+reductions are all-gathered over RCCL: strong scaling of one fixed instance.
+
+Also reported: the Schur-assembly roofline (its kernels timed with HIP events on the library's
+stream over the timed region) and a CPU baseline (the numpy restatement of the reference
+algorithm in oracle/, one iteration of the same instance, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (J, delta, rank, n_y, m, L)
+    "c3": dict(J=64, delta=128, rank=1, n_y=128),
+    "c2": dict(J=16, delta=64, rank=2, n_y=64),
+    "c1": dict(J=2, delta=4, rank=1, n_y=4),
+}
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X fp64 matrix spec; measured ceiling 72.4 (profiles/r01_f64_mfma_probe.log)
+HBM_PEAK_GBS = 8000.0
+
+
+def schur_flops_bytes(bi, word=8):
+    """Algorithmic Schur-assembly work of one iteration: per (j,l) block
+    4 m^2 delta K (delta + K) + 8 rank^2 D(D+1)/2 flops and
+    word * [2 n^2 + delta K + K + D(D+1)/2 + m(m+1)/2 K] bytes."""
+    fl, by = 0.0, 0.0
+    for j in range(bi.J):
+        m, D = bi.m[j], bi.dim_S[j]
+        for l in range(bi.L[j]):
+            n = bi.Y_blocksizes[j][l]
+            d = n // m
+            K = bi.rank_sums[j][l][-1]
+            rk = max(bi.ranks[j][l])
+            fl += 4.0 * m * m * d * K * (d + K) + 8.0 * rk * rk * D * (D + 1) / 2
+            by += word * (2 * n * n + d * K + K + D * (D + 1) / 2 + m * (m + 1) / 2 * K)
+    return fl, by
+
+
+def cpu_baseline(cons, b, bi, budget_s=20.0):
+    """Time the oracle (numpy fp64 restatement of MPMP.jl) on this instance: one loop body."""
+    from oracle import mpmp_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+    except Exception:
+        cores = 1
+    ar = O.Fp64()
+    prm = {k: O._param(ar, v) for k, v in O.DEFAULTS.items()}
+    state = O.initial_point(ar, bi, 100.0, 100.0)
+    t0 = time.time()
+    n = 0
+    while True:
+        state, _ = O.iteration(ar, cons, bi, b, None, 0.0, state, False, prm)
+        n += 1
+        if time.time() - t0 > budget_s * 0.5 or n >= 3:
+            break
+    dt = time.time() - t0
+    return {"value": n / dt, "unit": "iterations/s", "cores": int(cores), "kind": "port",
+            "sample": f"{n} loop bodies of the same instance from the initial point, numpy/scipy "
+                      f"fp64 restatement (oracle/mpmp_oracle.py), BLAS threads={cores}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--precision", type=int, default=1)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import _clrsdp_pkg
+    pk = _clrsdp_pkg.load()
+    from clrsdp_amd import _lib
+
+    cfg = CONFIGS[args.config]
+    cons, b = pk.synth(seed=args.seed, **cfg)
+    bi = pk.get_block_info(cons)
+    parts = pk.partition_clusters(bi, world)
+    owned = parts[rank] if world > 1 else None
+
+    dist = None
+    if world > 1:
+        from clrsdp_amd import dist as cdist
+        dist = cdist.TorchExchange(local_rank)
+    dev = pk.DeviceSolver(cons, b, bi, precision_words=args.precision, device=local_rank,
+                          rank=rank, world=world, owned=owned, timing=True)
+    if dist is not None:
+        dist.attach(dev)
+    prm = pk.make_params("0.3", "0.1", "0.7", 0)
+    x0, X0, y0, Y0 = pk.initial_point(bi, 100.0, 100.0)
+    dev.set_state(x0, X0, y0, Y0)
+    dev.initial_residuals(prm)
+
+    def step(pd_feas=False):
+        return dev.iterate(prm, pd_feas)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier_sync():
+        dev.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    barrier_sync()
+    t0 = time.perf_counter()
+    schur_ms = 0.0
+    phase = np.zeros(_lib.NUM_STAGES)
+    for _ in range(args.steps):
+        st = step()
+        ph = np.array(st.phase_ms[:])
+        phase += ph
+        schur_ms += ph[_lib.STAGE_SCHUR]
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        dt = dist.max_over_ranks(dt)
+        schur_ms = dist.max_over_ranks(schur_ms)
+
+    if rank != 0:
+        dist.close()
+        return
+    its = args.steps / dt
+    fl, by = schur_flops_bytes(bi, 8 * args.precision)
+    if world > 1:
+        fl /= world   # per-rank share of the Schur work (the roofline is per GPU)
+        by /= world
+    sch_s = schur_ms / 1e3 / args.steps
+    achieved = fl / sch_s / 1e12
+    res = {
+        "metric": "interior-point iterations/sec (solverank1sdp loop body, MPMP.jl:755-887)",
+        "value": its,
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64" if args.precision == 1 else "dd(f64x2)",
+        "data": "synthetic (seeded splitmix64 instance, SURVEY.md §8d)",
+        "config": {"workload": f"{args.config}: J={cfg['J']} clusters, {cfg['delta']}x{cfg['delta']} blocks, "
+                               f"rank {cfg['rank']}, N={2 * cfg['delta'] - 1} samples, n_y={cfg['n_y']}",
+                   "parallelism": f"clusters sharded over {world} GPU(s)" if world > 1 else "1 GPU"},
+        "roofline": {"bound": "mfma", "kernel": "Schur assembly (stage SCHUR)",
+                     "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "schur_ms_per_iteration": sch_s * 1e3,
+                     "schur_alg_gbs": by / sch_s / 1e9},
+        "phase_ms_per_iteration": {n: float(v / args.steps) for n, v in zip(_lib.STAGE_NAMES, phase)},
+    }
+    if world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(cons, b, bi)
+    print(json.dumps(res))
+    if dist is not None:
+        dist.close()
+    dev.close()
+
+
+if __name__ == "__main__":
+    main()

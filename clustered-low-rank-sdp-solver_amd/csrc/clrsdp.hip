@@ -18,6 +18,7 @@
 
 #include "../../include/clrsdp.h"
 #include "kernels.h"
+#include "kernels_dense.h"
 
 using namespace clrsdp;
 using mw::dd;
@@ -60,6 +61,13 @@ inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) /
 // --------------------------------------------------------------------------------------------
 // launch plans: descriptor arrays built once at creation, replayed every iteration
 // --------------------------------------------------------------------------------------------
+// register-tile shapes of chol_inv_reg per word type (NMAX = TR * GR)
+template <class T> struct RegCfg { static constexpr int TR = 4, TC = 8, GR = 32, GC = 16; };
+template <> struct RegCfg<dd> { static constexpr int TR = 2, TC = 4, GR = 32, GC = 16; };
+template <class T> constexpr int reg_nmax() { return RegCfg<T>::TR * RegCfg<T>::GR; }
+template <class T> size_t eig_lds_bytes(int n) { return sizeof(T) * ((size_t)n * n + 8 * (size_t)n + 16); }
+constexpr size_t LDS_MAX = 160 * 1024;
+
 template <class T>
 struct GemmPlan {
   bool ta = false, tb = false;
@@ -161,8 +169,43 @@ struct MatPlan {  // potrf / eigmin
   }
   void eigmin(hipStream_t s, T* out) const {
     if (h.empty()) return;
-    const size_t lds = sizeof(T) * (4 * (size_t)nmax + 256);
-    eigmin_batched<T><<<(unsigned)h.size(), 256, lds, s>>>(d, out);
+    if (eig_lds_bytes<T>(nmax) <= LDS_MAX) {
+      const size_t lds = eig_lds_bytes<T>(nmax);
+      static bool attr = false;
+      if (!attr) {
+        HIPCHK(hipFuncSetAttribute((const void*)eigmin_lds<T>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX));
+        attr = true;
+      }
+      eigmin_lds<T><<<(unsigned)h.size(), 512, lds, s>>>(d, out);
+    } else {
+      const size_t lds = sizeof(T) * (4 * (size_t)nmax + 256);
+      eigmin_batched<T><<<(unsigned)h.size(), 256, lds, s>>>(d, out);
+    }
+    HIPCHK(hipGetLastError());
+  }
+};
+
+
+template <class T>
+struct CholInvPlan {  // A_b -> L_b^-1 (and optionally L_b)
+  std::vector<MatDesc<T>> hin, hout, hl;
+  MatDesc<T>*din = nullptr, *dout = nullptr, *dl = nullptr;
+  void add(T* A, int n, int lda, T* out, int ldo, T* L = nullptr) {
+    hin.push_back(MatDesc<T>{A, n, lda});
+    hout.push_back(MatDesc<T>{out, n, ldo});
+    if (L) hl.push_back(MatDesc<T>{L, n, ldo});
+  }
+  void finalize() {
+    if (hin.empty()) return;
+    din = upload_vec(hin);
+    dout = upload_vec(hout);
+    if (!hl.empty()) dl = upload_vec(hl);
+  }
+  void launch(hipStream_t s, int* info) const {
+    if (hin.empty()) return;
+    using C = RegCfg<T>;
+    chol_inv_reg<T, C::TR, C::TC, C::GR, C::GC><<<(unsigned)hin.size(), C::GR * C::GC, 0, s>>>(din, dout, dl, info);
     HIPCHK(hipGetLastError());
   }
 };
@@ -226,6 +269,10 @@ struct Solver final : HandleBase {
       p_trU_Y, p_By, p_Btx, p_Wt, p_Wdy, p_PY, p_Z, p_dXY, p_dY;
   TrsmPlan<T> t_Linv, t_W, t_t, t_Q, t_sX1, t_sX2, t_sY1, t_sY2;
   MatPlan<T> f_X, f_Y, f_S, f_Q, e_X, e_Y;
+  // on-chip factorisation path (all sizes <= reg_nmax<T>()): L^-1 and MFMA products
+  bool reg_blk = false, reg_S = false, reg_Q = false;
+  CholInvPlan<T> ci_X, ci_Y, ci_S, ci_Q;
+  GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2;
   BlkDesc* d_blk = nullptr;      // all local blocks
   BlkDesc* d_blk_m = nullptr;    // local blocks with m > 1
   int n_blk_m = 0;
@@ -404,6 +451,18 @@ struct Solver final : HandleBase {
   }
 
   void build_plans() {
+    {
+      int nmax_b = 0, nmax_S = 0;
+      for (const LBlk& b : lb) nmax_b = std::max(nmax_b, b.n);
+      for (int c = 0; c < nc(); ++c) nmax_S = std::max(nmax_S, (int)Ds[oc[c]]);
+      reg_blk = nmax_b <= reg_nmax<T>();
+      reg_S = nmax_S <= reg_nmax<T>();
+      reg_Q = n_y <= reg_nmax<T>();
+    }
+    q_xinv.ta = true;
+    q_sx2.tb = q_sy2.tb = true;
+    q_dx.ta = true;
+    q_q2.ta = true;
     p_xinv.ta = true;
     p_s2x.ta = p_s2y.ta = true;
     p_Q.ta = true;
@@ -433,6 +492,13 @@ struct Solver final : HandleBase {
       t_sY2.add(LY + b.off, n, tB + b.off, n, n, n);
       f_X.add(LX + b.off, n, n);
       f_Y.add(LY + b.off, n, n);
+      ci_X.add(X + b.off, n, n, LX + b.off, n);
+      ci_Y.add(Y + b.off, n, n, LY + b.off, n);
+      q_xinv.add(LX + b.off, n, LX + b.off, n, nullptr, n, Xinv + b.off, n, n, n, n);
+      q_sx1.add(LX + b.off, n, dX + b.off, n, nullptr, n, tA + b.off, n, n, n, n);
+      q_sx2.add(tA + b.off, n, LX + b.off, n, nullptr, n, tB + b.off, n, n, n, n);
+      q_sy1.add(LY + b.off, n, dY + b.off, n, nullptr, n, tA + b.off, n, n, n, n);
+      q_sy2.add(tA + b.off, n, LY + b.off, n, nullptr, n, tB + b.off, n, n, n, n);
       e_X.add(tB + b.off, n, n);
       e_Y.add(tB + b.off, n, n);
       const int ldT = n;           // TX_b is (m delta) x (m K)
@@ -495,6 +561,11 @@ struct Solver final : HandleBase {
       T* Bc = Bm + c_Boff[c];
       const int64_t xo = c_xoff[c];
       f_S.add(Sc, D, D);
+      ci_S.add(Sc, D, D, Sc, D);
+      q_W.add(Sc, D, Bc, D, nullptr, 0, Wc, D, D, (int)n_y, D);
+      q_t.add(Sc, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D, 1, D);
+      q_Wdy.add(Wc, D, dyv, (int)n_y, tvec + xo, D, tmpv + xo, D, D, 1, (int)n_y);
+      q_dx.add(Sc, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D, 1, D);
       t_W.add(Sc, D, Wc, D, D, (int)n_y);
       t_t.add(Sc, D, tvec + xo, D, D, 1);
       p_Q.add(Wc, D, Wc, D, nullptr, 0, Qslab + (int64_t)c * n_y * n_y, (int)n_y, (int)n_y, (int)n_y, D);
@@ -526,6 +597,9 @@ struct Solver final : HandleBase {
     t_Q.add(Qf, (int)n_y, dyv, (int)n_y, (int)n_y, 1);
     t_dxadd_init();
     f_Q.add(Qf, (int)n_y, (int)n_y);
+    ci_Q.add(Q, (int)n_y, (int)n_y, Qf, (int)n_y);
+    q_q1.add(Qf, (int)n_y, dyv, (int)n_y, nullptr, 0, uvec, (int)n_y, (int)n_y, 1, (int)n_y);
+    q_q2.add(Qf, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
     if (nc()) {
       d_scd = upload_vec(scd);
       d_sbd = upload_vec(sbd);
@@ -534,8 +608,10 @@ struct Solver final : HandleBase {
     }
     for (GemmPlan<T>* g : {&p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
-                           &p_Z, &p_dXY, &p_dY})
+                           &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
+                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2})
       g->finalize();
+    for (CholInvPlan<T>* c : {&ci_X, &ci_Y, &ci_S, &ci_Q}) c->finalize();
     for (TrsmPlan<T>* t : {&t_Linv, &t_W, &t_t, &t_Q, &t_sX1, &t_sX2, &t_sY1, &t_sY2, &t_dx})
       t->finalize();
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q, &e_X, &e_Y}) f->finalize();
@@ -694,6 +770,11 @@ struct Solver final : HandleBase {
     blk_lin(R, R, 1.0, nullptr, 0.0, sc + SC_MU_P);  // R += mu_p I
   }
   void st_xinv() {
+    if (reg_blk) {                            // L_X^-1 on chip, X^-1 = L^-T L^-1 on MFMA
+      ci_X.launch(stream, info);
+      q_xinv.launch(stream, 1.0, 0.0);
+      return;
+    }
     blk_lin(LX, X, 1.0, nullptr, 0.0);
     f_X.potrf(stream, info);
     if (nb()) blk_identity<T><<<nb(), 256, 0, stream>>>(d_blk, tA);
@@ -711,17 +792,26 @@ struct Solver final : HandleBase {
                                                                  BY, S, n_pairs);
   }
   void st_factor() {
-    f_S.potrf(stream, info + info_S0);
-    vlin(Wm, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
-    t_W.launch(stream, false);                // W_j = L_j^-1 B_j
+    if (reg_S) {                              // S_j <- L_j^-1 in place; W_j = L_j^-1 B_j (MFMA)
+      ci_S.launch(stream, info + info_S0);
+      q_W.launch(stream, 1.0, 0.0);
+    } else {
+      f_S.potrf(stream, info + info_S0);
+      vlin(Wm, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
+      t_W.launch(stream, false);              // W_j = L_j^-1 B_j
+    }
     p_Q.launch(stream, 1.0, 0.0);             // slab_j = W_j^T W_j
     const int64_t q2 = n_y * n_y;
     if (nc()) slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(Qslab, nc(), q2, q2, xsend);
     else fill(xsend, 0.0, q2);
     exchange(2, q2);
     slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(xrecv, world, q2, q2, Q);
-    vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
-    f_Q.potrf(stream, info + info_Q0);
+    if (reg_Q) {
+      ci_Q.launch(stream, info + info_Q0);    // Qf = L_Q^-1
+    } else {
+      vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
+      f_Q.potrf(stream, info + info_Q0);
+    }
   }
   void st_residuals(bool use_AY) {
     // P = sum_i x_i A_i - X - C
@@ -760,19 +850,33 @@ struct Solver final : HandleBase {
     colsums();
     trace_aggregate(tval, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
     // t_j = L_j^-1 rhs_j ;  u = sum_j W_j^T t_j ;  dy = Q^-1 (p - u)
-    vlin(tvec, rhs, 1.0, nullptr, 0, nullptr, 0, nx);
-    t_t.launch(stream, false);
+    if (reg_S) {
+      q_t.launch(stream, 1.0, 0.0);
+    } else {
+      vlin(tvec, rhs, 1.0, nullptr, 0, nullptr, 0, nx);
+      t_t.launch(stream, false);
+    }
     p_Wt.launch(stream, 1.0, 0.0);
     if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
     else fill(xsend, 0.0, n_y);
     exchange(tag, n_y);
     slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec);
     vlin(dyv, pvec, 1.0, uvec, -1.0, nullptr, 0, n_y);
-    t_Q.launch(stream, false);
-    t_Q.launch(stream, true);
+    if (reg_Q) {
+      q_q1.launch(stream, 1.0, 0.0);          // u = L_Q^-1 r
+      q_q2.launch(stream, 1.0, 0.0);          // dy = L_Q^-T u
+    } else {
+      t_Q.launch(stream, false);
+      t_Q.launch(stream, true);
+    }
     // dx_j = L_j^-T (t_j + W_j dy)
-    p_Wdy.launch(stream, 1.0, 1.0);
-    t_dx.launch(stream, true);
+    if (reg_S) {
+      q_Wdy.launch(stream, 1.0, 1.0);
+      q_dx.launch(stream, 1.0, 0.0);
+    } else {
+      p_Wdy.launch(stream, 1.0, 1.0);
+      t_dx.launch(stream, true);
+    }
     // dX = P + sum_i dx_i A_i
     weighted_A(dx, p_wA_dX, dX);
     blk_lin(dX, dX, 1.0, P, 1.0);
@@ -791,20 +895,31 @@ struct Solver final : HandleBase {
     blk_lin(R, R, 1.0, nullptr, 0.0, sc + SC_MU_C);
   }
   void st_step(const clrsdp_params* prm, int pd_feas) {
-    // X: L_X from the X^-1 stage
-    blk_lin(tA, dX, 1.0, nullptr, 0.0);
-    t_sX1.launch(stream, false);
-    sym(tB, tA, 2);
-    t_sX2.launch(stream, false);
-    e_X.eigmin(stream, eigX);
-    // Y
-    blk_lin(LY, Y, 1.0, nullptr, 0.0);
-    f_Y.potrf(stream, info + info_Y0);
-    blk_lin(tA, dY, 1.0, nullptr, 0.0);
-    t_sY1.launch(stream, false);
-    sym(tB, tA, 2);
-    t_sY2.launch(stream, false);
-    e_Y.eigmin(stream, eigY);
+    if (reg_blk) {
+      // X: L_X^-1 from the X^-1 stage;  M = L^-1 dX L^-T on MFMA
+      q_sx1.launch(stream, 1.0, 0.0);
+      q_sx2.launch(stream, 1.0, 0.0);
+      e_X.eigmin(stream, eigX);
+      ci_Y.launch(stream, info + info_Y0);
+      q_sy1.launch(stream, 1.0, 0.0);
+      q_sy2.launch(stream, 1.0, 0.0);
+      e_Y.eigmin(stream, eigY);
+    } else {
+      // X: L_X from the X^-1 stage
+      blk_lin(tA, dX, 1.0, nullptr, 0.0);
+      t_sX1.launch(stream, false);
+      sym(tB, tA, 2);
+      t_sX2.launch(stream, false);
+      e_X.eigmin(stream, eigX);
+      // Y
+      blk_lin(LY, Y, 1.0, nullptr, 0.0);
+      f_Y.potrf(stream, info + info_Y0);
+      blk_lin(tA, dY, 1.0, nullptr, 0.0);
+      t_sY1.launch(stream, false);
+      sym(tB, tA, 2);
+      t_sY2.launch(stream, false);
+      e_Y.eigmin(stream, eigY);
+    }
     if (nb()) {
       ordered_reduce<T><<<1, 1, 0, stream>>>(eigX, nb(), 1, 3, xsend);
       ordered_reduce<T><<<1, 1, 0, stream>>>(eigY, nb(), 1, 3, xsend + 1);

@@ -1,0 +1,73 @@
+"""Multi-GPU plumbing: one process per GPU, the library's cross-rank exchange over
+torch.distributed (backend "nccl" = RCCL over xGMI on ROCm; "gloo" for CPU-side tests).
+
+The library (include/clrsdp.h) calls the registered exchange in the middle of a stage with its
+work enqueued on `stream`; here that stream is torch's current stream, so an RCCL all-gather on
+it is ordered after the partials were written and before their rank-ordered reduction, with no
+host synchronisation.  Payloads are the few cross-cluster quantities of one iteration (Q:
+n_y^2 words, three n_y-vectors, ~10 scalars), so the exchange is latency-bound.
+"""
+from __future__ import annotations
+
+import os
+
+
+class TorchExchange:
+    def __init__(self, local_rank: int, backend: str = "nccl", device: str = "cuda"):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.backend = backend
+        if device == "cuda":
+            torch.cuda.set_device(local_rank)
+        if not dist.is_initialized():
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            else:
+                dist.init_process_group(backend)
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.local_rank = local_rank
+        self.dev = None
+
+    def attach(self, dev):
+        torch = self.torch
+        nbytes = dev.exchange_bytes()
+        self.send = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+        self.recv = torch.zeros(nbytes * self.world, dtype=torch.uint8, device="cuda")
+        dev.set_stream(torch.cuda.current_stream().cuda_stream)
+        dev.set_exchange(self._exchange, self.send.data_ptr(), self.recv.data_ptr())
+        self.dev = dev
+
+    def _exchange(self, ctx, tag, nbytes, stream):
+        try:
+            w = self.world
+            if self.backend == "nccl":
+                self.dist.all_gather_into_tensor(self.recv[:nbytes * w], self.send[:nbytes])
+            else:  # host staging for gloo (tests on a single GPU)
+                self.torch.cuda.current_stream().synchronize()
+                src = self.send[:nbytes].cpu()
+                outs = [self.torch.empty_like(src) for _ in range(w)]
+                self.dist.all_gather(outs, src)
+                self.recv[:nbytes * w].copy_(self.torch.cat(outs).to("cuda"))
+            return 0
+        except Exception as e:  # never let an exception cross the C ABI
+            print(f"[clrsdp exchange tag {tag}] {e!r}", flush=True)
+            return 1
+
+    def barrier(self):
+        if self.backend == "nccl":
+            self.dist.barrier(device_ids=[self.local_rank])
+        else:
+            self.dist.barrier()
+
+    def max_over_ranks(self, v: float) -> float:
+        torch = self.torch
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist.is_initialized():
+            self.dist.destroy_process_group()

@@ -11,9 +11,9 @@ from importlib import import_module
 inst = import_module("clrsdp_amd.instance")
 
 
-def rel(a, b):
+def rel(a, b, scale=0.0):
     a = np.asarray(a, dtype=float).ravel(); b = np.asarray(b, dtype=float).ravel()
-    return float(np.max(np.abs(a - b)) / max(1e-300, np.max(np.abs(b))))
+    return float(np.max(np.abs(a - b)) / max(1e-300, np.max(np.abs(b)), scale))
 
 
 def run(cfg, iters_before=2):
@@ -49,8 +49,8 @@ def run(cfg, iters_before=2):
     dev.run_stage(L.STAGE_FACTOR, P, pd)
     out["Q"] = rel(dev.buffer(L.BUF_Q), it["dec"].Q_raw.reshape(-1, order="F"))
     dev.run_stage(L.STAGE_RESIDUALS, P, pd)
-    out["P"] = rel(dev.buffer(L.BUF_P), fl(it["P"]))
-    out["p"] = rel(dev.buffer(L.BUF_PVEC), it["p"])
+    out["P"] = rel(dev.buffer(L.BUF_P), fl(it["P"]), np.max(np.abs(fl(X))))
+    out["p"] = rel(dev.buffer(L.BUF_PVEC), it["p"], np.max(np.abs(b)))
     out["d"] = rel(dev.buffer(L.BUF_DVEC), it["d"])
     dev.run_stage(L.STAGE_PREDICTOR, P, pd)
     dx, dXp, dy, dYp = it["pred"]
@@ -82,7 +82,8 @@ def run(cfg, iters_before=2):
 if __name__ == "__main__":
     cfgs = [dict(J=2, delta=4, rank=1, n_y=4), dict(J=2, delta=3, rank=1, n_y=3, m=2, L=2),
             dict(J=3, delta=4, rank=2, n_y=5), dict(J=4, delta=20, rank=1, n_y=8),
-            dict(J=2, delta=64, rank=2, n_y=64), dict(J=2, delta=128, rank=1, n_y=128)]
+            dict(J=2, delta=64, rank=2, n_y=64), dict(J=2, delta=128, rank=1, n_y=128),
+            dict(J=2, delta=150, rank=1, n_y=140), dict(J=3, delta=5, rank=1, n_y=4, m=3, L=2)]
     for cfg in cfgs:
         t = time.time()
         try:
