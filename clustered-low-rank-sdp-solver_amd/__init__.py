@@ -5,10 +5,10 @@ Public API mirrors MPMP.jl (exports at MPMP.jl:19): ``solverank1sdp``, ``get_blo
 """
 from .blockinfo import BlockInfo, block_info, distribute_weights_swapping, get_block_info, \
     partition_clusters
-from .instance import Cluster, synth
+from .instance import SPHERE_PACKING_SHAPE, Cluster, synth, synth_mixed
 from .solver import DeviceSolver, initial_point, make_params, solverank1sdp
 from . import _lib
 
 __all__ = ["BlockInfo", "block_info", "get_block_info", "distribute_weights_swapping",
-           "partition_clusters", "Cluster", "synth", "DeviceSolver", "initial_point",
+           "partition_clusters", "Cluster", "synth", "synth_mixed", "SPHERE_PACKING_SHAPE", "DeviceSolver", "initial_point",
            "make_params", "solverank1sdp"]

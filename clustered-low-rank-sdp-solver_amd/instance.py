@@ -106,6 +106,50 @@ def synth(J: int, delta: int, rank: int, n_y: int, seed: int = 0, m: int = 1, L:
     return cons, b
 
 
+def synth_mixed(specs, n_y: int, seed: int = 0) -> tuple:
+    """Synthetic instance with per-cluster shapes: ``specs[j] = dict(m=, deltas=[delta_l...],
+    N=, ranks=None or ranks[l][k])``.  Same construction (and feasibility) as :func:`synth`.
+    The sphere-packing shape of BASELINE config 5 is :data:`SPHERE_PACKING_SHAPE`."""
+    cons, xs = [], []
+    for j, sp in enumerate(specs):
+        m, deltas, N = sp["m"], sp["deltas"], sp["N"]
+        A, H = [], []
+        for l, delta in enumerate(deltas):
+            Al, Hl = [], []
+            for k in range(N):
+                rk = 1 if sp.get("ranks") is None else sp["ranks"][l][k]
+                st = ((j * 131 + l) * 65537 + k) * 17 + 3
+                Al.append([uniform(seed, st + q, delta) / math.sqrt(delta) for q in range(rk)])
+                Hl.append(list(uniform(seed, st + 7919, max(rk, 1), 0.5, 1.5)[:rk]))
+            A.append(Al)
+            H.append(Hl)
+        D = m * (m + 1) // 2 * N
+        B = uniform(seed, 10_000_019 + j, D * n_y).reshape(n_y, D).T.copy()
+        c = np.zeros(D)
+        for r in range(m):
+            for k in range(N):
+                t = k + (r + r * (r + 1) // 2) * N
+                c[t] = sum(lam * float(v @ v) for l in range(len(deltas))
+                           for v, lam in zip(A[l][k], H[l][k]))
+        cons.append(Cluster(A, B, c, H))
+        xs.append(np.ones(D))
+    y0 = uniform(seed, 77_777_777, n_y)
+    b = np.zeros(n_y)
+    for cl, x0 in zip(cons, xs):
+        cl.c = cl.c + cl.B @ y0
+        b = b + cl.B.T @ x0
+    return cons, b
+
+
+# Block structure of the sphere-packing instance of examples/SpherePacking.jl (n = 3, d = 8,
+# N = 2 radii; SP.jl:56-105): J = 7 clusters, blocks {2}, {18, 16}, {9, 8} x 3, {1} x 2,
+# dim_S = {3, 51, 17, 17, 17, 1, 1}, n_y = 52 (SURVEY.md §8 "C5").
+SPHERE_PACKING_SHAPE = dict(
+    specs=[dict(m=2, deltas=[1], N=1), dict(m=2, deltas=[9, 8], N=17)]
+    + [dict(m=1, deltas=[9, 8], N=17)] * 3 + [dict(m=1, deltas=[1], N=1)] * 2,
+    n_y=52)
+
+
 # ---------------------------------------------------------------------------------------------
 # flat C-ABI layout (include/clrsdp.h)
 # ---------------------------------------------------------------------------------------------

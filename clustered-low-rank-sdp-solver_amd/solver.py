@@ -227,6 +227,7 @@ class RunInfo:
     time_total: float
     time_loop_after2: float
     status: str
+    exact: list = None   # per iteration, the device scalar slots at full precision (record_exact)
 
 
 def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterations=500,
@@ -234,7 +235,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
                   omega_d=None, duality_gap_threshold=None, primal_error_threshold=None,
                   dual_error_threshold=None, need_primal_feasible=False, need_dual_feasible=False,
                   testing=True, initial_solutions=(), precision_words=1, device=0, verbose=True,
-                  solver: Optional[DeviceSolver] = None, return_info=False):
+                  solver: Optional[DeviceSolver] = None, return_info=False, record_exact=False):
     """Solve the clustered low-rank SDP on the GPU; same signature/semantics as MPMP.jl:595-614.
 
     Returns ``(x, X, y, Y, P, p, d, duality_gap, primal_objective, dual_objective, time)``
@@ -273,6 +274,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     t_start = time.time()
     t_after2 = None
     status = "maxiterations"
+    exact = []
     while True:
         if _terminate(dual_gap, perr, derr, gthr, pthr, dthr, need_primal_feasible,
                       need_dual_feasible, out):
@@ -285,6 +287,9 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
         st = dev.iterate(prm, pd_feas)
         if it > 2:
             phase += np.array(st.phase_ms[:])
+        if record_exact:
+            sc = dev.buffer(_lib.BUF_SCALARS, exact=True)
+            exact.append({k: sc[v] for k, v in _lib.SC.items()})
         row = (it, time.time() - t_start, st.mu, p_obj, d_obj, dual_gap, st.P_err, st.p_err,
                st.d_err, st.alpha_p, st.alpha_d, st.beta_c)
         log.append(row)
@@ -305,7 +310,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     res = (xf, Xf, yf, Yf, P, p, d, gap_nob0, p_obj, d_obj, t_total)
     if return_info:
         res = res + (RunInfo(it - 1, log, phase, t_total,
-                             (time.time() - t_after2) if t_after2 else 0.0, status),)
+                             (time.time() - t_after2) if t_after2 else 0.0, status, exact),)
     if solver is None:
         dev.close()
     return res

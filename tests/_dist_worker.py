@@ -1,0 +1,41 @@
+"""Worker for tests/test_gpu_dist.py: one rank of a sharded run on a (shared) GPU, exchanging
+through torch.distributed gloo (host-staged), printing its iteration log as JSON."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import _clrsdp_pkg  # noqa: E402
+
+
+def main():
+    out = sys.argv[1]
+    iters = int(sys.argv[2])
+    pk = _clrsdp_pkg.load()
+    from clrsdp_amd import dist as cdist
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    ex = cdist.TorchExchange(0, backend="gloo")
+    cons, b = pk.synth(seed=12, J=5, delta=16, rank=1, n_y=9, m=1)
+    bi = pk.get_block_info(cons)
+    owned = pk.partition_clusters(bi, world)[rank]
+    dev = pk.DeviceSolver(cons, b, bi, device=0, rank=rank, world=world, owned=owned)
+    ex.attach(dev)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    dev.set_state(*pk.initial_point(bi, 10.0, 10.0))
+    log = []
+    for _ in range(iters):
+        st = dev.iterate(P, False)
+        log.append([st.mu, st.alpha_p, st.alpha_d, st.beta_c, st.p_obj, st.d_obj, st.P_err,
+                    st.p_err, st.d_err])
+    x, X, y, Y = dev.get_state()
+    json.dump({"rank": rank, "owned": owned, "log": log, "y": list(map(float, y)),
+               "x": list(map(float, x))}, open(f"{out}.{rank}.json", "w"))
+    dev.close()
+    ex.close()
+
+
+if __name__ == "__main__":
+    main()

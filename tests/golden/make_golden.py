@@ -1,0 +1,65 @@
+"""Generate the golden vectors under tests/golden/ with the oracle (oracle/mpmp_oracle.py).
+
+The reference (Julia + Arblib) cannot run in this container, so these vectors
+are produced by the restatement itself: an fp64 run and a 256-bit run of solverank1sdp on small
+seeded synthetic instances.  They pin the oracle and the HIP path against regressions and give
+the multi-word (double-double) path something exact to converge to.
+
+    python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import mpmath  # noqa: E402
+
+import _clrsdp_pkg  # noqa: E402
+from oracle import mpmp_oracle as O  # noqa: E402
+
+pk = _clrsdp_pkg.load()
+PARAMS = dict(omega_p=10.0, omega_d=10.0, primal_error_threshold=1e-10, dual_error_threshold=1e-10,
+              duality_gap_threshold=1e-10)
+
+
+def to_mp(ar, cons):
+    return [pk.Cluster([[[ar.asarray(v) for v in vk] for vk in Al] for Al in cl.A],
+                       ar.asarray(cl.B), ar.asarray(cl.c),
+                       [[[ar.num(x) for x in hk] for hk in Hl] for Hl in cl.H]) for cl in cons]
+
+
+def run(name, inst, iters, prec=None, tol=1e-9):
+    cons, b = pk.synth(**inst)
+    bi = O.get_block_info(cons)
+    if prec:
+        ar = O.Mp(prec)
+        consr = to_mp(ar, cons)
+        br = ar.asarray(b)
+    else:
+        ar = O.Fp64()
+        consr, br = cons, b
+    res = O.solverank1sdp(consr, br, bi, ar=ar, maxiterations=iters + 1, **PARAMS)
+    fmt = (lambda v: mpmath.nstr(v, 70)) if prec else (lambda v: repr(float(v)))
+    out = {
+        "generator": "tests/golden/make_golden.py (oracle/mpmp_oracle.py, %s)" % ar.name,
+        "instance": inst, "params": PARAMS, "iterations": iters, "tolerance_fp64": tol,
+        "log": [{k: fmt(getattr(r, k)) for k in ("mu", "p_obj", "d_obj", "gap", "P_err", "p_err",
+                                                  "d_err", "alpha_p", "alpha_d", "beta")}
+                for r in res.log],
+        "x": [fmt(v) for v in res.x],
+        "y": [fmt(v) for v in res.y],
+    }
+    with open(os.path.join(HERE, name + ".json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(name, len(res.log), "iterations")
+
+
+if __name__ == "__main__":
+    run("c1_fp64_seed3", dict(J=2, delta=4, rank=1, n_y=4, seed=3), 10)
+    run("m2L2_fp64_seed4", dict(J=2, delta=3, rank=1, n_y=3, m=2, L=2, seed=4), 10)
+    run("c1_mp256_seed3", dict(J=2, delta=4, rank=1, n_y=4, seed=3), 10, prec=256)
+    run("rank2_mp256_seed5", dict(J=2, delta=3, rank=2, n_y=3, seed=5), 8, prec=256)

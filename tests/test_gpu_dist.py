@@ -1,0 +1,54 @@
+"""Two ranks sharing the box's GPU, clusters sharded, exchange over gloo: identical iterates to
+the single-process run (up to the rank-order summation of the exchanged partials)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_match_single_rank(pk):
+    iters = 4
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "r")
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={_port()}",
+               os.path.join(HERE, "_dist_worker.py"), out, str(iters)]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        res = [json.load(open(f"{out}.{k}.json")) for k in range(2)]
+    cons, b = pk.synth(seed=12, J=5, delta=16, rank=1, n_y=9, m=1)
+    bi = pk.get_block_info(cons)
+    dev = pk.DeviceSolver(cons, b, bi)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    dev.set_state(*pk.initial_point(bi, 10.0, 10.0))
+    ref = []
+    for _ in range(iters):
+        st = dev.iterate(P, False)
+        ref.append([st.mu, st.alpha_p, st.alpha_d, st.beta_c, st.p_obj, st.d_obj])
+    x, X, y, Y = dev.get_state()
+    dev.close()
+    for rr in res:
+        np.testing.assert_allclose(np.array(rr["log"])[:, :6], np.array(ref), rtol=1e-11, atol=1e-13)
+        np.testing.assert_allclose(rr["y"], y, rtol=1e-10, atol=1e-12)
+    # x is sharded: each rank holds its own clusters' entries
+    for rr in res:
+        for j in rr["owned"]:
+            a, c = bi.x_indices[j], bi.x_indices[j + 1]
+            np.testing.assert_allclose(rr["x"][a:c], x[a:c], rtol=1e-10, atol=1e-12)

@@ -1,0 +1,242 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle on the same seeded inputs.
+
+Tolerances (stated per precision):
+  fp64 stage outputs: 1e-11 relative to the largest entry (or to the input scale for residuals
+  that are themselves at round-off level);  double-double: 1e-25 relative against the 256-bit
+  oracle on well-conditioned states.  The reference factors S_j and Q with pivoted LU; the GPU
+  uses Cholesky + L^-1 (S and Q are SPD), so results agree to conditioning-scaled round-off.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from helpers import CONFIGS_SMALL, poly_min_instance, rel_err
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+TOL64 = 1e-11
+
+
+def _blocks(inst, blocks):
+    return inst.blocks_to_flat(blocks)
+
+
+def _oracle_states(oracle, cons, bi, b, iters_before, ar=None, omega=10.0):
+    ar = ar or oracle.Fp64()
+    prm = {k: oracle._param(ar, v) for k, v in oracle.DEFAULTS.items()}
+    state = oracle.initial_point(ar, bi, omega, omega)
+    for _ in range(iters_before):
+        state, _ = oracle.iteration(ar, cons, bi, b, None, ar.num(0), state, False, prm)
+    nxt, it = oracle.iteration(ar, cons, bi, b, None, ar.num(0), state, False, prm)
+    return state, nxt, it
+
+
+def _stage_compare(pk, oracle, cons, b, iters_before=2, words=1, ar=None, tol=TOL64):
+    from clrsdp_amd import _lib as L
+    from clrsdp_amd import instance as inst
+    bi = oracle.get_block_info(cons)
+    state, nxt, it = _oracle_states(oracle, cons, bi, b, iters_before, ar)
+    dev = pk.DeviceSolver(cons, b, pk.get_block_info(cons), precision_words=words)
+    try:
+        x, X, y, Y = state
+        dev.set_state(x, X, y, Y)
+        P = pk.make_params("0.3", "0.1", "0.7", 0)
+        exact = words > 1
+        fl = lambda blocks: _blocks(inst, blocks)
+        buf = lambda k: np.array(dev.buffer(k, exact), dtype=float if not exact else object)
+        e = {}
+        dev.run_stage(L.STAGE_MU_R, P, False)
+        e["mu"] = rel_err([dev.scalar("mu", exact)], [it["mu"]])
+        e["R"] = rel_err(buf(L.BUF_R), fl(it["R"]))
+        dev.run_stage(L.STAGE_XINV, P, False)
+        e["Xinv"] = rel_err(buf(L.BUF_XINV), fl(it["X_inv"]))
+        dev.run_stage(L.STAGE_SCHUR, P, False)
+        e["S"] = rel_err(buf(L.BUF_S), np.concatenate([s.reshape(-1, order="F") for s in it["dec"].S_raw]))
+        ay = [it["A_Y"][j][l][r][s] for j in range(bi.J) for l in range(bi.L[j])
+              for r in range(bi.m[j]) for s in range(r + 1)]
+        e["A_Y"] = rel_err(buf(L.BUF_AY), np.concatenate(ay))
+        dev.run_stage(L.STAGE_FACTOR, P, False)
+        e["Q"] = rel_err(buf(L.BUF_Q), it["dec"].Q_raw.reshape(-1, order="F"))
+        dev.run_stage(L.STAGE_RESIDUALS, P, False)
+        Xscale = float(np.max(np.abs(np.array(fl(X), dtype=float))))
+        e["P"] = rel_err(buf(L.BUF_P), fl(it["P"]), Xscale)
+        e["p"] = rel_err(buf(L.BUF_PVEC), it["p"], float(np.max(np.abs(np.array(b, dtype=float)))))
+        # d is also a residual that reaches round-off once the dual is feasible
+        cscale = float(max(np.max(np.abs(np.array(c.c, dtype=float))) for c in cons))
+        e["d"] = rel_err(buf(L.BUF_DVEC), it["d"], cscale)
+        for stage, key, Rk in ((L.STAGE_PREDICTOR, "pred", None), (L.STAGE_CORRECTOR, "corr", "R2")):
+            if Rk:
+                dev.run_stage(L.STAGE_CORRECTOR_R, P, False)
+                e["beta_c"] = rel_err([dev.scalar("beta_c", exact)], [it["beta_c"]])
+                e["R2"] = rel_err(buf(L.BUF_R), fl(it["R2"]))
+            dev.run_stage(stage, P, False)
+            dx, dX, dy, dY = it[key]
+            e[key + "_dx"] = rel_err(buf(L.BUF_DX), dx)
+            e[key + "_dy"] = rel_err(buf(L.BUF_DY), dy)
+            e[key + "_dX"] = rel_err(buf(L.BUF_DXMAT), fl(dX))
+            e[key + "_dY"] = rel_err(buf(L.BUF_DYMAT), fl(dY))
+        dev.run_stage(L.STAGE_STEP, P, False)
+        e["alpha_p"] = rel_err([dev.scalar("alpha_p", exact)], [it["alpha_p"]])
+        e["alpha_d"] = rel_err([dev.scalar("alpha_d", exact)], [it["alpha_d"]])
+        dev.run_stage(L.STAGE_UPDATE, P, False)
+        xg, Xg, yg, Yg = dev.get_state(exact)
+        e["x+"] = rel_err(xg, nxt[0])
+        e["X+"] = rel_err(fl(Xg), fl(nxt[1]))
+        e["y+"] = rel_err(yg, nxt[2])
+        e["Y+"] = rel_err(fl(Yg), fl(nxt[3]))
+        bad = {k: v for k, v in e.items() if not v <= tol}
+        assert not bad, f"stage parity failures: {bad}"
+        return e
+    finally:
+        dev.close()
+
+
+CONFIGS_GPU = CONFIGS_SMALL + [
+    dict(J=4, delta=20, rank=1, n_y=8),
+    dict(J=2, delta=64, rank=2, n_y=64),      # C2 cluster shape (dim_S = 127)
+    dict(J=2, delta=128, rank=1, n_y=128),    # C3 cluster shape (dim_S = 255 > on-chip limit)
+    dict(J=2, delta=150, rank=1, n_y=140),    # blocks > 128: global-memory factorisation path
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS_GPU, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_stage_parity_fp64(pk, oracle, cfg):
+    cons, b = pk.synth(seed=3, **cfg)
+    _stage_compare(pk, oracle, cons, b)
+
+
+def test_stage_parity_sphere_packing_shape(pk, oracle):
+    """Mixed block sizes 1..18, m = 2 and m = 1 clusters, 2 blocks per cluster (config 5 shape)."""
+    cons, b = pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, seed=1)
+    _stage_compare(pk, oracle, cons, b, iters_before=3)
+
+
+def test_stage_parity_zero_rank_samples(pk, oracle):
+    """Samples with rank 0 (nz_k > 0, MPMP.jl:489-491) and unequal ranks."""
+    ranks = [[0, 1, 2, 1, 0, 3, 1], [1, 1, 1, 0, 2, 1, 1]]
+    cons, b = pk.synth(seed=4, J=2, delta=3, rank=1, n_y=3, m=2, L=2, ranks=ranks, N=7)
+    _stage_compare(pk, oracle, cons, b)
+
+
+def test_stage_parity_dd_vs_256bit(pk, oracle):
+    """double-double kernels against the 256-bit oracle."""
+    cons, b = pk.synth(seed=3, J=2, delta=4, rank=1, n_y=4)
+    ar = oracle.Mp(256)
+    consm = [pk.Cluster([[[ar.asarray(v) for v in vk] for vk in Al] for Al in cl.A],
+                        ar.asarray(cl.B), ar.asarray(cl.c),
+                        [[[ar.num(x) for x in hk] for hk in Hl] for Hl in cl.H]) for cl in cons]
+    _stage_compare(pk, oracle, consm, ar.asarray(b), words=2, ar=ar, tol=1e-25)
+
+
+def _golden(name):
+    return json.load(open(os.path.join(GOLDEN, name + ".json")))
+
+
+@pytest.mark.parametrize("name,words,tol", [("c1_fp64_seed3", 1, 1e-9), ("m2L2_fp64_seed4", 1, 1e-9),
+                                            ("c1_mp256_seed3", 1, 1e-9), ("c1_mp256_seed3", 2, 1e-24),
+                                            ("rank2_mp256_seed5", 2, 1e-24)])
+def test_full_run_matches_golden(pk, name, words, tol):
+    """solverank1sdp on the GPU reproduces the golden iteration log (mu, alpha_p, alpha_d, beta)."""
+    import mpmath
+    mpmath.mp.prec = 256
+    g = _golden(name)
+    cons, b = pk.synth(**g["instance"])
+    bi = pk.get_block_info(cons)
+    res = pk.solverank1sdp(cons, b, bi, maxiterations=g["iterations"] + 1, precision_words=words,
+                           verbose=False, return_info=True, record_exact=True, **g["params"])
+    info = res[-1]
+    assert len(info.exact) >= len(g["log"]) - 1
+    for it, (sc, ref) in enumerate(zip(info.exact, g["log"])):
+        for key, slot in (("mu", "mu"), ("alpha_p", "alpha_p"), ("alpha_d", "alpha_d"),
+                          ("beta", "beta_c")):
+            r = mpmath.mpf(ref[key])
+            v = mpmath.mpf(sc[slot])
+            assert abs(v - r) <= tol * max(1, abs(r)), (it + 1, key, float(v), float(r))
+
+
+def test_known_answer_polynomial_minimum_gpu(pk):
+    cons, b, pmin = poly_min_instance(pk)
+    bi = pk.get_block_info(cons)
+    res = pk.solverank1sdp(cons, b, bi, omega_p=10.0, omega_d=10.0, maxiterations=100,
+                           duality_gap_threshold=1e-10, primal_error_threshold=1e-10,
+                           dual_error_threshold=1e-10, verbose=False, return_info=True)
+    assert res[-1].status == "terminated"
+    assert abs(res[9] - pmin) < 1e-8 and abs(res[8] - pmin) < 1e-8
+
+
+def test_iterate_equals_stagewise(pk):
+    """clrsdp_iterate == the ten stages run one by one (bitwise)."""
+    from clrsdp_amd import _lib as L
+    cons, b = pk.synth(seed=9, J=3, delta=6, rank=1, n_y=5, m=2)
+    bi = pk.get_block_info(cons)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    st0 = pk.initial_point(bi, 10.0, 10.0)
+    outs = []
+    for mode in ("iterate", "stages"):
+        dev = pk.DeviceSolver(cons, b, bi)
+        dev.set_state(*st0)
+        for _ in range(3):
+            if mode == "iterate":
+                dev.iterate(P, False)
+            else:
+                for s in range(L.NUM_STAGES):
+                    dev.run_stage(s, P, False)
+        outs.append(dev.get_state())
+        dev.close()
+    a, c = outs
+    assert np.array_equal(a[0], c[0]) and np.array_equal(a[2], c[2])
+    for j in range(bi.J):
+        assert np.array_equal(a[1][j][0], c[1][j][0])
+
+
+def test_not_positive_definite_reports_error(pk):
+    from clrsdp_amd import _lib as L
+    cons, b = pk.synth(seed=9, J=2, delta=4, rank=1, n_y=3)
+    bi = pk.get_block_info(cons)
+    x, X, y, Y = pk.initial_point(bi, 10.0, 10.0)
+    X[1][0][2, 2] = -5.0
+    dev = pk.DeviceSolver(cons, b, bi)
+    dev.set_state(x, X, y, Y)
+    with pytest.raises(L.ClrsdpError) as ei:
+        dev.iterate(pk.make_params("0.3", "0.1", "0.7", 0), False)
+    assert ei.value.code == L.E_NOT_PD_X
+    dev.close()
+
+
+def test_c3_full_size_newton_identities(pk, oracle):
+    """At the bench size (64 clusters x 128x128 blocks) check size-independent properties of one
+    GPU iteration: B^T dx = p, Tr(A_* dY) + B dy = d, dX = P + sum dx_i A_i, S symmetric."""
+    from clrsdp_amd import _lib as L
+    from clrsdp_amd import instance as inst
+    cons, b = pk.synth(seed=0, J=64, delta=128, rank=1, n_y=128)
+    bi = pk.get_block_info(cons)
+    dev = pk.DeviceSolver(cons, b, bi)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    dev.set_state(*pk.initial_point(bi, 100.0, 100.0))
+    for _ in range(2):
+        dev.iterate(P, False)
+    for s in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR):
+        dev.run_stage(s, P, False)
+    S = dev.buffer(L.BUF_S)
+    D = bi.dim_S[0]
+    S0 = S[:D * D].reshape(D, D, order="F")
+    assert np.array_equal(S0, S0.T)
+    for s in (L.STAGE_FACTOR, L.STAGE_RESIDUALS, L.STAGE_PREDICTOR):
+        dev.run_stage(s, P, False)
+    ar = oracle.Fp64()
+    dx, dy = dev.buffer(L.BUF_DX), dev.buffer(L.BUF_DY)
+    dY = inst.flat_to_blocks(dev.buffer(L.BUF_DYMAT), bi)
+    dX = inst.flat_to_blocks(dev.buffer(L.BUF_DXMAT), bi)
+    Pm = inst.flat_to_blocks(dev.buffer(L.BUF_P), bi)
+    p, d = dev.buffer(L.BUF_PVEC), dev.buffer(L.BUF_DVEC)
+    Bst = oracle.stack_B(cons)
+    assert rel_err(Bst.T @ dx, p, np.abs(b).max()) < 1e-9
+    lhs = oracle.trace_A(ar, cons, dY, bi) + Bst @ dy
+    assert rel_err(lhs, d, np.abs(oracle.stack_c(cons)).max()) < 1e-8
+    WA = oracle.compute_weighted_A(ar, cons, dx, bi)
+    for j in range(0, bi.J, 7):
+        assert rel_err(dX[j][0], WA[j][0] + Pm[j][0]) < 1e-12
+    dev.close()

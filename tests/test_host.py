@@ -1,0 +1,96 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every symbol of
+include/clrsdp.h (no compute call without a GPU), limb splitting, layouts, the balancer."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol(pk):
+    hdr = open(os.path.join(ROOT, "include", "clrsdp.h")).read()
+    declared = sorted(set(re.findall(r"\b(clrsdp_[a-z_]+)\s*\(", hdr)))
+    assert "clrsdp_iterate" in declared and len(declared) >= 15
+    lib = pk._lib.lib()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(pk._lib.EXPORTS) == declared
+    assert lib.clrsdp_version() >= 100
+
+
+def test_library_rejects_bad_arguments_without_gpu(pk):
+    """Argument validation happens before any HIP call, so it can run here."""
+    L = pk._lib
+    lib = L.lib()
+    h = ctypes.c_void_p()
+    assert lib.clrsdp_create(None, None, ctypes.byref(h)) == L.E_ARG
+    assert lib.clrsdp_iterate(None, None, 0, None) == L.E_ARG
+    assert b"null" in lib.clrsdp_last_error(None)
+    assert lib.clrsdp_destroy(None) == L.OK
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "clustered-low-rank-sdp-solver_amd")
+    for fn in os.listdir(pkg):
+        if fn.endswith(".py"):
+            src = open(os.path.join(pkg, fn)).read()
+            assert "oracle" not in re.sub(r'""".*?"""', "", src, flags=re.S).replace("# ", ""), fn
+
+
+def test_planar_limbs_are_exact(pk):
+    import mpmath
+    from clrsdp_amd.instance import to_planes
+    mpmath.mp.prec = 256
+    vals = np.array([mpmath.mpf(1) / 3, -mpmath.pi, mpmath.mpf("1e-40"), mpmath.mpf(0)],
+                    dtype=object)
+    for w in (1, 2, 4):
+        P = to_planes(vals, w).reshape(w, -1)
+        for i, v in enumerate(vals):
+            s = mpmath.mpf(0)
+            for q in range(w):
+                s += mpmath.mpf(P[q, i])
+            assert abs(s - v) <= abs(v) * mpmath.mpf(2) ** (-52 * w) + mpmath.mpf(1e-300)
+        if w > 1:  # limbs are non-overlapping: |lo| <= ulp(hi)/2
+            assert np.all(np.abs(P[1]) <= np.abs(P[0]) * 2.0 ** -52 + 1e-300)
+
+
+def test_flat_layout_matches_reference_hcat(pk):
+    """V of block (j,l) is the hcat of v_{j,l,k,rnk} in (k, rnk) order (MPMP.jl:1249-1254)."""
+    from clrsdp_amd.instance import flatten, concat_colmajor
+    cons, b = pk.synth(seed=2, J=2, delta=3, rank=1, n_y=2, m=2, L=2,
+                       ranks=[[1, 2, 0, 1, 1], [1, 1, 1, 1, 3]], N=5)
+    bi = pk.get_block_info(cons)
+    fl = flatten(cons, bi)
+    assert list(fl.ranks[:5]) == [1, 2, 0, 1, 1]
+    assert fl.V[0].shape == (3, 5) and fl.V[1].shape == (3, 7)
+    np.testing.assert_array_equal(fl.V[0][:, 2], cons[0].A[0][1][1])
+    assert fl.block_sizes == [6, 6, 6, 6]
+    allv = concat_colmajor(fl.V)
+    assert allv.size == sum(v.size for v in fl.V)
+
+
+def test_partition_clusters_balanced_and_complete(pk):
+    for cfg, world in [(dict(J=64, delta=8, rank=1, n_y=4), 8), (dict(J=7, delta=4, rank=1, n_y=2), 8),
+                       (dict(J=5, delta=4, rank=1, n_y=2), 2)]:
+        cons, b = pk.synth(seed=0, **cfg)
+        bi = pk.get_block_info(cons)
+        parts = pk.partition_clusters(bi, world)
+        assert len(parts) == world
+        assert sorted(c for p in parts for c in p) == list(range(bi.J))
+        if cfg["J"] % world == 0:
+            assert all(len(p) == cfg["J"] // world for p in parts)
+
+
+def test_bench_algorithmic_counts():
+    import bench
+    import _clrsdp_pkg
+    pk = _clrsdp_pkg.load()
+    cons, b = pk.synth(seed=0, J=2, delta=8, rank=1, n_y=4)
+    bi = pk.get_block_info(cons)
+    fl, by = bench.schur_flops_bytes(bi)
+    d, K, D = 8, 15, 15
+    assert fl == 2 * (4.0 * d * K * (d + K) + 8.0 * D * (D + 1) / 2)
+    assert by == 2 * 8 * (2 * d * d + d * K + K + D * (D + 1) / 2 + K)
