@@ -429,7 +429,7 @@ struct Solver final : HandleBase {
     info_S0 = nb();
     info_Q0 = nb() + nc();
     info_Y0 = nb() + nc() + 1;
-    info = dmalloc<int>(info_count);
+    info = dmalloc<int>(info_count + 1);  // + the OR of all entries (update guard)
     xcap = n_y * n_y + n_y + 16;
     own_send = dmalloc<T>(xcap);
     xsend = own_send;
@@ -943,11 +943,13 @@ struct Solver final : HandleBase {
     scalars(prm, pd_feas, 3);
   }
   void st_update(const clrsdp_params* prm, int pd_feas) {
-    if (nx > 0) vec_axpy_dev<T><<<cdiv(nx, 256), 256, 0, stream>>>(x, dx, sc + SC_ALPHA_P, nx);
-    vec_axpy_dev<T><<<cdiv(n_y, 256), 256, 0, stream>>>(y, dyv, sc + SC_ALPHA_D, n_y);
+    int* flag = info + info_count;
+    status_reduce<<<1, 256, 0, stream>>>(info, info_count, flag);
+    if (nx > 0) vec_axpy_dev<T><<<cdiv(nx, 256), 256, 0, stream>>>(x, dx, sc + SC_ALPHA_P, nx, flag);
+    vec_axpy_dev<T><<<cdiv(n_y, 256), 256, 0, stream>>>(y, dyv, sc + SC_ALPHA_D, n_y, flag);
     if (nb()) {
-      blk_axpy_dev<T><<<nb(), 256, 0, stream>>>(d_blk, X, dX, sc + SC_ALPHA_P);
-      blk_axpy_dev<T><<<nb(), 256, 0, stream>>>(d_blk, Y, dY, sc + SC_ALPHA_D);
+      blk_axpy_dev<T><<<nb(), 256, 0, stream>>>(d_blk, X, dX, sc + SC_ALPHA_P, flag);
+      blk_axpy_dev<T><<<nb(), 256, 0, stream>>>(d_blk, Y, dY, sc + SC_ALPHA_D, flag);
     }
     objectives(prm, pd_feas);
   }

@@ -614,9 +614,22 @@ __global__ void blk_axpby(const BlkDesc* __restrict__ bd, T* out, const T* X, co
   }
 }
 
-// X += alpha * dX with alpha = *sc
+// *flag = OR of info[0..n): a failed factorisation anywhere in this iteration
+__global__ void status_reduce(const int* info, int n, int* flag) {
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    if (info[i]) atomicOr(&any, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = any;
+}
+
+// X += alpha * dX with alpha = *sc  (skipped when *flag != 0: the state survives a failed step)
 template <class T>
-__global__ void blk_axpy_dev(const BlkDesc* __restrict__ bd, T* X, const T* dX, const T* sc) {
+__global__ void blk_axpy_dev(const BlkDesc* __restrict__ bd, T* X, const T* dX, const T* sc,
+                             const int* flag) {
+  if (*flag) return;
   const BlkDesc B = bd[blockIdx.x];
   const int nn = B.n * B.n;
   const T a = *sc;
@@ -746,9 +759,9 @@ __global__ void vec_fill(T* out, double v, long long n) {
 
 // x += (*sc) * dx
 template <class T>
-__global__ void vec_axpy_dev(T* x, const T* dx, const T* sc, long long n) {
+__global__ void vec_axpy_dev(T* x, const T* dx, const T* sc, long long n, const int* flag) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
+  if (e >= n || *flag) return;
   x[e] = x[e] + (*sc) * dx[e];
 }
 

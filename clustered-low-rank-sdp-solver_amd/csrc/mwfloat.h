@@ -15,21 +15,28 @@
 #include <cstdint>
 
 #define MW_HD __host__ __device__ __forceinline__
+// Error-free transformations must not be contracted into FMAs by the compiler (hipcc's default
+// -ffp-contract=fast-honor-pragmas would fuse e.g. `a.hi*b.hi + p2` inside quick_two_sum and
+// silently lose the low word).  Every multi-word function body starts with this pragma.
+#define MW_EXACT _Pragma("clang fp contract(off)")
 
 namespace mw {
 
 MW_HD double two_sum(double a, double b, double& err) {
+  MW_EXACT
   double s = a + b;
   double bb = s - a;
   err = (a - (s - bb)) + (b - bb);
   return s;
 }
 MW_HD double quick_two_sum(double a, double b, double& err) {
+  MW_EXACT
   double s = a + b;
   err = b - (s - a);
   return s;
 }
 MW_HD double two_prod(double a, double b, double& err) {
+  MW_EXACT
   double p = a * b;
   err = fma(a, b, -p);
   return p;
@@ -43,6 +50,7 @@ struct dd {
 };
 
 MW_HD dd operator+(const dd& a, const dd& b) {
+  MW_EXACT
   double s2, t2;
   double s1 = two_sum(a.hi, b.hi, s2);
   double t1 = two_sum(a.lo, b.lo, t2);
@@ -52,9 +60,12 @@ MW_HD dd operator+(const dd& a, const dd& b) {
   s1 = quick_two_sum(s1, s2, s2);
   return dd(s1, s2);
 }
-MW_HD dd operator-(const dd& a) { return dd(-a.hi, -a.lo); }
-MW_HD dd operator-(const dd& a, const dd& b) { return a + (-b); }
+MW_HD dd operator-(const dd& a) {
+  MW_EXACT return dd(-a.hi, -a.lo); }
+MW_HD dd operator-(const dd& a, const dd& b) {
+  MW_EXACT return a + (-b); }
 MW_HD dd operator*(const dd& a, const dd& b) {
+  MW_EXACT
   double p2;
   double p1 = two_prod(a.hi, b.hi, p2);
   p2 = fma(a.hi, b.lo, p2);
@@ -63,6 +74,7 @@ MW_HD dd operator*(const dd& a, const dd& b) {
   return dd(p1, p2);
 }
 MW_HD dd operator*(const dd& a, double b) {
+  MW_EXACT
   double p2;
   double p1 = two_prod(a.hi, b, p2);
   p2 = fma(a.lo, b, p2);
@@ -70,6 +82,7 @@ MW_HD dd operator*(const dd& a, double b) {
   return dd(p1, p2);
 }
 MW_HD dd operator/(const dd& a, const dd& b) {
+  MW_EXACT
   // long division: q1 = a/b, r = a - q1 b, q2 = r/b, r -= q2 b, q3 = r/b
   double q1 = a.hi / b.hi;
   dd r = a - b * q1;
@@ -80,18 +93,29 @@ MW_HD dd operator/(const dd& a, const dd& b) {
   q1 = quick_two_sum(q1, q2, e);
   return dd(q1, e) + dd(q3);
 }
-MW_HD dd& operator+=(dd& a, const dd& b) { a = a + b; return a; }
-MW_HD dd& operator-=(dd& a, const dd& b) { a = a - b; return a; }
-MW_HD dd& operator*=(dd& a, const dd& b) { a = a * b; return a; }
-MW_HD dd& operator/=(dd& a, const dd& b) { a = a / b; return a; }
-MW_HD bool operator<(const dd& a, const dd& b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
-MW_HD bool operator>(const dd& a, const dd& b) { return b < a; }
-MW_HD bool operator<=(const dd& a, const dd& b) { return !(b < a); }
-MW_HD bool operator>=(const dd& a, const dd& b) { return !(a < b); }
-MW_HD bool operator==(const dd& a, const dd& b) { return a.hi == b.hi && a.lo == b.lo; }
-MW_HD bool operator!=(const dd& a, const dd& b) { return !(a == b); }
+MW_HD dd& operator+=(dd& a, const dd& b) {
+  MW_EXACT a = a + b; return a; }
+MW_HD dd& operator-=(dd& a, const dd& b) {
+  MW_EXACT a = a - b; return a; }
+MW_HD dd& operator*=(dd& a, const dd& b) {
+  MW_EXACT a = a * b; return a; }
+MW_HD dd& operator/=(dd& a, const dd& b) {
+  MW_EXACT a = a / b; return a; }
+MW_HD bool operator<(const dd& a, const dd& b) {
+  MW_EXACT return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
+MW_HD bool operator>(const dd& a, const dd& b) {
+  MW_EXACT return b < a; }
+MW_HD bool operator<=(const dd& a, const dd& b) {
+  MW_EXACT return !(b < a); }
+MW_HD bool operator>=(const dd& a, const dd& b) {
+  MW_EXACT return !(a < b); }
+MW_HD bool operator==(const dd& a, const dd& b) {
+  MW_EXACT return a.hi == b.hi && a.lo == b.lo; }
+MW_HD bool operator!=(const dd& a, const dd& b) {
+  MW_EXACT return !(a == b); }
 
 MW_HD dd sqrt_dd(const dd& a) {
+  MW_EXACT
   if (!(a.hi > 0.0)) return dd(a.hi == 0.0 ? 0.0 : NAN);
   // one Newton step on x = sqrt(a.hi):  sqrt(a) ~ x + (a - x^2) / (2x)
   double x = sqrt(a.hi);

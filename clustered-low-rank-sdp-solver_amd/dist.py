@@ -2,9 +2,9 @@
 torch.distributed (backend "nccl" = RCCL over xGMI on ROCm; "gloo" for CPU-side tests).
 
 The library (include/clrsdp.h) calls the registered exchange in the middle of a stage with its
-work enqueued on `stream`; here that stream is torch's current stream, so an RCCL all-gather on
-it is ordered after the partials were written and before their rank-ordered reduction, with no
-host synchronisation.  Payloads are the few cross-cluster quantities of one iteration (Q:
+work enqueued on its own stream; the collective is issued on that same stream (wrapped as a
+torch ExternalStream), so an RCCL all-gather is ordered after the partials were written and
+before their rank-ordered reduction, with no host synchronisation.  Payloads are the few cross-cluster quantities of one iteration (Q:
 n_y^2 words, three n_y-vectors, ~10 scalars), so the exchange is latency-bound.
 """
 from __future__ import annotations
@@ -35,21 +35,25 @@ class TorchExchange:
         nbytes = dev.exchange_bytes()
         self.send = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
         self.recv = torch.zeros(nbytes * self.world, dtype=torch.uint8, device="cuda")
-        dev.set_stream(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        self.stream = torch.cuda.ExternalStream(dev.stream_ptr())
         dev.set_exchange(self._exchange, self.send.data_ptr(), self.recv.data_ptr())
         self.dev = dev
 
     def _exchange(self, ctx, tag, nbytes, stream):
         try:
             w = self.world
-            if self.backend == "nccl":
-                self.dist.all_gather_into_tensor(self.recv[:nbytes * w], self.send[:nbytes])
-            else:  # host staging for gloo (tests on a single GPU)
-                self.torch.cuda.current_stream().synchronize()
-                src = self.send[:nbytes].cpu()
-                outs = [self.torch.empty_like(src) for _ in range(w)]
-                self.dist.all_gather(outs, src)
-                self.recv[:nbytes * w].copy_(self.torch.cat(outs).to("cuda"))
+            torch = self.torch
+            with torch.cuda.stream(self.stream):
+                if self.backend == "nccl":
+                    self.dist.all_gather_into_tensor(self.recv[:nbytes * w], self.send[:nbytes])
+                else:  # host staging for gloo (tests on a single GPU)
+                    self.stream.synchronize()
+                    src = self.send[:nbytes].cpu()
+                    outs = [torch.empty_like(src) for _ in range(w)]
+                    self.dist.all_gather(outs, src)
+                    self.recv[:nbytes * w].copy_(torch.cat(outs).to("cuda"))
+                    self.stream.synchronize()
             return 0
         except Exception as e:  # never let an exception cross the C ABI
             print(f"[clrsdp exchange tag {tag}] {e!r}", flush=True)

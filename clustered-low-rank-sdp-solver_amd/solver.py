@@ -179,6 +179,10 @@ class DeviceSolver:
     def set_stream(self, stream_ptr: int):
         self.check(self.L.clrsdp_set_stream(self.h, C.c_void_p(stream_ptr)))
 
+    def stream_ptr(self) -> int:
+        """The hipStream_t every launch of this handle goes to."""
+        return self.L.clrsdp_get_stream(self.h) or 0
+
     def exchange_bytes(self) -> int:
         b = C.c_int64()
         self.check(self.L.clrsdp_exchange_bytes(self.h, C.byref(b)))
