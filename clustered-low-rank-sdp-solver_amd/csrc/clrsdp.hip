@@ -64,8 +64,8 @@ inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) /
 // register-tile shapes of chol_inv_reg per word type (NMAX = TR * GR)
 template <class T> struct RegCfg { static constexpr int TR = 4, TC = 8, GR = 32, GC = 16; };
 template <> struct RegCfg<dd> { static constexpr int TR = 2, TC = 4, GR = 32, GC = 16; };
-template <class T> constexpr int reg_nmax() { return RegCfg<T>::TR * RegCfg<T>::GR; }
-template <class T> size_t eig_lds_bytes(int n) { return sizeof(T) * ((size_t)n * n + 8 * (size_t)n + 16); }
+template <class T> constexpr int reg_nmax() { return std::is_same<T, double>::value ? 128 : RegCfg<T>::TR * RegCfg<T>::GR; }
+template <class T> size_t eig_lds_bytes(int n) { return sizeof(T) * ((size_t)n * n + 10 * (size_t)n + 40); }
 constexpr size_t LDS_MAX = 160 * 1024;
 
 template <class T>
@@ -194,6 +194,7 @@ struct CholInvPlan {  // A_b -> L_b^-1 (and optionally L_b)
   void add(T* A, int n, int lda, T* out, int ldo, T* L = nullptr) {
     hin.push_back(MatDesc<T>{A, n, lda});
     hout.push_back(MatDesc<T>{out, n, ldo});
+    nmax = std::max(nmax, n);
     if (L) hl.push_back(MatDesc<T>{L, n, ldo});
   }
   void finalize() {
@@ -202,11 +203,30 @@ struct CholInvPlan {  // A_b -> L_b^-1 (and optionally L_b)
     dout = upload_vec(hout);
     if (!hl.empty()) dl = upload_vec(hl);
   }
+  int nmax = 0;
   void launch(hipStream_t s, int* info) const {
     if (hin.empty()) return;
-    using C = RegCfg<T>;
-    chol_inv_reg<T, C::TR, C::TC, C::GR, C::GC><<<(unsigned)hin.size(), C::GR * C::GC, 0, s>>>(din, dout, dl, info);
+    const unsigned nb = (unsigned)hin.size();
+    if constexpr (std::is_same<T, double>::value) {
+      if (nmax <= 32) go<32>(s, nb, info);
+      else if (nmax <= 64) go<64>(s, nb, info);
+      else go<128>(s, nb, info);
+    } else {
+      using C = RegCfg<T>;
+      chol_inv_reg<T, C::TR, C::TC, C::GR, C::GC><<<nb, C::GR * C::GC, 0, s>>>(din, dout, dl, info);
+    }
     HIPCHK(hipGetLastError());
+  }
+  template <int NP>
+  void go(hipStream_t s, unsigned nb, int* info) const {
+    static bool attr = false;
+    if (!attr) {
+      HIPCHK(hipFuncSetAttribute((const void*)chol_inv_mfma<NP>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX));
+      attr = true;
+    }
+    chol_inv_mfma<NP><<<nb, 512, chol_inv_mfma_lds<NP>(), s>>>(
+        reinterpret_cast<const MatDesc<double>*>(din), reinterpret_cast<const MatDesc<double>*>(dout), info);
   }
 };
 
@@ -249,13 +269,14 @@ struct Solver final : HandleBase {
   std::vector<int64_t> c_xoff, c_Soff, c_Boff;   // per local cluster
   int64_t nx = 0, nblk_el = 0, nV = 0, nK = 0, nT = 0, nBX = 0, nAY = 0, nS = 0, nB = 0, nRS = 0;
   bool anyMgt1 = false, hasC = false;
+  int nc2 = 0;  // clusters factorised as 2x2 blocks (128 < dim_S <= 256, fp64)
 
   // ---------------- device memory
   hipStream_t own_stream = nullptr, stream = nullptr;
   T *X, *Y, *Xinv, *LX, *LY, *R, *P, *dX, *dY, *Z, *tA, *tB, *Cm;
   T *V, *lam, *TX, *TY, *BX, *BY, *AY, *tval, *S, *Wm, *Bm, *Qslab, *Q, *Qf;
   T *cvec, *x, *dx, *dvec, *rhs, *tvec, *tmpv, *pslab, *y, *bvec, *dyv, *pvec, *uvec;
-  T *sc, *bpart, *eigX, *eigY, *tmpsc;
+  T *sc, *bpart, *eigX, *eigY, *tmpsc, *tC = nullptr, *Stmp = nullptr;
   int *ksamp, *rsums, *info;
   T *xsend = nullptr, *xrecv = nullptr, *own_send = nullptr;
   int64_t xcap = 0;  // exchange capacity in T values
@@ -271,8 +292,12 @@ struct Solver final : HandleBase {
   MatPlan<T> f_X, f_Y, f_S, f_Q, e_X, e_Y;
   // on-chip factorisation path (all sizes <= reg_nmax<T>()): L^-1 and MFMA products
   bool reg_blk = false, reg_S = false, reg_Q = false;
-  CholInvPlan<T> ci_X, ci_Y, ci_S, ci_Q;
+  CholInvPlan<T> ci_XY, ci_S, ci_S11, ci_S22, ci_Q;
   GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2;
+  GemmPlan<T> q_L21, q_S22, q_M, q_X21;  // 2x2 blocked L^-1 of S (dim_S in (128, 256])
+  MatPlan<T> e_XY;                        // both step-length eigenproblems in one launch
+  RectDesc* d_zero = nullptr;            // upper-right blocks of the 2x2 S factors
+  int n_zero = 0;
   BlkDesc* d_blk = nullptr;      // all local blocks
   BlkDesc* d_blk_m = nullptr;    // local blocks with m > 1
   int n_blk_m = 0;
@@ -360,6 +385,7 @@ struct Solver final : HandleBase {
       nS += Ds[j] * Ds[j];
       c_Boff.push_back(nB);
       nB += Ds[j] * n_y;
+      if (std::is_same<T, double>::value && Ds[j] > 128 && Ds[j] <= 256) ++nc2;
       if (m[j] > 1) anyMgt1 = true;
       for (int l = 0; l < Lc[j]; ++l) {
         LBlk b;
@@ -388,7 +414,7 @@ struct Solver final : HandleBase {
     // device memory is released with the process / hipDeviceReset; free what we own explicitly
     T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, BX, BY, AY,
                  tval, S, Wm, Bm, Qslab, Q, Qf, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
-                 bvec, dyv, pvec, uvec, sc, bpart, eigX, eigY, tmpsc, own_send};
+                 bvec, dyv, pvec, uvec, sc, bpart, eigX, tmpsc, tC, Stmp, own_send};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
     (void)hipFree(ksamp);
@@ -420,15 +446,23 @@ struct Solver final : HandleBase {
     uvec = dmalloc<T>(n_y);
     sc = dmalloc<T>(SC_COUNT);
     bpart = dmalloc<T>(std::max(nb(), 1));
-    eigX = dmalloc<T>(std::max(nb(), 1));
-    eigY = dmalloc<T>(std::max(nb(), 1));
+    eigX = dmalloc<T>(2 * std::max(nb(), 1));
+    eigY = eigX + std::max(nb(), 1);  // X-side and Y-side minima of one batched eigen launch
+    tC = dmalloc<T>(B);
+    {
+      int64_t ns = 0;
+      for (int c = 0; c < nc(); ++c)
+        if (std::is_same<T, double>::value && Ds[oc[c]] > 128 && Ds[oc[c]] <= 256) ns += 2 * (Ds[oc[c]] - 128) * 128;
+      Stmp = dmalloc<T>(ns);
+    }
     tmpsc = dmalloc<T>(8);
     ksamp = dmalloc<int>(nK);
     rsums = dmalloc<int>(nRS);
-    info_count = nb() + nc() + 1 + nb();
-    info_S0 = nb();
-    info_Q0 = nb() + nc();
-    info_Y0 = nb() + nc() + 1;
+    // info layout: [X: nb][Y: nb][S: nc single + nc2 second blocks][Q: 1]
+    info_count = 2 * nb() + nc() + nc2 + 1;
+    info_Y0 = nb();
+    info_S0 = 2 * nb();
+    info_Q0 = 2 * nb() + nc() + nc2;
     info = dmalloc<int>(info_count + 1);  // + the OR of all entries (update guard)
     xcap = n_y * n_y + n_y + 16;
     own_send = dmalloc<T>(xcap);
@@ -456,11 +490,13 @@ struct Solver final : HandleBase {
       for (const LBlk& b : lb) nmax_b = std::max(nmax_b, b.n);
       for (int c = 0; c < nc(); ++c) nmax_S = std::max(nmax_S, (int)Ds[oc[c]]);
       reg_blk = nmax_b <= reg_nmax<T>();
-      reg_S = nmax_S <= reg_nmax<T>();
+      reg_S = nmax_S <= (std::is_same<T, double>::value ? 2 : 1) * reg_nmax<T>();
       reg_Q = n_y <= reg_nmax<T>();
     }
     q_xinv.ta = true;
     q_sx2.tb = q_sy2.tb = true;
+    q_L21.tb = true;
+    q_S22.tb = true;
     q_dx.ta = true;
     q_q2.ta = true;
     p_xinv.ta = true;
@@ -492,15 +528,15 @@ struct Solver final : HandleBase {
       t_sY2.add(LY + b.off, n, tB + b.off, n, n, n);
       f_X.add(LX + b.off, n, n);
       f_Y.add(LY + b.off, n, n);
-      ci_X.add(X + b.off, n, n, LX + b.off, n);
-      ci_Y.add(Y + b.off, n, n, LY + b.off, n);
+      ci_XY.add(X + b.off, n, n, LX + b.off, n);
       q_xinv.add(LX + b.off, n, LX + b.off, n, nullptr, n, Xinv + b.off, n, n, n, n);
       q_sx1.add(LX + b.off, n, dX + b.off, n, nullptr, n, tA + b.off, n, n, n, n);
       q_sx2.add(tA + b.off, n, LX + b.off, n, nullptr, n, tB + b.off, n, n, n, n);
       q_sy1.add(LY + b.off, n, dY + b.off, n, nullptr, n, tA + b.off, n, n, n, n);
-      q_sy2.add(tA + b.off, n, LY + b.off, n, nullptr, n, tB + b.off, n, n, n, n);
+      q_sy2.add(tA + b.off, n, LY + b.off, n, nullptr, n, tC + b.off, n, n, n, n);
       e_X.add(tB + b.off, n, n);
       e_Y.add(tB + b.off, n, n);
+      e_XY.add(tB + b.off, n, n);
       const int ldT = n;           // TX_b is (m delta) x (m K)
       const int ldBX = mm * K;     // BX_b is (m K) x (m K)
       for (int s = 0; s < mm; ++s) {
@@ -540,6 +576,8 @@ struct Solver final : HandleBase {
                       dX + b.off + s * del + (int64_t)r * del * n, n, del, del, K);
         }
     }
+    for (const LBlk& b : lb) ci_XY.add(Y + b.off, b.n, b.n, LY + b.off, b.n);
+    for (const LBlk& b : lb) e_XY.add(tC + b.off, b.n, b.n);
     n_blk_m = (int)bdm.size();
     d_blk = upload_vec(bd);
     if (n_blk_m) d_blk_m = upload_vec(bdm);
@@ -553,6 +591,8 @@ struct Solver final : HandleBase {
     std::vector<TupleDesc> td;
     std::vector<TupleBlock> tbk;
     int bi = 0;
+    int64_t s2off = 0;
+    std::vector<RectDesc> zr;
     for (int c = 0; c < nc(); ++c) {
       const int j = oc[c];
       const int D = (int)Ds[j];
@@ -561,7 +601,24 @@ struct Solver final : HandleBase {
       T* Bc = Bm + c_Boff[c];
       const int64_t xo = c_xoff[c];
       f_S.add(Sc, D, D);
-      ci_S.add(Sc, D, D, Sc, D);
+      if (!std::is_same<T, double>::value || D <= 128) {
+        ci_S.add(Sc, D, D, Sc, D);
+      } else if (D <= 256) {
+        const int D1 = 128, D2 = D - 128;
+        T* S11 = Sc;
+        T* S21 = Sc + D1;
+        T* S22 = Sc + D1 + (int64_t)D1 * D;
+        T* T21 = Stmp + s2off;
+        T* T21b = T21 + (int64_t)D2 * D1;
+        s2off += 2 * (int64_t)D2 * D1;
+        ci_S11.add(S11, D1, D, S11, D);                                       // S11 <- L11^-1
+        q_L21.add(S21, D, S11, D, nullptr, 0, T21, D2, D2, D1, D1);           // L21 = S21 L11^-T
+        q_S22.add(T21, D2, T21, D2, S22, D, S22, D, D2, D2, D1);             // S22 -= L21 L21^T
+        ci_S22.add(S22, D2, D, S22, D);                                       // S22 <- L22^-1
+        q_M.add(S22, D, T21, D2, nullptr, 0, T21b, D2, D2, D1, D2);           // M = L22^-1 L21
+        q_X21.add(T21b, D2, S11, D, nullptr, 0, S21, D, D2, D1, D1);          // S21 <- -M L11^-1
+        zr.push_back(RectDesc{Sc + (int64_t)D1 * D, D1, D2, D});             // S12 <- 0
+      }
       q_W.add(Sc, D, Bc, D, nullptr, 0, Wc, D, D, (int)n_y, D);
       q_t.add(Sc, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D, 1, D);
       q_Wdy.add(Wc, D, dyv, (int)n_y, tvec + xo, D, tmpv + xo, D, D, 1, (int)n_y);
@@ -600,6 +657,8 @@ struct Solver final : HandleBase {
     ci_Q.add(Q, (int)n_y, (int)n_y, Qf, (int)n_y);
     q_q1.add(Qf, (int)n_y, dyv, (int)n_y, nullptr, 0, uvec, (int)n_y, (int)n_y, 1, (int)n_y);
     q_q2.add(Qf, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
+    n_zero = (int)zr.size();
+    if (n_zero) d_zero = upload_vec(zr);
     if (nc()) {
       d_scd = upload_vec(scd);
       d_sbd = upload_vec(sbd);
@@ -609,9 +668,10 @@ struct Solver final : HandleBase {
     for (GemmPlan<T>* g : {&p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
-                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2})
+                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_L21, &q_S22, &q_M, &q_X21})
       g->finalize();
-    for (CholInvPlan<T>* c : {&ci_X, &ci_Y, &ci_S, &ci_Q}) c->finalize();
+    for (CholInvPlan<T>* c : {&ci_XY, &ci_S, &ci_S11, &ci_S22, &ci_Q}) c->finalize();
+    e_XY.finalize();
     for (TrsmPlan<T>* t : {&t_Linv, &t_W, &t_t, &t_Q, &t_sX1, &t_sX2, &t_sY1, &t_sY2, &t_dx})
       t->finalize();
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q, &e_X, &e_Y}) f->finalize();
@@ -770,8 +830,8 @@ struct Solver final : HandleBase {
     blk_lin(R, R, 1.0, nullptr, 0.0, sc + SC_MU_P);  // R += mu_p I
   }
   void st_xinv() {
-    if (reg_blk) {                            // L_X^-1 on chip, X^-1 = L^-T L^-1 on MFMA
-      ci_X.launch(stream, info);
+    if (reg_blk) {  // L_X^-1 and L_Y^-1 on chip in one launch, X^-1 = L^-T L^-1 on MFMA
+      ci_XY.launch(stream, info);
       q_xinv.launch(stream, 1.0, 0.0);
       return;
     }
@@ -794,6 +854,17 @@ struct Solver final : HandleBase {
   void st_factor() {
     if (reg_S) {                              // S_j <- L_j^-1 in place; W_j = L_j^-1 B_j (MFMA)
       ci_S.launch(stream, info + info_S0);
+      if (nc2) {                              // 2x2 blocked L^-1 for 128 < dim_S <= 256
+        const int n1 = (int)ci_S.hin.size();
+        ci_S11.launch(stream, info + info_S0 + n1);
+        q_L21.launch(stream, 1.0, 0.0);
+        q_S22.launch(stream, -1.0, 1.0);
+        ci_S22.launch(stream, info + info_S0 + n1 + nc2);
+        q_M.launch(stream, 1.0, 0.0);
+        q_X21.launch(stream, -1.0, 0.0);
+        dim3 g(16, n_zero);
+        rect_fill<T><<<g, 256, 0, stream>>>(d_zero, 0.0);
+      }
       q_W.launch(stream, 1.0, 0.0);
     } else {
       f_S.potrf(stream, info + info_S0);
@@ -896,14 +967,12 @@ struct Solver final : HandleBase {
   }
   void st_step(const clrsdp_params* prm, int pd_feas) {
     if (reg_blk) {
-      // X: L_X^-1 from the X^-1 stage;  M = L^-1 dX L^-T on MFMA
+      // L_X^-1, L_Y^-1 from the X^-1 stage;  M = L^-1 dM L^-T on MFMA; one eigen launch
       q_sx1.launch(stream, 1.0, 0.0);
       q_sx2.launch(stream, 1.0, 0.0);
-      e_X.eigmin(stream, eigX);
-      ci_Y.launch(stream, info + info_Y0);
       q_sy1.launch(stream, 1.0, 0.0);
       q_sy2.launch(stream, 1.0, 0.0);
-      e_Y.eigmin(stream, eigY);
+      e_XY.eigmin(stream, eigX);
     } else {
       // X: L_X from the X^-1 stage
       blk_lin(tA, dX, 1.0, nullptr, 0.0);
@@ -977,7 +1046,7 @@ struct Solver final : HandleBase {
     HIPCHK(hipStreamSynchronize(stream));
     for (int i = 0; i < nb(); ++i)
       if (h[i]) { err = "X block not positive definite (spd_inv! failed)"; return CLRSDP_E_NOT_PD_X; }
-    for (int i = 0; i < nc(); ++i)
+    for (int i = 0; i < nc() + nc2; ++i)
       if (h[info_S0 + i]) { err = "S was not decomposed succesfully, try again with higher precision"; return CLRSDP_E_NOT_PD_S; }
     if (h[info_Q0]) { err = "Q was not decomposed correctly. Try restarting with a higher precision."; return CLRSDP_E_NOT_PD_Q; }
     for (int i = 0; i < nb(); ++i)

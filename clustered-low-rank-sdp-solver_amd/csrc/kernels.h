@@ -750,6 +750,19 @@ __global__ void vec_lin(T* out, const T* x, double a, const T* y, double b, cons
   out[e] = v;
 }
 
+// fill rectangles (rows x cols, column-major with ld) with v; blockIdx.y = rectangle
+struct RectDesc {
+  void* p;
+  int rows, cols, ld;
+};
+template <class T>
+__global__ void rect_fill(const RectDesc* __restrict__ rd, double v) {
+  const RectDesc R = rd[blockIdx.y];
+  T* p = reinterpret_cast<T*>(R.p);
+  for (int c = blockIdx.x; c < R.cols; c += gridDim.x)
+    for (int r = threadIdx.x; r < R.rows; r += blockDim.x) p[r + (size_t)c * R.ld] = T(v);
+}
+
 // out[0..n) = v
 template <class T>
 __global__ void vec_fill(T* out, double v, long long n) {

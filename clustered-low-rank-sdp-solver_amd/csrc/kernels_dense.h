@@ -179,9 +179,23 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
 // is symmetrised into LDS (ld = n), tridiagonalised by Householder reflections (full storage),
 // then one wave runs a 64-point Sturm multisection.
 // ------------------------------------------------------------------------------------------
+#ifdef CLRSDP_EIG_STAMPS
+__device__ unsigned long long g_eig_stamps[8];
+#define EIG_STAMP(slot)                                                     \
+  if (tid == 0) {                                                           \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                   \
+    atomicAdd(&g_eig_stamps[slot], t_ - t_prev);                           \
+    t_prev = t_;                                                            \
+  }
+#else
+#define EIG_STAMP(slot)
+#endif
 template <class T>
 __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__ descs,
                                                   T* __restrict__ out) {
+#ifdef CLRSDP_EIG_STAMPS
+  unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#endif
   constexpr int NT = 512, NW = 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const MatDesc<T> d = descs[blockIdx.x];
@@ -191,65 +205,102 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
   T* p = v + n;                            // 4 * n partials, then p
   T* dg = p + 4 * n;                       // n
   T* e2 = dg + n;                          // n
-  T* red = e2 + n;                         // NW + 4
-  for (int e = tid; e < n * n; e += NT) {
-    const int i = e % n, j = e / n;
-    A[e] = (d.A[i + (size_t)j * d.lda] + d.A[j + (size_t)i * d.lda]) * T(0.5);
-  }
+  T* red = e2 + 3 * n + 12;                // NW + 4 (after w, scalars and partials)
+  // 2-D thread map (no integer division in the element loops): ti = tid % 32, tj = tid / 32
+  const int ti = tid & 31, tj = tid >> 5;
+  for (int j = tj; j < n; j += NT / 32)
+    for (int i = ti; i < n; i += 32)
+      A[i + (size_t)j * n] = (d.A[i + (size_t)j * d.lda] + d.A[j + (size_t)i * d.lda]) * T(0.5);
   __syncthreads();
+  T* Wv = e2 + n;        // w vector (n)            -- carved after e2
+  T* scal = Wv + n;      // [0] = beta, [1] = tail flag
+  T* redw = scal + 4;    // NW partials of v^T A' v
   for (int k = 0; k + 2 < n; ++k) {
     const int m = n - k - 1;
     T* Ak = A + (k + 1) + (size_t)(k + 1) * n;  // trailing m x m, ld n
-    T s = T(0.0);
-    for (int i = tid; i < m; i += NT) {
-      const T xi = A[(k + 1 + i) + (size_t)k * n];
-      v[i] = xi;
-      s += xi * xi;
-    }
-    s = block_sum_w<T, NW>(s, red);
-    const T x0 = v[0];
-    if (tid == 0) dg[k] = A[k + (size_t)k * n];
-    const T tail = s - x0 * x0;
-    if (!(tail > T(0.0))) {
-      if (tid == 0) e2[k] = x0 * x0;
-      __syncthreads();
-      continue;
-    }
-    const T nrm = Num<T>::sqrt_(s);
-    const T alpha = (x0 > T(0.0)) ? -nrm : nrm;
-    const T v0 = x0 - alpha;
-    const T beta = T(2.0) / (tail + v0 * v0);
-    if (tid == 0) {
-      e2[k] = alpha * alpha;
-      v[0] = v0;
-    }
-    __syncthreads();
-    // p = beta A' v : thread (i, q) sums columns j = q, q+4, ... (4 partials per row)
-    {
-      const int i = tid & 127, q = tid >> 7;
-      for (int ii = i; ii < m; ii += 128) {
-        T acc = T(0.0);
-        for (int j = q; j < m; j += 4) acc += Ak[ii + (size_t)j * n] * v[j];
-        p[q * n + ii] = acc;
+    // ---- (A) wave 0: reflector of column k
+    if (tid < 64) {
+      T s = T(0.0);
+      for (int i = tid; i < m; i += 64) {
+        const T xi = A[(k + 1 + i) + (size_t)k * n];
+        v[i] = xi;
+        s += xi * xi;
+      }
+      s = wave_sum(s);
+      const T x0 = A[(k + 1) + (size_t)k * n];
+      const T tail = s - x0 * x0;
+      if (tid == 0) {
+        dg[k] = A[k + (size_t)k * n];
+        if (!(tail > T(0.0))) {
+          e2[k] = x0 * x0;
+          scal[0] = T(0.0);  // beta = 0: no reflection
+        } else {
+          const T nrm = Num<T>::sqrt_(s);
+          const T alpha = (x0 > T(0.0)) ? -nrm : nrm;
+          const T v0 = x0 - alpha;
+          e2[k] = alpha * alpha;
+          v[0] = v0;
+          scal[0] = T(2.0) / (tail + v0 * v0);
+        }
       }
     }
     __syncthreads();
-    T pv = T(0.0);
-    for (int i = tid; i < m; i += NT) {
-      const T pi = (p[i] + p[n + i] + p[2 * n + i] + p[3 * n + i]) * beta;
-      p[i] = pi;
-      pv += pi * v[i];
+    EIG_STAMP(0)
+    const T beta = scal[0];
+    if (beta == T(0.0)) continue;  // uniform: nothing to update
+    // ---- (B) partial rows of A'v (4 column classes) and v^T A' v
+    const int ri = tid & 127, cq = tid >> 7;
+    T vav = T(0.0);
+    for (int ii = ri; ii < m; ii += 128) {
+      T a0 = T(0.0), a1 = T(0.0), a2 = T(0.0), a3 = T(0.0);
+      int j = cq;
+      for (; j + 12 < m; j += 16) {
+        a0 += Ak[ii + (size_t)j * n] * v[j];
+        a1 += Ak[ii + (size_t)(j + 4) * n] * v[j + 4];
+        a2 += Ak[ii + (size_t)(j + 8) * n] * v[j + 8];
+        a3 += Ak[ii + (size_t)(j + 12) * n] * v[j + 12];
+      }
+      for (; j < m; j += 4) a0 += Ak[ii + (size_t)j * n] * v[j];
+      const T part = (a0 + a1) + (a2 + a3);
+      p[cq * n + ii] = part;
+      vav += part * v[ii];
     }
-    pv = block_sum_w<T, NW>(pv, red);
-    const T Kc = beta * pv * T(0.5);
-    for (int i = tid; i < m; i += NT) p[i] = p[i] - Kc * v[i];
+    EIG_STAMP(1)
+    vav = wave_sum(vav);
+    if ((tid & 63) == 0) redw[tid >> 6] = vav;
     __syncthreads();
-    for (int e = tid; e < m * m; e += NT) {
-      const int i = e % m, j = e / m;
-      Ak[i + (size_t)j * n] = Ak[i + (size_t)j * n] - (v[i] * p[j] + p[i] * v[j]);
+    EIG_STAMP(2)
+    // ---- (C) w = beta A'v - K v,  K = beta^2 v^T A' v / 2
+    {
+      T tot = redw[0];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) tot += redw[q];
+      const T Kc = beta * beta * tot * T(0.5);
+      for (int i = tid; i < m; i += NT)
+        Wv[i] = ((p[i] + p[n + i]) + (p[2 * n + i] + p[3 * n + i])) * beta - Kc * v[i];
     }
     __syncthreads();
+    EIG_STAMP(3)
+    // ---- (D) A' -= v w^T + w v^T
+    for (int ii = ri; ii < m; ii += 128) {
+      const T vi = v[ii], wi = Wv[ii];
+      int j = cq;
+      for (; j + 12 < m; j += 16) {
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) {
+          T* a = Ak + ii + (size_t)(j + u) * n;
+          *a = *a - (vi * Wv[j + u] + wi * v[j + u]);
+        }
+      }
+      for (; j < m; j += 4) {
+        T* a = Ak + ii + (size_t)j * n;
+        *a = *a - (vi * Wv[j] + wi * v[j]);
+      }
+    }
+    __syncthreads();
+    EIG_STAMP(4)
   }
+  EIG_STAMP(5)
   if (tid == 0) {
     if (n >= 2) {
       dg[n - 2] = A[(n - 2) + (size_t)(n - 2) * n];
@@ -304,3 +355,196 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
 }
 
 }  // namespace clrsdp
+
+namespace clrsdp {
+
+// ------------------------------------------------------------------------------------------
+// chol_inv_mfma: A = L L^T and L^-1 for n <= 128 (fp64), one 512-thread workgroup per matrix.
+// A lives in LDS (swizzled column-major, padded to a multiple of 16 with the identity); L^-1
+// lives in registers as v_mfma_f64_16x16x4 accumulator tiles (the lower 16x16 tiles are dealt
+// round-robin to the 8 waves).  Blocked right-looking over 16-column panels, 3 barriers each:
+//   (a) wave 0 factors the 16x16 diagonal block and inverts it (lane-per-row, shuffles);
+//   (b) panel L21 = A21 L11^-T and row block X_k <- L11^-1 X_k   (MFMA);
+//   (c) trailing A22 -= L21 L21^T and X_ik -= L21_i X_k           (MFMA).
+// An accumulator tile is directly the B operand of the next MFMA (register r of lane l holds
+// row (l>>4)+4r = the B-operand row of K-chunk r), so X never round-trips through LDS except the
+// one row block broadcast per panel.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int NP>
+struct CholLds {
+  // element (i, j) of the NP x NP column-major image; odd columns XOR row bit 4 so the two
+  // 16-lane halves of an operand read hit opposite bank halves
+  static __device__ __forceinline__ int idx(int i, int j) { return j * NP + (i ^ ((j & 1) << 4)); }
+};
+
+__device__ __forceinline__ void tile_of(int t, int& i, int& j) {
+  i = 0;
+  while ((i + 1) * (i + 2) / 2 <= t) ++i;
+  j = t - i * (i + 1) / 2;
+}
+
+template <int NP>
+__global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __restrict__ in,
+                                                     const MatDesc<double>* __restrict__ out_inv,
+                                                     int* __restrict__ info) {
+  constexpr int NT = NP / 16, NTILES = NT * (NT + 1) / 2, NW = 8, SLOTS = (NTILES + NW - 1) / NW;
+  constexpr int XLD = NP + 16;  // X row-block buffer: 16 x NP, padded rows
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  double* A = reinterpret_cast<double*>(smem_raw);  // NP * NP
+  double* Dinv = A + NP * NP;                         // 16 x 16, column-major
+  double* Xr = Dinv + 256;                            // 16 x XLD, row-major
+  int* flag = reinterpret_cast<int*>(Xr + 16 * XLD);
+  using LI = CholLds<NP>;
+  const MatDesc<double> d = in[blockIdx.x];
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nt = (n + 15) / 16;  // active tile rows
+  const int lr = lane & 15, lk = lane >> 4;
+  // ---- load A (lower triangle mirrored), identity padding
+  for (int j = tid >> 4; j < NP; j += 32)
+    for (int i = (tid & 15); i < NP; i += 16) {
+      double v;
+      if (i < n && j < n) v = (i >= j) ? d.A[i + (size_t)j * d.lda] : d.A[j + (size_t)i * d.lda];
+      else v = (i == j) ? 1.0 : 0.0;
+      A[LI::idx(i, j)] = v;
+    }
+  if (tid == 0) *flag = 0;
+  // ---- X accumulators: identity on diagonal tiles
+  d4 X[SLOTS];
+#pragma unroll
+  for (int q = 0; q < SLOTS; ++q) {
+    const int t = w + NW * q;
+    int ti = 0, tj = 0;
+    if (t < NTILES) tile_of(t, ti, tj);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X[q][r] = (t < NTILES && ti == tj && (lk + 4 * r) == lr) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  for (int k = 0; k < nt; ++k) {
+    const int k0 = 16 * k;
+    // ---------------- (a) diagonal block: wave 0, lane i < 16 holds row i
+    if (w == 0) {
+      double row[16], lin[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) row[c] = (lane < 16 && c <= lane) ? A[LI::idx(k0 + lane, k0 + c)] : 0.0;
+      int bad = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double djj = __shfl(row[j], j);
+        if (!(djj > 0.0)) bad = 1;
+        const double s = sqrt(djj);
+        const double lij = (lane == j) ? s : row[j] / s;
+        if (lane >= j) row[j] = lij;
+        // rank-1 update of the rows below: row[c] -= l_ij * l_cj for j < c <= i
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) {
+          const double lcj = __shfl(lij, c);
+          if (lane >= c) row[c] -= lij * lcj;
+        }
+      }
+      // inverse: lane c holds column c of L^-1 in lin[0..15]
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        double s = (lane == i) ? 1.0 : 0.0;
+#pragma unroll
+        for (int q = 0; q < i; ++q) s -= __shfl(row[q], i) * lin[q];
+        lin[i] = (lane <= i) ? s / __shfl(row[i], i) : 0.0;
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          A[LI::idx(k0 + lane, k0 + c)] = (c <= lane) ? row[c] : 0.0;
+          Dinv[lane * 16 + c] = lin[c];  // Dinv column `lane` = column lane of L^-1
+        }
+      }
+      if (lane == 0 && bad) *flag = k0 + 1;
+    }
+    __syncthreads();
+    if (*flag) break;
+    // ---------------- (b) panel and X row block
+    // Linv_kk operands: A-op  a[r] = Linv[lr][4r+lk]  (Dinv column-major: Dinv[c*16 + i])
+    //                   B-op of Linv^T: b[r] = Linv^T[4r+lk][lr] = Linv[lr][4r+lk]  (same value)
+    double lopA[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lopA[r] = Dinv[(4 * r + lk) * 16 + lr];
+#pragma unroll
+    for (int q = 0; q < SLOTS; ++q) {
+      const int t = w + NW * q;
+      if (t >= NTILES) continue;
+      int ti, tj;
+      tile_of(t, ti, tj);
+      if (ti >= nt) continue;
+      if (tj == k && ti > k) {  // panel tile: L21_i = A_ik Linv^T
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc = mfma64(A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)], lopA[r], acc);
+        // (B-op of Linv^T for K-chunk r: B[4r+lk][lr] = Linv[lr][4r+lk] = lopA[r])
+#pragma unroll
+        for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, k0 + lr)] = acc[r];
+      }
+      if (ti == k && tj <= k) {  // X_kj <- Linv_kk X_kj
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = mfma64(lopA[r], X[q][r], acc);
+        X[q] = acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Xr[(lk + 4 * r) * XLD + 16 * tj + lr] = acc[r];
+      }
+    }
+    __syncthreads();
+    // ---------------- (c) trailing updates
+#pragma unroll
+    for (int q = 0; q < SLOTS; ++q) {
+      const int t = w + NW * q;
+      if (t >= NTILES) continue;
+      int ti, tj;
+      tile_of(t, ti, tj);
+      if (ti >= nt || ti <= k) continue;
+      if (tj > k) {  // A_ij -= L21_i L21_j^T
+        d4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = A[LI::idx(16 * ti + lk + 4 * r, 16 * tj + lr)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc = mfma64(-A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)],
+                       A[LI::idx(16 * tj + lr, k0 + 4 * r + lk)], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, 16 * tj + lr)] = acc[r];
+      } else {  // X_ij -= L21_i X_kj  (tj <= k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          X[q] = mfma64(-A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)],
+                        Xr[(4 * r + lk) * XLD + 16 * tj + lr], X[q]);
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && info) info[blockIdx.x] = *flag;
+  // ---- write L^-1 (lower tiles from registers, zeros above)
+  const MatDesc<double> o = out_inv[blockIdx.x];
+#pragma unroll
+  for (int q = 0; q < SLOTS; ++q) {
+    const int t = w + NW * q;
+    if (t >= NTILES) continue;
+    int ti, tj;
+    tile_of(t, ti, tj);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = 16 * ti + lk + 4 * r, gj = 16 * tj + lr;
+      if (gi < n && gj < n) o.A[gi + (size_t)gj * o.lda] = X[q][r];
+    }
+  }
+  for (int j = tid >> 4; j < n; j += 32)
+    for (int i = (tid & 15); i < (j & ~15); i += 16) o.A[i + (size_t)j * o.lda] = 0.0;  // tiles above
+}
+
+template <int NP>
+size_t chol_inv_mfma_lds() { return sizeof(double) * ((size_t)NP * NP + 256 + 16 * (NP + 16)) + 16; }
+
+}  // namespace clrsdp
+
+

@@ -1,0 +1,96 @@
+// Standalone timing of the on-chip dense kernels (chol_inv_reg, eigmin_lds) on a batch of SPD
+// matrices, with a correctness spot check (||L^-1 A L^-T - I||, lambda_min vs power iteration).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cmath>
+#include "../../clustered-low-rank-sdp-solver_amd/csrc/kernels_dense.h"
+using namespace clrsdp;
+#define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP %s @%d\n",hipGetErrorString(e),__LINE__); exit(1);} }while(0)
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 128, nb = argc > 2 ? atoi(argv[2]) : 64;
+  std::vector<double> h((size_t)nb * n * n);
+  srand(1);
+  for (int b = 0; b < nb; ++b) {
+    std::vector<double> G((size_t)n * n);
+    for (auto& g : G) g = (rand() / (double)RAND_MAX - 0.5);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        double s = (i == j) ? 1.0 : 0.0;
+        for (int k = 0; k < n; ++k) s += G[i + k * n] * G[j + k * n] / n;
+        h[(size_t)b * n * n + i + j * n] = s;
+      }
+  }
+  double *dA, *dO, *dE;
+  CK(hipMalloc(&dA, h.size() * 8)); CK(hipMalloc(&dO, h.size() * 8)); CK(hipMalloc(&dE, nb * 8));
+  CK(hipMemcpy(dA, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  std::vector<MatDesc<double>> din(nb), dout(nb);
+  for (int b = 0; b < nb; ++b) { din[b] = {dA + (size_t)b * n * n, n, n}; dout[b] = {dO + (size_t)b * n * n, n, n}; }
+  MatDesc<double> *ddin, *ddout; int* info;
+  CK(hipMalloc(&ddin, nb * sizeof(MatDesc<double>))); CK(hipMalloc(&ddout, nb * sizeof(MatDesc<double>)));
+  CK(hipMalloc(&info, nb * 4));
+  CK(hipMemcpy(ddin, din.data(), nb * sizeof(MatDesc<double>), hipMemcpyHostToDevice));
+  CK(hipMemcpy(ddout, dout.data(), nb * sizeof(MatDesc<double>), hipMemcpyHostToDevice));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  float ms;
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipEventRecord(e0));
+    chol_inv_reg<double, 4, 8, 32, 16><<<nb, 512>>>(ddin, ddout, nullptr, info);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("chol_inv_reg n=%d batch=%d: %.1f us\n", n, nb, ms * 1e3);
+  }
+  {
+    int NPv = n <= 32 ? 32 : n <= 64 ? 64 : 128;
+    size_t lds = NPv == 32 ? chol_inv_mfma_lds<32>() : NPv == 64 ? chol_inv_mfma_lds<64>() : chol_inv_mfma_lds<128>();
+    CK(hipFuncSetAttribute((const void*)chol_inv_mfma<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CK(hipFuncSetAttribute((const void*)chol_inv_mfma<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipEventRecord(e0));
+      if (NPv == 128) chol_inv_mfma<128><<<nb, 512, lds>>>(ddin, ddout, info);
+      else if (NPv == 64) chol_inv_mfma<64><<<nb, 512, lds>>>(ddin, ddout, info);
+      else chol_inv_mfma<32><<<nb, 512, lds>>>(ddin, ddout, info);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("chol_inv_mfma<%d> n=%d batch=%d: %.1f us\n", NPv, n, nb, ms * 1e3);
+    }
+  }
+  // check L^-1 A L^-T = I for matrix 0
+  std::vector<double> Li((size_t)n * n);
+  CK(hipMemcpy(Li.data(), dO, (size_t)n * n * 8, hipMemcpyDeviceToHost));
+  double err = 0;
+  for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) {
+    double s = 0;
+    for (int k = 0; k < n; ++k) for (int l = 0; l < n; ++l) s += Li[i + k * n] * h[k + l * n] * Li[j + l * n];
+    err = fmax(err, fabs(s - (i == j)));
+  }
+  printf("  ||L^-1 A L^-T - I||_max = %.2e\n", err);
+  size_t lds = sizeof(double) * ((size_t)n * n + 10 * n + 40);
+  CK(hipFuncSetAttribute((const void*)eigmin_lds<double>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipEventRecord(e0));
+    eigmin_lds<double><<<nb, 512, lds>>>(ddin, dE);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("eigmin_lds n=%d batch=%d: %.1f us\n", n, nb, ms * 1e3);
+  }
+  double ev; CK(hipMemcpy(&ev, dE, 8, hipMemcpyDeviceToHost));
+#ifdef CLRSDP_EIG_STAMPS
+  {
+    unsigned long long st[8];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_eig_stamps), sizeof(st)));
+    const char* names[] = {"A:reflector", "B:symv", "B:reduce", "C:w", "D:update", "tail", "sturm"};
+    for (int i = 0; i < 7; ++i) printf("  stamp %-12s %10.0f cycles per matrix (all reps)\n", names[i], st[i] / (3.0 * nb));
+  }
+#endif
+  // lambda_min by shifted power iteration on matrix 0
+  std::vector<double> v(n, 1.0), w(n);
+  double shift = 10.0, lam = 0;
+  for (int it = 0; it < 20000; ++it) {
+    double nv = 0;
+    for (int i = 0; i < n; ++i) { double s = shift * v[i]; for (int k = 0; k < n; ++k) s -= h[i + k * n] * v[k]; w[i] = s; nv += s * s; }
+    nv = sqrt(nv); lam = 0;
+    for (int i = 0; i < n; ++i) { lam += w[i] * v[i]; v[i] = w[i] / nv; }
+  }
+  printf("  eigmin %.15f vs power-iteration %.15f\n", ev, shift - lam);
+  return 0;
+}
