@@ -9,6 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "clrsdp.hip")
 OUT = os.path.join(HERE, "libclrsdp.so")
 DEPS = [SRC, os.path.join(HERE, "csrc", "kernels.h"), os.path.join(HERE, "csrc", "mwfloat.h"),
+        os.path.join(HERE, "csrc", "kernels_dense.h"),
         os.path.join(HERE, "..", "include", "clrsdp.h")]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",

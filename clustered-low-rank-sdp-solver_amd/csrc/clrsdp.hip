@@ -75,6 +75,7 @@ struct GemmPlan {
   std::vector<int> t2d;
   GemmDesc<T>* d = nullptr;
   int* dt = nullptr;
+  // gemm_f64_lds (fp64) and gemm_valu (multi-word) output tiles
   static constexpr int TILE = std::is_same<T, double>::value ? 64 : 32;
 
   void add(const T* A, int lda, const T* B, int ldb, const T* Cin, int ldcin, T* C, int ldc, int M,
@@ -90,19 +91,36 @@ struct GemmPlan {
     for (int i = 0; i < nt; ++i) t2d.push_back((int)h.size());
     h.push_back(g);
   }
+  bool gemv = false;
   void finalize() {
     if (h.empty()) return;
+    gemv = true;
+    for (const auto& g : h) gemv = gemv && g.N == 1;
+    if (gemv) {  // re-tile: one workgroup per 64 outputs
+      t2d.clear();
+      for (size_t q = 0; q < h.size(); ++q) {
+        h[q].tile0 = (int)t2d.size();
+        for (int i = 0; i < (int)cdiv(h[q].M, 64); ++i) t2d.push_back((int)q);
+      }
+    }
     d = upload_vec(h);
     dt = upload_vec(t2d);
   }
   void launch(hipStream_t s, double alpha, double beta) const {
     if (h.empty()) return;
     const unsigned grid = (unsigned)t2d.size();
+    if (gemv) {
+      if (tb) throw ClrsdpError{CLRSDP_E_ARG, "gemv with transposed vector"};
+      if (ta) gemv_batched<T, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else gemv_batched<T, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      HIPCHK(hipGetLastError());
+      return;
+    }
     if constexpr (std::is_same<T, double>::value) {
-      if (!ta && !tb) gemm_f64_mfma<false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
-      else if (ta && !tb) gemm_f64_mfma<true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
-      else if (!ta && tb) gemm_f64_mfma<false, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
-      else gemm_f64_mfma<true, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else gemm_f64_lds<true, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
     } else {
       if (!ta && !tb) gemm_valu<T, false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else if (ta && !tb) gemm_valu<T, true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
@@ -445,7 +463,7 @@ struct Solver final : HandleBase {
     y = dmalloc<T>(n_y); bvec = dmalloc<T>(n_y); dyv = dmalloc<T>(n_y); pvec = dmalloc<T>(n_y);
     uvec = dmalloc<T>(n_y);
     sc = dmalloc<T>(SC_COUNT);
-    bpart = dmalloc<T>(std::max(nb(), 1));
+    bpart = dmalloc<T>(std::max(nb(), 256));
     eigX = dmalloc<T>(2 * std::max(nb(), 1));
     eigY = eigX + std::max(nb(), 1);  // X-side and Y-side minima of one batched eigen launch
     tC = dmalloc<T>(B);
@@ -752,9 +770,13 @@ struct Solver final : HandleBase {
   }
 
   // ---------------- kernels shorthands
+  // out = a*A + b*B over all local blocks (flat), then += s I if scal
   void blk_lin(T* out, const T* A, double a, const T* B_, double b, const T* scal = nullptr,
                double sm = 1.0) {
-    if (nb()) blk_axpby<T><<<nb(), 256, 0, stream>>>(d_blk, out, A, B_, a, b, scal, sm);
+    if (!nb()) return;
+    if (!(scal && A == out && a == 1.0 && !B_))
+      vec_lin<T><<<std::min<unsigned>(cdiv(nblk_el, 256), 4096), 256, 0, stream>>>(out, A, a, B_, b, nullptr, 0.0, nblk_el);
+    if (scal) diag_add<T><<<nb(), 128, 0, stream>>>(d_blk, out, scal, sm);
   }
   void vlin(T* out, const T* a_, double ca, const T* b_, double cb, const T* c_, double cc,
             int64_t n) {
@@ -765,9 +787,9 @@ struct Solver final : HandleBase {
   }
   void sym(T* out, const T* Zm, int mode, bool only_m = false) {
     if (only_m) {
-      if (n_blk_m) blk_sym<T><<<n_blk_m, 256, 0, stream>>>(d_blk_m, out, Zm, mode);
+      if (n_blk_m) blk_sym2<T><<<dim3(n_blk_m, 32), 128, 0, stream>>>(d_blk_m, out, Zm, mode);
     } else if (nb()) {
-      blk_sym<T><<<nb(), 256, 0, stream>>>(d_blk, out, Zm, mode);
+      blk_sym2<T><<<dim3(nb(), 32), 128, 0, stream>>>(d_blk, out, Zm, mode);
     }
   }
   ScalarParams<T> sparams(const clrsdp_params* prm, int pd_feas) {
@@ -789,13 +811,19 @@ struct Solver final : HandleBase {
     scalar_kernel<T><<<1, 1, 0, stream>>>(sc, sparams(prm, pd_feas), which);
   }
   // local block-sum (op 0/1) or block-max (op 2) into *dst
+  static constexpr int RED_G = 256;  // fixed chunking of the flat reductions (deterministic)
   void local_blk_reduce(const T* A, const T* B_, const T* dA, const T* dB, int op, T* dst) {
     if (nb()) {
-      blk_reduce<T><<<nb(), 256, 0, stream>>>(d_blk, A, B_, dA, dB, op, bpart);
-      ordered_reduce<T><<<1, 1, 0, stream>>>(bpart, nb(), 1, op, dst);
+      flat_reduce<T><<<RED_G, 256, 0, stream>>>(A, B_, dA, dB, nblk_el, op, bpart);
+      vec_reduce_tree(bpart, RED_G, op, dst);
     } else {
       fill(dst, 0.0, 1);
     }
+  }
+
+  // one-workgroup fixed-tree reduction of n <= 256 partials
+  void vec_reduce_tree(const T* in, int n, int op, T* dst) {
+    vec_reduce<T><<<1, 256, 0, stream>>>(in, in, n, op == 2 ? 2 : 3, dst);
   }
 
   // trace_A with the products U already in TX -> val (tval) -> aggregate
@@ -1017,8 +1045,9 @@ struct Solver final : HandleBase {
     if (nx > 0) vec_axpy_dev<T><<<cdiv(nx, 256), 256, 0, stream>>>(x, dx, sc + SC_ALPHA_P, nx, flag);
     vec_axpy_dev<T><<<cdiv(n_y, 256), 256, 0, stream>>>(y, dyv, sc + SC_ALPHA_D, n_y, flag);
     if (nb()) {
-      blk_axpy_dev<T><<<nb(), 256, 0, stream>>>(d_blk, X, dX, sc + SC_ALPHA_P, flag);
-      blk_axpy_dev<T><<<nb(), 256, 0, stream>>>(d_blk, Y, dY, sc + SC_ALPHA_D, flag);
+      const unsigned g = std::min<unsigned>(cdiv(nblk_el, 256), 4096);
+      vec_axpy_dev<T><<<g, 256, 0, stream>>>(X, dX, sc + SC_ALPHA_P, nblk_el, flag);
+      vec_axpy_dev<T><<<g, 256, 0, stream>>>(Y, dY, sc + SC_ALPHA_D, nblk_el, flag);
     }
     objectives(prm, pd_feas);
   }

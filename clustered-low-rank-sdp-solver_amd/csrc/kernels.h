@@ -140,6 +140,207 @@ __global__ __launch_bounds__(256) void gemm_f64_mfma(const GemmDesc<double>* __r
 }
 
 // ------------------------------------------------------------------------------------------
+// GEMM, fp64 matrix cores, LDS-free: one 64-thread workgroup (one wave) per 32x32 output tile
+// (2x2 accumulators of v_mfma_f64_16x16x4).  Every lane loads its MFMA operand fragments
+// straight from L2 (A-op: A[i0+(l&15)][k+(l>>4)], B-op: B[k+(l>>4)][j0+(l&15)]): no LDS, no
+// barrier, and the K loop is unrolled 8 k-steps deep so 32 fragment loads are in flight per lane.
+// Small batched products (128x128 blocks) get 16 independent waves per block -- 4 per CU at the
+// solver's sizes -- instead of one latency-bound workgroup.
+// ------------------------------------------------------------------------------------------
+template <bool TA, bool TB>
+__global__ __launch_bounds__(64) void gemm_f64_direct(const GemmDesc<double>* __restrict__ descs,
+                                                      const int* __restrict__ t2d, double alpha,
+                                                      double beta) {
+  const GemmDesc<double> d = descs[t2d[blockIdx.x]];
+  const int t = blockIdx.x - d.tile0;
+  const int m0 = (t / d.tn) * 32, n0 = (t % d.tn) * 32;
+  const int lane = threadIdx.x, lr = lane & 15, lk = lane >> 4;
+  const int M = d.M, N = d.N, K = d.K;
+  // rows / columns past the edge are clamped to a valid one: they only feed outputs that are
+  // never stored.  Only the K tail needs zero-filled operands.
+  const int ia0 = min(m0 + lr, M - 1), ia1 = min(m0 + 16 + lr, M - 1);
+  const int jb0 = min(n0 + lr, N - 1), jb1 = min(n0 + 16 + lr, N - 1);
+  // per-lane fragment pointers at k = lk, and the step per k-step of 4
+  const double* a0p = TA ? d.A + (size_t)ia0 * d.lda + lk : d.A + ia0 + (size_t)lk * d.lda;
+  const double* a1p = TA ? d.A + (size_t)ia1 * d.lda + lk : d.A + ia1 + (size_t)lk * d.lda;
+  const double* b0p = TB ? d.B + jb0 + (size_t)lk * d.ldb : d.B + (size_t)jb0 * d.ldb + lk;
+  const double* b1p = TB ? d.B + jb1 + (size_t)lk * d.ldb : d.B + (size_t)jb1 * d.ldb + lk;
+  const size_t sa = TA ? 4 : 4 * (size_t)d.lda, sb = TB ? 4 * (size_t)d.ldb : 4;
+  d4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c10 = c00, c11 = c00;
+  constexpr int U = 4, KS = 4 * U;
+  double pa0[U], pa1[U], pb0[U], pb1[U], qa0[U], qa1[U], qb0[U], qb1[U];
+  auto load = [&](double* x0, double* x1, double* y0, double* y1, int kb) {
+    if (kb + KS <= K) {  // interior stage: plain loads
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t ka = (size_t)(kb / 4 + u) * sa, kbb = (size_t)(kb / 4 + u) * sb;
+        x0[u] = a0p[ka];
+        x1[u] = a1p[ka];
+        y0[u] = b0p[kbb];
+        y1[u] = b1p[kbb];
+      }
+    } else {  // K tail
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = kb + 4 * u + lk < K;
+        const size_t ka = (size_t)(kb / 4 + u) * sa, kbb = (size_t)(kb / 4 + u) * sb;
+        x0[u] = ok ? a0p[ka] : 0.0;
+        x1[u] = ok ? a1p[ka] : 0.0;
+        y0[u] = ok ? b0p[kbb] : 0.0;
+        y1[u] = ok ? b1p[kbb] : 0.0;
+      }
+    }
+  };
+  auto mma = [&](const double* x0, const double* x1, const double* y0, const double* y1) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], y0[u], c00, 0, 0, 0);
+      c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], y1[u], c01, 0, 0, 0);
+      c10 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], y0[u], c10, 0, 0, 0);
+      c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], y1[u], c11, 0, 0, 0);
+    }
+  };
+  load(pa0, pa1, pb0, pb1, 0);
+  for (int k0 = 0; k0 < K; k0 += 2 * KS) {
+    if (k0 + KS < K) load(qa0, qa1, qb0, qb1, k0 + KS);
+    mma(pa0, pa1, pb0, pb1);
+    if (k0 + KS >= K) break;
+    if (k0 + 2 * KS < K) load(pa0, pa1, pb0, pb1, k0 + 2 * KS);
+    mma(qa0, qa1, qb0, qb1);
+  }
+  auto store = [&](const d4& c, int ib, int jb) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = ib + lk + 4 * r, col = jb + lr;
+      if (row < M && col < N) {
+        double v = alpha * c[r];
+        if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];
+        d.C[row + (size_t)col * d.ldc] = v;
+      }
+    }
+  };
+  store(c00, m0, n0);
+  store(c01, m0, n0 + 16);
+  store(c10, m0 + 16, n0);
+  store(c11, m0 + 16, n0 + 16);
+}
+
+// ------------------------------------------------------------------------------------------
+// GEMM, fp64 matrix cores, LDS-tiled and software-pipelined: 64x64 tile per 256-thread
+// workgroup (4 waves as 2x2, 2x2 MFMA tiles each), K-step 32.  The next K-slab is loaded into
+// registers (coalesced: each load instruction reads whole 256-512 B column runs) while the
+// current one is multiplied out of LDS, then written behind one barrier.
+// An operand that is contiguous along its 64-wide dimension (A, or B^T) is kept k-major,
+// Os[k*80 + i]; one contiguous along k (A^T, or B) is kept as Os[i*34 + k].  Both pitches make
+// the ds_read_b64 MFMA fragment reads (lanes (k = l>>4, i = l&15)) and the ds_write_b64 stores
+// bank-conflict free (MI355X_MICROARCH.md §LDS: b64 reads bank by (a/4) mod 64 in 32-lane
+// groups, b64 writes by (a/4) mod 32 in 16-lane groups).
+// ------------------------------------------------------------------------------------------
+namespace lds_gemm {
+constexpr int BK = 32, LSM = 80, LSK = 34, PER = 8;
+constexpr int OPSZ = 64 * LSK > BK * LSM ? 64 * LSK : BK * LSM;  // doubles per operand image
+
+// load one 64 x BK slab of an operand into registers.  kcontig: element (i, k) at P[k + i*ld];
+// else at P[i + k*ld].  Rows i beyond `rows` are clamped (their products are never stored),
+// k beyond K is zero.
+template <bool kcontig>
+__device__ inline void slab_load(double (&r)[PER], const double* __restrict__ P, int ld, int i0,
+                                 int rows, int k0, int K, int tid) {
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (!kcontig) {
+      const int i = tid & 63, k = (tid >> 6) + 4 * q;
+      const int gi = min(i0 + i, rows - 1), gk = k0 + k;
+      r[q] = gk < K ? P[gi + (size_t)gk * ld] : 0.0;
+    } else {
+      const int k = tid & 31, i = (tid >> 5) + 8 * q;
+      const int gi = min(i0 + i, rows - 1), gk = k0 + k;
+      r[q] = gk < K ? P[gk + (size_t)gi * ld] : 0.0;
+    }
+  }
+}
+template <bool kcontig>
+__device__ inline void slab_store(const double (&r)[PER], double* __restrict__ S, int tid) {
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (!kcontig) S[((tid >> 6) + 4 * q) * LSM + (tid & 63)] = r[q];
+    else S[((tid >> 5) + 8 * q) * LSK + (tid & 31)] = r[q];
+  }
+}
+// MFMA fragment: element (i, k) of the staged image
+template <bool kcontig>
+__device__ inline double frag(const double* __restrict__ S, int i, int k) {
+  return kcontig ? S[i * LSK + k] : S[k * LSM + i];
+}
+}  // namespace lds_gemm
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
+                                                    const int* __restrict__ t2d, double alpha,
+                                                    double beta) {
+  using namespace lds_gemm;
+  __shared__ double smem[2 * OPSZ];
+  double* As = smem;
+  double* Bs = smem + OPSZ;
+  const GemmDesc<double> d = descs[t2d[blockIdx.x]];
+  const int t = blockIdx.x - d.tile0;
+  const int m0 = (t / d.tn) * 64, n0 = (t % d.tn) * 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1, lr = lane & 15, lk = lane >> 4;
+  const int M = d.M, N = d.N, K = d.K;
+  // A is (i, k) with i along M: contiguous along k iff TA.  B is (j, k): contiguous along k iff !TB.
+  constexpr bool AK = TA, BKc = !TB;
+  double ra[PER], rb[PER];
+  d4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  slab_load<AK>(ra, d.A, d.lda, m0, M, 0, K, tid);
+  slab_load<BKc>(rb, d.B, d.ldb, n0, N, 0, K, tid);
+  slab_store<AK>(ra, As, tid);
+  slab_store<BKc>(rb, Bs, tid);
+  __syncthreads();
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    const bool more = k0 + BK < K;
+    if (more) {
+      slab_load<AK>(ra, d.A, d.lda, m0, M, k0 + BK, K, tid);
+      slab_load<BKc>(rb, d.B, d.ldb, n0, N, k0 + BK, K, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const double a0 = frag<AK>(As, wm * 32 + lr, kk + lk);
+      const double a1 = frag<AK>(As, wm * 32 + 16 + lr, kk + lk);
+      const double b0 = frag<BKc>(Bs, wn * 32 + lr, kk + lk);
+      const double b1 = frag<BKc>(Bs, wn * 32 + 16 + lr, kk + lk);
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (!more) break;
+    __syncthreads();
+    slab_store<AK>(ra, As, tid);
+    slab_store<BKc>(rb, Bs, tid);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + mi * 16 + lk + 4 * r;
+        const int col = n0 + wn * 32 + ni * 16 + lr;
+        if (row < M && col < N) {
+          double v = alpha * acc[mi][ni][r];
+          if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];
+          d.C[row + (size_t)col * d.ldc] = v;
+        }
+      }
+}
+
+// ------------------------------------------------------------------------------------------
 // GEMM on the VALU for multi-word T: 32x32 tile, 256 threads, 2x2 outputs per thread.
 // ------------------------------------------------------------------------------------------
 template <class T, bool TA, bool TB>
@@ -193,6 +394,100 @@ __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__
       }
     }
 }
+
+// ------------------------------------------------------------------------------------------
+// Batched GEMV (the N = 1 problems of a GemmDesc batch): y = alpha op(A) x + beta y_in.
+// One 256-thread workgroup per 64 outputs.  TA = false: 64 rows x 4 k-classes (coalesced along
+// the rows, LDS combine of the 4 partials in a fixed order).  TA = true: each wave owns 16
+// outputs (columns of A) and sweeps each with 64 lanes along k + a fixed butterfly.
+// ------------------------------------------------------------------------------------------
+template <class T>
+__device__ __forceinline__ T shfl_xor_t(T v, int o) {
+  if constexpr (sizeof(T) == 8) {
+    return __shfl_xor(v, o);
+  } else {
+    T t;
+    double* td = reinterpret_cast<double*>(&t);
+    const double* vd = reinterpret_cast<const double*>(&v);
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(T) / 8); ++q) td[q] = __shfl_xor(vd[q], o);
+    return t;
+  }
+}
+
+template <class T, bool TA>
+__global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restrict__ descs,
+                                                    const int* __restrict__ t2d, double alpha,
+                                                    double beta) {
+  const GemmDesc<T> d = descs[t2d[blockIdx.x]];
+  const int o0 = (blockIdx.x - d.tile0) * 64;
+  const int tid = threadIdx.x;
+  const T* __restrict__ A = d.A;
+  const T* __restrict__ x = d.B;
+  if (!TA) {
+    __shared__ T part[4][64];
+    const int r = tid & 63, g = tid >> 6, i = o0 + r;
+    T acc = T(0.0);
+    if (i < d.M)
+      for (int k = g; k < d.K; k += 4) acc += A[i + (size_t)k * d.lda] * x[k];
+    part[g][r] = acc;
+    __syncthreads();
+    if (g == 0 && i < d.M) {
+      T v = ((part[0][r] + part[1][r]) + (part[2][r] + part[3][r])) * T(alpha);
+      if (beta != 0.0) v += d.Cin[i] * T(beta);
+      d.C[i] = v;
+    }
+  } else {
+    const int lane = tid & 63, w = tid >> 6;
+    for (int c = 0; c < 16; ++c) {
+      const int j = o0 + w * 16 + c;
+      if (j >= d.M) break;
+      const T* col = A + (size_t)j * d.lda;
+      T acc = T(0.0);
+      for (int k = lane; k < d.K; k += 64) acc += col[k] * x[k];
+      for (int o = 32; o > 0; o >>= 1) acc += shfl_xor_t(acc, o);
+      if (lane == 0) {
+        T v = acc * T(alpha);
+        if (beta != 0.0) v += d.Cin[j] * T(beta);
+        d.C[j] = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Flat 2-level reductions over a contiguous range (deterministic: fixed chunking + fixed tree)
+//   op 0: sum a.*b    op 1: sum (a+da).*(b+db)    op 2: max |a|
+// ------------------------------------------------------------------------------------------
+template <class T>
+__global__ __launch_bounds__(256) void flat_reduce(const T* a, const T* b, const T* da,
+                                                   const T* db, long long n, int op,
+                                                   T* __restrict__ partial) {
+  __shared__ T red[256];
+  const long long chunk = (n + gridDim.x - 1) / gridDim.x;
+  const long long lo = (long long)blockIdx.x * chunk;
+  const long long hi = lo + chunk < n ? lo + chunk : n;
+  T acc = T(0.0);
+  for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) {
+    if (op == 0) acc += a[e] * b[e];
+    else if (op == 1) acc += (a[e] + da[e]) * (b[e] + db[e]);
+    else {
+      const T v = Num<T>::abs_(a[e]);
+      if (v > acc) acc = v;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      if (op == 2) red[threadIdx.x] = (red[threadIdx.x + s] > red[threadIdx.x]) ? red[threadIdx.x + s] : red[threadIdx.x];
+      else red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
 
 // ------------------------------------------------------------------------------------------
 // Block reductions (deterministic: fixed tree over a fixed thread->element map)
@@ -625,6 +920,41 @@ __global__ void status_reduce(const int* info, int n, int* flag) {
   if (threadIdx.x == 0) *flag = any;
 }
 
+// R_b += s I with s = (*sc) * mult; one workgroup per block
+template <class T>
+__global__ void diag_add(const BlkDesc* __restrict__ bd, T* R, const T* sc, double mult) {
+  const BlkDesc B = bd[blockIdx.x];
+  const T s = (*sc) * T(mult);
+  for (int i = threadIdx.x; i < B.n; i += blockDim.x) {
+    T* p = R + B.off + (size_t)i * (B.n + 1);
+    *p = *p + s;
+  }
+}
+
+// per-block symmetrise / mirror / transpose with a 2-D grid (block, column class):
+//   mode 0: out = (Z + Z^T)/2   mode 1: out = upper triangle mirrored   mode 2: out = Z^T
+template <class T>
+__global__ void blk_sym2(const BlkDesc* __restrict__ bd, T* out, const T* Z, int mode) {
+  const BlkDesc B = bd[blockIdx.x];
+  const int n = B.n;
+  const T* z = Z + B.off;
+  T* o = out + B.off;
+  for (int j = blockIdx.y; j < n; j += gridDim.y) {
+    if (mode == 2) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) o[i + (size_t)j * n] = z[j + (size_t)i * n];
+    } else {
+      for (int i = threadIdx.x; i < j; i += blockDim.x) {
+        T v;
+        if (mode == 0) v = (z[i + (size_t)j * n] + z[j + (size_t)i * n]) * T(0.5);
+        else v = z[i + (size_t)j * n];
+        o[i + (size_t)j * n] = v;
+        o[j + (size_t)i * n] = v;
+      }
+      if (threadIdx.x == 0) o[j + (size_t)j * n] = z[j + (size_t)j * n];
+    }
+  }
+}
+
 // X += alpha * dX with alpha = *sc  (skipped when *flag != 0: the state survives a failed step)
 template <class T>
 __global__ void blk_axpy_dev(const BlkDesc* __restrict__ bd, T* X, const T* dX, const T* sc,
@@ -705,6 +1035,7 @@ __global__ __launch_bounds__(256) void vec_reduce(const T* a, const T* b, long l
   T acc = T(0.0);
   for (long long e = threadIdx.x; e < n; e += blockDim.x) {
     if (op == 0) acc += a[e] * b[e];
+    else if (op == 3) acc += a[e];
     else {
       const T v = Num<T>::abs_(a[e]);
       if (v > acc) acc = v;
@@ -742,12 +1073,13 @@ __global__ void slab_sum(const T* in, int cnt, long long stride, long long n, T*
 template <class T>
 __global__ void vec_lin(T* out, const T* x, double a, const T* y, double b, const T* z, double c,
                         long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  T v = x[e] * T(a);
-  if (y) v += y[e] * T(b);
-  if (z) v += z[e] * T(c);
-  out[e] = v;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x) {
+    T v = x[e] * T(a);
+    if (y) v += y[e] * T(b);
+    if (z) v += z[e] * T(c);
+    out[e] = v;
+  }
 }
 
 // fill rectangles (rows x cols, column-major with ld) with v; blockIdx.y = rectangle
@@ -773,9 +1105,11 @@ __global__ void vec_fill(T* out, double v, long long n) {
 // x += (*sc) * dx
 template <class T>
 __global__ void vec_axpy_dev(T* x, const T* dx, const T* sc, long long n, const int* flag) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n || *flag) return;
-  x[e] = x[e] + (*sc) * dx[e];
+  if (*flag) return;
+  const T a = *sc;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x)
+    x[e] = x[e] + a * dx[e];
 }
 
 // ------------------------------------------------------------------------------------------

@@ -206,11 +206,16 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
   T* dg = p + 4 * n;                       // n
   T* e2 = dg + n;                          // n
   T* red = e2 + 3 * n + 12;                // NW + 4 (after w, scalars and partials)
-  // 2-D thread map (no integer division in the element loops): ti = tid % 32, tj = tid / 32
-  const int ti = tid & 31, tj = tid >> 5;
-  for (int j = tj; j < n; j += NT / 32)
-    for (int i = ti; i < n; i += 32)
-      A[i + (size_t)j * n] = (d.A[i + (size_t)j * d.lda] + d.A[j + (size_t)i * d.lda]) * T(0.5);
+  // coalesced load, then symmetrise in LDS: A = (A + A^T)/2
+  for (int j = tid >> 6; j < n; j += NT / 64)
+    for (int i = tid & 63; i < n; i += 64) A[i + (size_t)j * n] = d.A[i + (size_t)j * d.lda];
+  __syncthreads();
+  for (int j = tid >> 6; j < n; j += NT / 64)
+    for (int i = tid & 63; i < j; i += 64) {
+      const T sv = (A[i + (size_t)j * n] + A[j + (size_t)i * n]) * T(0.5);
+      A[i + (size_t)j * n] = sv;
+      A[j + (size_t)i * n] = sv;
+    }
   __syncthreads();
   T* Wv = e2 + n;        // w vector (n)            -- carved after e2
   T* scal = Wv + n;      // [0] = beta, [1] = tail flag
@@ -391,6 +396,13 @@ template <int NP>
 __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __restrict__ in,
                                                      const MatDesc<double>* __restrict__ out_inv,
                                                      int* __restrict__ info) {
+#ifdef CLRSDP_EIG_STAMPS
+  unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+  const int tid_s = threadIdx.x;
+#define CH_STAMP(slot) if (tid_s == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); atomicAdd(&g_eig_stamps[slot], t_ - t_prev); t_prev = t_; }
+#else
+#define CH_STAMP(slot)
+#endif
   constexpr int NT = NP / 16, NTILES = NT * (NT + 1) / 2, NW = 8, SLOTS = (NTILES + NW - 1) / NW;
   constexpr int XLD = NP + 16;  // X row-block buffer: 16 x NP, padded rows
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -403,11 +415,13 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nt = (n + 15) / 16;  // active tile rows
   const int lr = lane & 15, lk = lane >> 4;
-  // ---- load A (lower triangle mirrored), identity padding
-  for (int j = tid >> 4; j < NP; j += 32)
-    for (int i = (tid & 15); i < NP; i += 16) {
+  // ---- load the lower triangle (coalesced along columns); identity padding.  Nothing above
+  // the diagonal tiles is ever read, and the upper halves of diagonal tiles only carry junk.
+  for (int j = tid >> 6; j < NP; j += 8)
+    for (int i = (tid & 63); i < NP; i += 64) {
+      if (i < j) continue;
       double v;
-      if (i < n && j < n) v = (i >= j) ? d.A[i + (size_t)j * d.lda] : d.A[j + (size_t)i * d.lda];
+      if (i < n && j < n) v = d.A[i + (size_t)j * d.lda];
       else v = (i == j) ? 1.0 : 0.0;
       A[LI::idx(i, j)] = v;
     }
@@ -423,46 +437,87 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
     for (int r = 0; r < 4; ++r) X[q][r] = (t < NTILES && ti == tj && (lk + 4 * r) == lr) ? 1.0 : 0.0;
   }
   __syncthreads();
+  CH_STAMP(3)
   for (int k = 0; k < nt; ++k) {
     const int k0 = 16 * k;
-    // ---------------- (a) diagonal block: wave 0, lane i < 16 holds row i
+    // ---------------- (a) diagonal block: wave 0; lane (i = lane & 15, cg = lane >> 4) keeps row
+    // i, columns 4cg..4cg+3 of A_kk and of X_kk = L_kk^-1 in registers.  Per column one LDS round
+    // trip: the owners publish column j of A and row j of X (unscaled), every lane reads the
+    // pivot, its l_ij, the l_cj of its columns and X_j, and scales by r = 1/sqrt(a_jj)
+    // (v_rsq_f64 + one Newton step: no fp64 divide or sqrt on the critical path).
+#ifdef CLRSDP_SKIP_DIAG
+    if (w == 0) { for (int e = lane; e < 256; e += 64) Dinv[e] = ((e & 15) == (e >> 4)) ? 1.0 : 0.0; }
+    if (false) {
+#else
     if (w == 0) {
-      double row[16], lin[16];
+#endif
+      const int i = lane & 15, cg = lane >> 4;
+      double a[4], x[4];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) row[c] = (lane < 16 && c <= lane) ? A[LI::idx(k0 + lane, k0 + c)] : 0.0;
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * cg + q;
+        a[q] = (c <= i) ? A[LI::idx(k0 + i, k0 + c)] : 0.0;
+        x[q] = (c == i) ? 1.0 : 0.0;
+      }
+      double* colL = Dinv;         // 16: column j of the partially factored block
+      double* rowX = Dinv + 16;    // 16: row j of X (unscaled)
       int bad = 0;
+      // publish column 0 and row 0 (non-owners write to a scratch slot: no branches)
+      double* scratch = Dinv + 64;  // 64 dummy slots
+      colL[cg == 0 ? i : 64 + lane] = a[0];
+      if (i == 0) {
 #pragma unroll
+        for (int q = 0; q < 4; ++q) rowX[4 * cg + q] = x[q];
+      }
+#pragma unroll 1
       for (int j = 0; j < 16; ++j) {
-        const double djj = __shfl(row[j], j);
-        if (!(djj > 0.0)) bad = 1;
-        const double s = sqrt(djj);
-        const double lij = (lane == j) ? s : row[j] / s;
-        if (lane >= j) row[j] = lij;
-        // rank-1 update of the rows below: row[c] -= l_ij * l_cj for j < c <= i
+        __builtin_amdgcn_wave_barrier();
+        const double djj = colL[j];
+        const double ci = colL[i];
+        double cc[4], xr[4];
 #pragma unroll
-        for (int c = j + 1; c < 16; ++c) {
-          const double lcj = __shfl(lij, c);
-          if (lane >= c) row[c] -= lij * lcj;
+        for (int q = 0; q < 4; ++q) {
+          cc[q] = colL[4 * cg + q];
+          xr[q] = rowX[4 * cg + q];
+        }
+        bad |= !(djj > 0.0);
+        double r = __builtin_amdgcn_rsq(djj);
+        r = r * (1.5 - 0.5 * djj * r * r);  // Newton step: r = 1/sqrt(d) to ~1 ulp
+        const bool diag = (i == j), below = (i > j);
+        const double lij = diag ? djj * r : ci * r;
+        const double lr_ = lij * r;
+        __builtin_amdgcn_wave_barrier();    // every lane has read column j / row j
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = 4 * cg + q;
+          const double upd = a[q] - lr_ * cc[q];
+          a[q] = (c == j && i >= j) ? lij : ((below && c > j && c <= i) ? upd : a[q]);
+          x[q] = diag ? x[q] * r : (below ? x[q] - lr_ * xr[q] : x[q]);
+        }
+        // publish column j+1 of A (rows >= j+1) and row j+1 of X
+        const int jn = j + 1;
+        double an = a[0];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) an = (q == (jn & 3)) ? a[q] : an;
+        const bool own = (cg == (jn >> 2)) && (i >= jn) && (jn < 16);
+        colL[own ? i : 64 + lane] = an;
+        if (i == jn) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rowX[4 * cg + q] = x[q];
         }
       }
-      // inverse: lane c holds column c of L^-1 in lin[0..15]
+      (void)scratch;
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        double s = (lane == i) ? 1.0 : 0.0;
-#pragma unroll
-        for (int q = 0; q < i; ++q) s -= __shfl(row[q], i) * lin[q];
-        lin[i] = (lane <= i) ? s / __shfl(row[i], i) : 0.0;
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          A[LI::idx(k0 + lane, k0 + c)] = (c <= lane) ? row[c] : 0.0;
-          Dinv[lane * 16 + c] = lin[c];  // Dinv column `lane` = column lane of L^-1
-        }
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * cg + q;
+        A[LI::idx(k0 + i, k0 + c)] = (c <= i) ? a[q] : 0.0;
+        Dinv[c * 16 + i] = x[q];  // column-major L_kk^-1 (colL/rowX no longer needed)
       }
       if (lane == 0 && bad) *flag = k0 + 1;
     }
     __syncthreads();
+    CH_STAMP(0)
     if (*flag) break;
     // ---------------- (b) panel and X row block
     // Linv_kk operands: A-op  a[r] = Linv[lr][4r+lk]  (Dinv column-major: Dinv[c*16 + i])
@@ -496,6 +551,7 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
       }
     }
     __syncthreads();
+    CH_STAMP(1)
     // ---------------- (c) trailing updates
 #pragma unroll
     for (int q = 0; q < SLOTS; ++q) {
@@ -522,6 +578,7 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
       }
     }
     __syncthreads();
+    CH_STAMP(2)
   }
   if (tid == 0 && info) info[blockIdx.x] = *flag;
   // ---- write L^-1 (lower tiles from registers, zeros above)

@@ -54,6 +54,13 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
       printf("chol_inv_mfma<%d> n=%d batch=%d: %.1f us\n", NPv, n, nb, ms * 1e3);
     }
+#ifdef CLRSDP_EIG_STAMPS
+    unsigned long long st[8];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_eig_stamps), sizeof(st)));
+    printf("  chol stamps per matrix: load %.0f diag %.0f  panel %.0f  trailing %.0f\n", st[3] / (3.0 * nb), st[0] / (3.0 * nb), st[1] / (3.0 * nb), st[2] / (3.0 * nb));
+    unsigned long long z[8] = {0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_eig_stamps), z, sizeof(z)));
+#endif
   }
   // check L^-1 A L^-T = I for matrix 0
   std::vector<double> Li((size_t)n * n);

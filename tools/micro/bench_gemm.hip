@@ -1,0 +1,66 @@
+// Batched fp64 GEMM timing for the solver's shapes: descriptor kernels (LDS-tiled 64x64 and
+// LDS-free 32x32 direct) on 64 x (M x N x K), alpha=1, beta=0.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../../clustered-low-rank-sdp-solver_amd/csrc/kernels.h"
+using namespace clrsdp;
+#define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP %s @%d\n",hipGetErrorString(e),__LINE__); exit(1);} }while(0)
+
+template <class K>
+float timeit(K k, int reps = 20) {
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  k(); CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) k();
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1e3f / reps;
+}
+
+__global__ void empty_kernel(const GemmDesc<double>* d, const int* t) {
+  if (threadIdx.x == 999) ((double*)d)[0] = t[0];
+}
+
+int main(int argc, char** argv) {
+  int M = argc > 1 ? atoi(argv[1]) : 128, N = argc > 2 ? atoi(argv[2]) : 128, K = argc > 3 ? atoi(argv[3]) : 128;
+  int nb = argc > 4 ? atoi(argv[4]) : 64;
+  size_t sa = (size_t)M * K, sb = (size_t)K * N, sc = (size_t)M * N;
+  double *A, *B, *C;
+  CK(hipMalloc(&A, sa * nb * 8)); CK(hipMalloc(&B, sb * nb * 8)); CK(hipMalloc(&C, sc * nb * 8));
+  std::vector<double> h(std::max(sa, sb) * nb);
+  for (auto& x : h) x = rand() / (double)RAND_MAX - 0.5;
+  CK(hipMemcpy(A, h.data(), sa * nb * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(B, h.data(), sb * nb * 8, hipMemcpyHostToDevice));
+  double flops = 2.0 * M * N * K * nb;
+  {
+    float us = timeit([&] { empty_kernel<<<1024, 256>>>(nullptr, nullptr); });
+    printf("empty kernel 1024x256: %.2f us\n", us);
+  }
+  for (int variant : {0, 1, 2, 3, 4}) {
+    const int TILE = variant == 1 ? 32 : 64;
+    std::vector<GemmDesc<double>> d;
+    std::vector<int> t2d;
+    for (int b = 0; b < nb; ++b) {
+      GemmDesc<double> g{A + sa * b, B + sb * b, nullptr, C + sc * b, M, N, K, M, K, M, M, (N + TILE - 1) / TILE, (int)t2d.size(), 0};
+      int nt = ((M + TILE - 1) / TILE) * g.tn;
+      for (int i = 0; i < nt; ++i) t2d.push_back(b);
+      d.push_back(g);
+    }
+    GemmDesc<double>* dd; int* dt;
+    CK(hipMalloc(&dd, d.size() * sizeof(d[0]))); CK(hipMalloc(&dt, t2d.size() * 4));
+    CK(hipMemcpy(dd, d.data(), d.size() * sizeof(d[0]), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dt, t2d.data(), t2d.size() * 4, hipMemcpyHostToDevice));
+    unsigned grid = t2d.size();
+    float us;
+    if (variant == 0) us = timeit([&] { gemm_f64_mfma<false, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 1) us = timeit([&] { gemm_f64_direct<false, false><<<grid, 64>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 2) us = timeit([&] { gemm_f64_lds<false, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 3) us = timeit([&] { gemm_f64_lds<true, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    else us = timeit([&] { gemm_f64_lds<false, true><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    const char* nm[] = {"mfma64 (LDS) ", "direct32     ", "lds NN       ", "lds TN       ", "lds NT       "};
+    printf("%s  batch %d x (%d x %d x %d): %.1f us  %.1f TFLOP/s  (grid %u)\n", nm[variant], nb, M, N, K, us, flops / us / 1e6, grid);
+  }
+  return 0;
+}

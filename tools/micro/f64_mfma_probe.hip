@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void valu_tput(double* out, int iters, double 
   if (t == 12345.678) out[threadIdx.x] = t;
 }
 
-int main() {
+int main(int argc, char** argv) {
   // layout
   std::vector<double> A(64), B(64), D(256);
   for (int i = 0; i < 16; ++i) for (int k = 0; k < 4; ++k) A[i * 4 + k] = i * 7 + k * 3 + 1;
@@ -66,7 +66,7 @@ int main() {
   printf("layout: map row=(l>>4)+4r : %s ; map row=(l>>4)*4+r : %s\n", okA ? "OK" : "no", okB ? "OK" : "no");
   // throughput
   double* dout; CK(hipMalloc(&dout, 1 << 20));
-  int nblk = 256 * 8, iters = 4096;
+  int nblk = argc > 1 ? atoi(argv[1]) : 256 * 8, iters = 4096;
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int rep = 0; rep < 2; ++rep) {
     CK(hipEventRecord(e0)); mfma_tput<<<nblk, 256>>>(dout, iters, 0.5); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
