@@ -295,6 +295,7 @@ struct Solver final : HandleBase {
   T *V, *lam, *TX, *TY, *BX, *BY, *AY, *tval, *S, *Wm, *Bm, *Qslab, *Q, *Qf;
   T *cvec, *x, *dx, *dvec, *rhs, *tvec, *tmpv, *pslab, *y, *bvec, *dyv, *pvec, *uvec;
   T *sc, *bpart, *eigX, *eigY, *tmpsc, *tC = nullptr, *Stmp = nullptr;
+  T* Vt = nullptr;  // per block V^T (K x delta), fused Schur path only
   int *ksamp, *rsums, *info;
   T *xsend = nullptr, *xrecv = nullptr, *own_send = nullptr;
   int64_t xcap = 0;  // exchange capacity in T values
@@ -319,6 +320,15 @@ struct Solver final : HandleBase {
   BlkDesc* d_blk = nullptr;      // all local blocks
   BlkDesc* d_blk_m = nullptr;    // local blocks with m > 1
   int n_blk_m = 0;
+  // fused Schur path (fp64, every local block m = 1): TXt/TYt = V^T X^-1 / V^T Y, then the
+  // paired Hadamard tiles; clusters with L > 1 or ranks != 1 are summed from G (BX arena)
+  bool fast_schur = false;
+  GemmPlan<T> p_txy;
+  PairTileDesc* d_ptd = nullptr;
+  int* d_pt2d = nullptr;
+  int n_ptiles = 0;
+  SchurClusterDesc* d_gcd = nullptr;  // clusters summed by schur_gsum
+  int n_gsum = 0, max_gD = 0;
   SchurClusterDesc* d_scd = nullptr;
   SchurBlockDesc* d_sbd = nullptr;
   long long n_pairs = 0;
@@ -421,6 +431,7 @@ struct Solver final : HandleBase {
         lb.push_back(b);
       }
     }
+    fast_schur = std::is_same<T, double>::value && !anyMgt1 && nb() > 0;
     HIPCHK(hipStreamCreateWithFlags(&own_stream, hipStreamNonBlocking));
     stream = own_stream;
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
@@ -432,7 +443,7 @@ struct Solver final : HandleBase {
     // device memory is released with the process / hipDeviceReset; free what we own explicitly
     T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, BX, BY, AY,
                  tval, S, Wm, Bm, Qslab, Q, Qf, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
-                 bvec, dyv, pvec, uvec, sc, bpart, eigX, tmpsc, tC, Stmp, own_send};
+                 bvec, dyv, pvec, uvec, sc, bpart, eigX, tmpsc, tC, Stmp, own_send, Vt};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
     (void)hipFree(ksamp);
@@ -476,6 +487,7 @@ struct Solver final : HandleBase {
     tmpsc = dmalloc<T>(8);
     ksamp = dmalloc<int>(nK);
     rsums = dmalloc<int>(nRS);
+    if (fast_schur) Vt = dmalloc<T>(std::max<int64_t>(nV, 1));
     // info layout: [X: nb][Y: nb][S: nc single + nc2 second blocks][Q: 1]
     info_count = 2 * nb() + nc() + nc2 + 1;
     info_Y0 = nb();
@@ -683,7 +695,8 @@ struct Solver final : HandleBase {
       d_td = upload_vec(td);
       d_tb = upload_vec(tbk);
     }
-    for (GemmPlan<T>* g : {&p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
+    if (fast_schur) build_fast_schur();
+    for (GemmPlan<T>* g : {&p_txy, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
                            &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_L21, &q_S22, &q_M, &q_X21})
@@ -693,6 +706,54 @@ struct Solver final : HandleBase {
     for (TrsmPlan<T>* t : {&t_Linv, &t_W, &t_t, &t_Q, &t_sX1, &t_sX2, &t_sY1, &t_sY2, &t_dx})
       t->finalize();
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q, &e_X, &e_Y}) f->finalize();
+  }
+
+  void build_fast_schur() {
+    if constexpr (std::is_same<T, double>::value) {
+      p_txy.tb = true;  // TXt = Vt * X^-1^T (X^-1 and Y are symmetric)
+      for (const LBlk& b : lb)
+        if (b.K > 0) {
+          p_txy.add(Vt + b.voff, b.K, Xinv + b.off, b.n, nullptr, 0, TX + b.toff, b.K, b.K, b.del, b.del);
+          p_txy.add(Vt + b.voff, b.K, Y + b.off, b.n, nullptr, 0, TY + b.toff, b.K, b.K, b.del, b.del);
+        }
+      std::vector<PairTileDesc> ptd;
+      std::vector<int> pt2d;
+      std::vector<SchurClusterDesc> gcd;
+      int bi = 0;
+      for (int c = 0; c < nc(); ++c) {
+        const int j = oc[c];
+        bool direct = Lc[j] == 1;
+        for (int l = 0; l < Lc[j] && direct; ++l) {
+          const LBlk& b = lb[bi + l];
+          for (int k = 0; k < b.N; ++k) direct = direct && ranks_all[rkoff_g[b.gjl] + k] == 1;
+        }
+        for (int l = 0; l < Lc[j]; ++l) {
+          const LBlk& b = lb[bi + l];
+          if (b.K == 0) continue;
+          PairTileDesc t;
+          t.Vt = Vt + b.voff; t.TXt = TX + b.toff; t.TYt = TY + b.toff; t.lam = lam + b.koff;
+          t.G = direct ? S + c_Soff[c] : BX + b.boff;
+          t.ldG = b.K;
+          t.AY = AY + b.ayoff;
+          t.K = b.K; t.del = b.del; t.tile0 = (int)pt2d.size();
+          const int nt = cdiv(b.K, 64);
+          for (int u = 0; u < nt * (nt + 1) / 2; ++u) pt2d.push_back((int)ptd.size());
+          ptd.push_back(t);
+        }
+        if (!direct) {
+          SchurClusterDesc g;
+          g.m = 1; g.N = (int)Ns[j]; g.D = (int)Ds[j]; g.blk0 = bi; g.nblk = (int)Lc[j];
+          g.pair0 = 0; g.S_off = c_Soff[c];
+          gcd.push_back(g);
+          max_gD = std::max(max_gD, g.D);
+        }
+        bi += (int)Lc[j];
+      }
+      n_ptiles = (int)pt2d.size();
+      if (n_ptiles) { d_ptd = upload_vec(ptd); d_pt2d = upload_vec(pt2d); }
+      n_gsum = (int)gcd.size();
+      if (n_gsum) d_gcd = upload_vec(gcd);
+    }
   }
 
   TrsmPlan<T> t_dx;
@@ -724,6 +785,13 @@ struct Solver final : HandleBase {
     for (const LBlk& b : lb) {
       put(V + b.voff, Vh, tot_V, voff_g[b.gjl], (int64_t)b.del * b.K);
       put(lam + b.koff, lamh, tot_K, koff_g[b.gjl], b.K);
+      if (fast_schur && b.K > 0) {  // V^T for the fused Schur path (fp64: one plane)
+        std::vector<double> vt((size_t)b.del * b.K);
+        const double* src = Vh + voff_g[b.gjl];
+        for (int i = 0; i < b.del; ++i)
+          for (int p = 0; p < b.K; ++p) vt[p + (size_t)i * b.K] = src[i + (size_t)p * b.del];
+        put(Vt + b.voff, vt.data(), (int64_t)vt.size(), 0, (int64_t)vt.size());
+      }
     }
     for (int c = 0; c < nc(); ++c) {
       const int j = oc[c];
@@ -870,6 +938,18 @@ struct Solver final : HandleBase {
     p_xinv.launch(stream, 1.0, 0.0);          // X^-1 = L^-T L^-1
   }
   void st_schur() {
+    if constexpr (std::is_same<T, double>::value) {
+      if (fast_schur) {
+        p_txy.launch(stream, 1.0, 0.0);
+        if (n_ptiles) schur_pairs_f64<<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d);
+        if (n_gsum) {
+          dim3 g((unsigned)std::min<int64_t>(cdiv((int64_t)max_gD * max_gD, 256), 64), n_gsum);
+          schur_gsum<T><<<g, 256, 0, stream>>>(d_gcd, d_sbd, rsums, BX, S);
+        }
+        HIPCHK(hipGetLastError());
+        return;
+      }
+    }
     p_s1x.launch(stream, 1.0, 0.0);
     p_s1y.launch(stream, 1.0, 0.0);
     p_s2x.launch(stream, 1.0, 0.0);

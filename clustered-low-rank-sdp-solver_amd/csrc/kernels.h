@@ -885,6 +885,129 @@ __global__ __launch_bounds__(256) void schur_assemble(const SchurClusterDesc* __
 }
 
 // ------------------------------------------------------------------------------------------
+// Fused Schur pairing for blocks with m = 1 (fp64 matrix cores).  With V the delta x K vectors of
+// block b and the transposed products TXt = V^T X^-1, TYt = V^T Y (K x delta, ld K), one 64x64
+// upper tile (I <= J) of
+//     G[p, q] = lambda_p lambda_q (V^T X^-1 V)[p, q] (V^T Y V)[q, p]
+// per 256-thread workgroup: both contractions over delta share the staged V^T slab (three
+// LDS slabs, k-major, pipelined like gemm_f64_lds), the Hadamard product and the lambda scaling
+// are applied in registers and G is written to both triangles.  Diagonal tiles also write
+// AY[p] = (V^T Y V)[p, p].  This is MPMP.jl:1291-1330 + 1373-1398 at m = 1 (the four pairing
+// terms coincide) without materialising the K x K pairings BX, BY.
+// ------------------------------------------------------------------------------------------
+struct PairTileDesc {
+  const double* Vt;   // K x delta, ld K  (V transposed, uploaded once)
+  const double* TXt;  // K x delta, ld K
+  const double* TYt;
+  const double* lam;  // K
+  double* G;          // K x K (ld ldG): S itself when L = 1 and every rank is 1
+  double* AY;         // K
+  int K, del, ldG, tile0;
+};
+
+__global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __restrict__ descs,
+                                                       const int* __restrict__ t2d) {
+  using namespace lds_gemm;
+  constexpr int SL = BK * LSM;
+  __shared__ double smem[3 * SL];
+  double* As = smem;
+  double* Xs = smem + SL;
+  double* Ys = smem + 2 * SL;
+  const PairTileDesc d = descs[t2d[blockIdx.x]];
+  const int u = blockIdx.x - d.tile0;
+  int J = 0;
+  while ((J + 1) * (J + 2) / 2 <= u) ++J;
+  const int I = u - J * (J + 1) / 2;
+  const int p0 = I * 64, q0 = J * 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1, lr = lane & 15, lk = lane >> 4;
+  const int K = d.K, D = d.del;
+  double ra[PER], rx[PER], ry[PER];
+  d4 ax[2][2], ay[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) ax[a][b] = ay[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  slab_load<false>(ra, d.Vt, K, p0, K, 0, D, tid);
+  slab_load<false>(rx, d.TXt, K, q0, K, 0, D, tid);
+  slab_load<false>(ry, d.TYt, K, q0, K, 0, D, tid);
+  slab_store<false>(ra, As, tid);
+  slab_store<false>(rx, Xs, tid);
+  slab_store<false>(ry, Ys, tid);
+  __syncthreads();
+  for (int k0 = 0; k0 < D; k0 += BK) {
+    const bool more = k0 + BK < D;
+    if (more) {
+      slab_load<false>(ra, d.Vt, K, p0, K, k0 + BK, D, tid);
+      slab_load<false>(rx, d.TXt, K, q0, K, k0 + BK, D, tid);
+      slab_load<false>(ry, d.TYt, K, q0, K, k0 + BK, D, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const int kr = (kk + lk) * LSM;
+      const double a0 = As[kr + wm * 32 + lr], a1 = As[kr + wm * 32 + 16 + lr];
+      const double x0 = Xs[kr + wn * 32 + lr], x1 = Xs[kr + wn * 32 + 16 + lr];
+      const double y0 = Ys[kr + wn * 32 + lr], y1 = Ys[kr + wn * 32 + 16 + lr];
+      ax[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, x0, ax[0][0], 0, 0, 0);
+      ay[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, y0, ay[0][0], 0, 0, 0);
+      ax[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, x1, ax[0][1], 0, 0, 0);
+      ay[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, y1, ay[0][1], 0, 0, 0);
+      ax[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, x0, ax[1][0], 0, 0, 0);
+      ay[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, y0, ay[1][0], 0, 0, 0);
+      ax[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, x1, ax[1][1], 0, 0, 0);
+      ay[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, y1, ay[1][1], 0, 0, 0);
+    }
+    if (!more) break;
+    __syncthreads();
+    slab_store<false>(ra, As, tid);
+    slab_store<false>(rx, Xs, tid);
+    slab_store<false>(ry, Ys, tid);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = p0 + wm * 32 + mi * 16 + lk + 4 * r;
+        const int q = q0 + wn * 32 + ni * 16 + lr;
+        if (p < K && q < K && (I < J || p <= q)) {
+          const double yv = ay[mi][ni][r];
+          const double v = d.lam[p] * d.lam[q] * (ax[mi][ni][r] * yv);
+          d.G[p + (size_t)q * d.ldG] = v;
+          if (p != q) d.G[q + (size_t)p * d.ldG] = v;
+          else d.AY[p] = yv;
+        }
+      }
+}
+
+// S_c[k1, k2] = sum over blocks l of cluster c, sum over p1 in sample k1, p2 in sample k2 of
+// G_l[p1, p2]  (the rank / block sums of MPMP.jl:1373-1399 when m = 1 and the pairings were
+// formed by schur_pairs_f64).  grid = (chunks, clusters).
+template <class T>
+__global__ __launch_bounds__(256) void schur_gsum(const SchurClusterDesc* __restrict__ cd,
+                                                  const SchurBlockDesc* __restrict__ bd,
+                                                  const int* __restrict__ rank_sums,
+                                                  const T* __restrict__ G, T* __restrict__ S) {
+  const SchurClusterDesc c = cd[blockIdx.y];
+  const long long n = (long long)c.D * c.D;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int k1 = (int)(e % c.D), k2 = (int)(e / c.D);
+    T tot = T(0.0);
+    for (int b = c.blk0; b < c.blk0 + c.nblk; ++b) {
+      const SchurBlockDesc B = bd[b];
+      const int* rs = rank_sums + B.rs_off;
+      const T* g = G + B.bx_off;
+      for (int p2 = rs[k2]; p2 < rs[k2 + 1]; ++p2)
+        for (int p1 = rs[k1]; p1 < rs[k1 + 1]; ++p1) tot += g[p1 + (size_t)p2 * B.K];
+    }
+    S[c.S_off + e] = tot;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // small batched elementwise kernels over block matrices (one workgroup per block)
 // ------------------------------------------------------------------------------------------
 struct BlkDesc {
