@@ -71,6 +71,7 @@ constexpr size_t LDS_MAX = 160 * 1024;
 template <class T>
 struct GemmPlan {
   bool ta = false, tb = false;
+  int tag = 0;  // 1: the Schur-stage V^T X^-1 / V^T Y launch (named separately in profiles)
   std::vector<GemmDesc<T>> h;
   std::vector<int> t2d;
   GemmDesc<T>* d = nullptr;
@@ -117,7 +118,8 @@ struct GemmPlan {
       return;
     }
     if constexpr (std::is_same<T, double>::value) {
-      if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else gemm_f64_lds<true, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
@@ -710,6 +712,7 @@ struct Solver final : HandleBase {
 
   void build_fast_schur() {
     if constexpr (std::is_same<T, double>::value) {
+      p_txy.tag = 1;
       p_txy.tb = true;  // TXt = Vt * X^-1^T (X^-1 and Y are symmetric)
       for (const LBlk& b : lb)
         if (b.K > 0) {

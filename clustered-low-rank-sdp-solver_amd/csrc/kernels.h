@@ -274,7 +274,8 @@ __device__ inline double frag(const double* __restrict__ S, int i, int k) {
 }
 }  // namespace lds_gemm
 
-template <bool TA, bool TB>
+// TAG only names the instantiation (a profile can tell the Schur-stage launch from the others)
+template <bool TA, bool TB, int TAG = 0>
 __global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
                                                     const int* __restrict__ t2d, double alpha,
                                                     double beta) {
