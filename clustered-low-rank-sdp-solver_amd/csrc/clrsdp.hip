@@ -944,7 +944,7 @@ struct Solver final : HandleBase {
     if constexpr (std::is_same<T, double>::value) {
       if (fast_schur) {
         p_txy.launch(stream, 1.0, 0.0);
-        if (n_ptiles) schur_pairs_f64<<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d);
+        if (n_ptiles) schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d);
         if (n_gsum) {
           dim3 g((unsigned)std::min<int64_t>(cdiv((int64_t)max_gD * max_gD, 256), 64), n_gsum);
           schur_gsum<T><<<g, 256, 0, stream>>>(d_gcd, d_sbd, rsums, BX, S);

@@ -38,12 +38,14 @@ int main(int argc, char** argv) {
     float us = timeit([&] { empty_kernel<<<1024, 256>>>(nullptr, nullptr); });
     printf("empty kernel 1024x256: %.2f us\n", us);
   }
-  for (int variant : {0, 1, 2, 3, 4}) {
+  for (int variant : {0, 1, 2, 3, 4, 5, 6, 7}) {
     const int TILE = variant == 1 ? 32 : 64;
     std::vector<GemmDesc<double>> d;
     std::vector<int> t2d;
     for (int b = 0; b < nb; ++b) {
-      GemmDesc<double> g{A + sa * b, B + sb * b, nullptr, C + sc * b, M, N, K, M, K, M, M, (N + TILE - 1) / TILE, (int)t2d.size(), 0};
+      // lda/ldb as each variant reads them: TA -> A is K x M (ld K), TB -> B is N x K (ld N)
+      const bool ta = variant == 3 || variant == 6, tb = variant == 4 || variant == 7;
+      GemmDesc<double> g{A + sa * b, B + sb * b, nullptr, C + sc * b, M, N, K, ta ? K : M, tb ? N : K, M, M, (N + TILE - 1) / TILE, (int)t2d.size(), 0};
       int nt = ((M + TILE - 1) / TILE) * g.tn;
       for (int i = 0; i < nt; ++i) t2d.push_back(b);
       d.push_back(g);
@@ -58,8 +60,11 @@ int main(int argc, char** argv) {
     else if (variant == 1) us = timeit([&] { gemm_f64_direct<false, false><<<grid, 64>>>(dd, dt, 1.0, 0.0); });
     else if (variant == 2) us = timeit([&] { gemm_f64_lds<false, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
     else if (variant == 3) us = timeit([&] { gemm_f64_lds<true, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
-    else us = timeit([&] { gemm_f64_lds<false, true><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
-    const char* nm[] = {"mfma64 (LDS) ", "direct32     ", "lds NN       ", "lds TN       ", "lds NT       "};
+    else if (variant == 4) us = timeit([&] { gemm_f64_lds<false, true><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 5) us = timeit([&] { gemm_f64_lds<false, false, 0, 16><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 6) us = timeit([&] { gemm_f64_lds<true, false, 0, 16><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    else us = timeit([&] { gemm_f64_lds<false, true, 0, 16><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    const char* nm[] = {"mfma64 (LDS) ", "direct32     ", "lds NN       ", "lds TN       ", "lds NT       ", "lds16 NN     ", "lds16 TN     ", "lds16 NT     "};
     printf("%s  batch %d x (%d x %d x %d): %.1f us  %.1f TFLOP/s  (grid %u)\n", nm[variant], nb, M, N, K, us, flops / us / 1e6, grid);
   }
   return 0;
