@@ -189,6 +189,13 @@ struct MatPlan {  // potrf / eigmin
   }
   void eigmin(hipStream_t s, T* out) const {
     if (h.empty()) return;
+    if constexpr (std::is_same<T, double>::value) {
+      if (nmax <= 128) {  // matrix in registers (eigmin_reg)
+        eigmin_reg<<<(unsigned)h.size(), 512, 0, s>>>(d, out);
+        HIPCHK(hipGetLastError());
+        return;
+      }
+    }
     if (eig_lds_bytes<T>(nmax) <= LDS_MAX) {
       const size_t lds = eig_lds_bytes<T>(nmax);
       static bool attr = false;

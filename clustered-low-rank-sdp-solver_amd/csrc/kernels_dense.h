@@ -12,6 +12,34 @@
 namespace clrsdp {
 
 // Deterministic block reduction for 512 threads: wave butterfly, then 8 wave sums in order.
+// In-register cross-lane sums of doubles (no LDS round trip, unlike __shfl_xor which is a
+// ds_bpermute): DPP quad permutes and row mirrors for lane distances 1..8, v_permlane16/32_swap
+// (CDNA4) for 16 and 32.  Every lane ends with the same, order-independent result.
+template <int CTRL>
+__device__ inline double dpp_d(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ inline double xsum16(double x) {  // x + x[lane ^ 16]
+  const auto rl = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(x), false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(x), false, false);
+  return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+}
+__device__ inline double xsum32(double x) {  // x + x[lane ^ 32]
+  const auto rl = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(x), false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(x), false, false);
+  return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+}
+__device__ inline double row16_sum(double x) {  // sum over the 16 lanes of a DPP row
+  x += dpp_d<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_d<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_d<0x141>(x);  // row_half_mirror
+  x += dpp_d<0x140>(x);  // row_mirror
+  return x;
+}
+__device__ inline double wave_sum_dpp(double x) { return xsum32(xsum16(row16_sum(x))); }
+
 template <class T>
 __device__ T wave_sum(T v) {
   for (int s = 32; s > 0; s >>= 1) {
@@ -179,6 +207,271 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
 // is symmetrised into LDS (ld = n), tridiagonalised by Householder reflections (full storage),
 // then one wave runs a 64-point Sturm multisection.
 // ------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------
+// eigmin_reg: lambda_min of a symmetric n <= 128 fp64 block with the matrix held in REGISTERS
+// (replaces approx_eig_qr! in compute_step_length, MPMP.jl:1857-1860).  512 threads; wave w
+// owns rows 16w..16w+15 (lane r = l & 15), lane class c = l >> 4 owns the column pairs
+// j = 2c + 8s + {0,1}, s = 0..15: 32 entries per thread.  Householder tridiagonalisation with
+// two barriers per column:
+//   (B) every wave rebuilds the reflector of column k redundantly from the column buffer
+//       (wave reduction, no barrier), p_i = sum_j A_ij v_j in registers (+ 2 shuffles across
+//       the column classes), per-wave v^T p to LDS                                 -- barrier
+//   (C) w = beta p - K v; A -= v w^T + w v^T in registers; the owners of column k+1 publish it
+//       to the other column buffer                                                -- barrier
+// then 512-way multisection with Sturm counts on the tridiagonal matrix.  No LDS image of A:
+// the only LDS traffic per column is the broadcast of v and p (two ds_read_b128 per pair).
+// ------------------------------------------------------------------------------------------
+#ifdef CLRSDP_EIGREG_STAMPS
+__device__ unsigned long long g_eigreg_stamps[8];
+#endif
+// Sturm count of the symmetric tridiagonal (dg, e2 = squared off-diagonals) below sigma, with a
+// Newton-refined hardware reciprocal instead of the IEEE division (only signs are used) and
+// the coefficients read two at a time.
+__device__ inline int sturm_count_fast(const double* dg, const double* e2, int n, double sigma) {
+  int cnt = 0;
+  double q = dg[0] - sigma;
+  cnt += q < 0.0;
+  int i = 1;
+  for (; i + 1 < n; i += 2) {
+    const double d0 = dg[i], d1 = dg[i + 1], f0 = e2[i - 1], f1 = e2[i];
+    q = q == 0.0 ? 1e-300 : q;
+    double r = __builtin_amdgcn_rcp(q);
+    r = fma(fma(-q, r, 1.0), r, r);
+    r = fma(fma(-q, r, 1.0), r, r);
+    q = (d0 - sigma) - f0 * r;
+    cnt += q < 0.0;
+    q = q == 0.0 ? 1e-300 : q;
+    r = __builtin_amdgcn_rcp(q);
+    r = fma(fma(-q, r, 1.0), r, r);
+    r = fma(fma(-q, r, 1.0), r, r);
+    q = (d1 - sigma) - f1 * r;
+    cnt += q < 0.0;
+  }
+  for (; i < n; ++i) {
+    q = q == 0.0 ? 1e-300 : q;
+    double r = __builtin_amdgcn_rcp(q);
+    r = fma(fma(-q, r, 1.0), r, r);
+    r = fma(fma(-q, r, 1.0), r, r);
+    q = (dg[i] - sigma) - e2[i - 1] * r;
+    cnt += q < 0.0;
+  }
+  return cnt;
+}
+
+__global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restrict__ descs,
+                                                  double* __restrict__ out) {
+  constexpr int NS = 16;
+#ifdef CLRSDP_EIGREG_STAMPS
+  unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#define ER_STAMP(slot) if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); atomicAdd(&g_eigreg_stamps[slot], t_ - t_prev); t_prev = t_; }
+#else
+#define ER_STAMP(slot)
+#endif
+  // colb[k&1] = column k of the current matrix with rows <= k-1 zeroed; pb = A'v with inactive
+  // rows zeroed; rows/columns >= n stay zero.  So v and w need no masking per element.
+  // entries 128..255 stay zero: the slots past the last column read zeros there
+  __shared__ __attribute__((aligned(16))) double colb[2][256];
+  __shared__ __attribute__((aligned(16))) double pb[256];
+  __shared__ double redw[8];
+  __shared__ double dg[128], e2[128];
+  __shared__ double bnd[2];
+  __shared__ unsigned long long masks[8];
+  const MatDesc<double> d = descs[blockIdx.x];
+  const int n = d.n, lda = d.lda, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int c = lane >> 4, i = w * 16 + (lane & 15);
+  const bool rowok = i < n;
+  // slot s holds columns j = 2c + 8(s + q) + {0,1}; q advances (the slots shift down by one)
+  // each time column k+1 enters a new group of 8, so column k+1 always sits in slot 0.
+  double a[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = 2 * c + 8 * s + e;
+      const int ic = min(i, n - 1), jc = min(j, n - 1);  // unconditional loads, masked after
+      const double v = (gload(d.A + ic + (size_t)jc * lda) + gload(d.A + jc + (size_t)ic * lda)) * 0.5;
+      a[s][e] = (rowok && j < n) ? v : 0.0;
+    }
+#define EIG_SHIFT_SLOTS()                                                    \
+  do {                                                                       \
+    _Pragma("unroll") for (int s = 0; s + 1 < NS; ++s) {                     \
+      a[s][0] = a[s + 1][0];                                                 \
+      a[s][1] = a[s + 1][1];                                                 \
+    }                                                                        \
+    a[NS - 1][0] = a[NS - 1][1] = 0.0;                                       \
+  } while (0)
+  if (tid < 256) {
+    pb[tid] = 0.0;
+    colb[1][tid] = 0.0;
+    if (tid >= n) colb[0][tid] = 0.0;
+  }
+  if (c == 0 && rowok) colb[0][i] = a[0][0];  // column 0
+  __syncthreads();
+  ER_STAMP(0)
+  int q = 0;
+  for (int k = 0; k + 2 < n; ++k) {
+    if (((k + 1) & 7) == 0) { EIG_SHIFT_SLOTS(); ++q; }
+    const double* col = colb[k & 1];
+    const int m = n - k - 1;
+    const int ns = NS - q;  // slots that hold existing columns
+    // ---- all LDS reads of this column first (one wait)
+    double2 cv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      cv[s] = *reinterpret_cast<const double2*>(col + 2 * c + 8 * (s + q));
+    const double xi = col[i < 128 ? i : 0];
+    // ---- reflector of column k (every wave, redundantly)
+    double ss = 0.0;
+    for (int t = lane; t < m; t += 64) {
+      const double x = col[k + 1 + t];
+      ss += x * x;
+    }
+    ss = wave_sum_dpp(ss);
+    const double x0 = col[k + 1];
+    const double tail = ss - x0 * x0;
+    double beta = 0.0, v0 = x0;
+    if (tail > 0.0) {
+      const double nrm = sqrt(ss);
+      const double alpha = x0 > 0.0 ? -nrm : nrm;
+      v0 = x0 - alpha;
+      beta = 2.0 / (tail + v0 * v0);
+      if (tid == 0) e2[k] = alpha * alpha;
+    } else if (tid == 0) {
+      e2[k] = x0 * x0;
+    }
+    if (tid == 0) dg[k] = col[k];
+    ER_STAMP(6)
+    if (beta != 0.0) {
+      // ---- (B) p = A' v.  v_j = col[j] for j > k+1, v0 at k+1 (slot 0, element (k+1)&1 of
+      // class ((k+1)>>1)&3), 0 for j <= k (zeroed rows of the column buffer)
+      const int jn = k + 1;
+      const bool own = c == ((jn >> 1) & 3);
+      if (own) {
+        if (jn & 1) cv[0].y = v0; else cv[0].x = v0;
+      }
+      // the pivot entry j = k holds the diagonal in the column buffer: v_k = 0.  Column k is in
+      // slot 0 unless the slots were just shifted past it.
+      if (((k + 1) & 7) != 0 && c == ((k >> 1) & 3)) {
+        if (k & 1) cv[0].y = 0.0; else cv[0].x = 0.0;
+      }
+      const double vi = i > k ? (i == jn ? v0 : xi) : 0.0;
+      const bool wave_live = w * 16 + 15 > k;  // wave-uniform: some row of this wave is active
+      double pp = 0.0;
+      // slots in groups of 4 behind one uniform branch each (a per-slot condition gets
+      // if-converted into computing everything plus selects)
+      if (wave_live) {
+#pragma unroll
+        for (int g = 0; g < NS / 4; ++g) {
+          if (4 * g < ns) {
+#pragma unroll
+            for (int s = 4 * g; s < 4 * g + 4; ++s) pp += a[s][0] * cv[s].x + a[s][1] * cv[s].y;
+          }
+        }
+      }
+      ER_STAMP(7)
+      pp = xsum32(xsum16(pp));
+      double t = 0.0;
+      if (c == 0) {
+        if (i < 128) pb[i] = i > k ? pp : 0.0;
+        t = vi * pp;
+      }
+      t = wave_sum_dpp(t);
+      if (lane == 0) redw[w] = t;
+      ER_STAMP(1)
+      __syncthreads();
+      ER_STAMP(2)
+      // ---- (C) w = beta p - K v;  A' -= v w^T + w v^T
+      double tot = redw[0];
+#pragma unroll
+      for (int r = 1; r < 8; ++r) tot += redw[r];
+      const double Kc = beta * beta * tot * 0.5;
+      double2 pv[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        pv[s] = *reinterpret_cast<const double2*>(pb + 2 * c + 8 * (s + q));
+      // a_ij -= v_i w_j + w_i v_j with w = beta p - K v:  a_ij += g_i v_j - h_i p_j,
+      // g_i = K v_i - w_i, h_i = beta v_i
+      const double wi = beta * pp - Kc * vi;
+      const double gi = Kc * vi - wi, hi = beta * vi;
+      if (wave_live) {
+#pragma unroll
+        for (int g = 0; g < NS / 4; ++g) {
+          if (4 * g < ns) {
+#pragma unroll
+            for (int s = 4 * g; s < 4 * g + 4; ++s) {
+              a[s][0] = fma(gi, cv[s].x, fma(-hi, pv[s].x, a[s][0]));
+              a[s][1] = fma(gi, cv[s].y, fma(-hi, pv[s].y, a[s][1]));
+            }
+          }
+        }
+      }
+    }
+    // ---- publish column k+1 from slot 0 of its owners; rows <= k+1-1 written as 0
+    {
+      const int jn = k + 1;
+      if (c == ((jn >> 1) & 3) && i < 128) colb[jn & 1][i] = (i >= jn && rowok) ? ((jn & 1) ? a[0][1] : a[0][0]) : 0.0;
+    }
+    ER_STAMP(3)
+    __syncthreads();
+    ER_STAMP(4)
+  }
+  // trailing 2x2 (or 1x1): column n-1 from slot 0 of its owners (after the last shift)
+  if (n >= 2) {
+    const int j1 = n - 1;
+    if (n >= 3 && ((n - 2 + 1) & 7) == 0) EIG_SHIFT_SLOTS();
+    if (c == ((j1 >> 1) & 3) && rowok && i >= n - 2) pb[i] = (j1 & 1) ? a[0][1] : a[0][0];
+  }
+#undef EIG_SHIFT_SLOTS
+  __syncthreads();
+  if (tid == 0) {
+    if (n >= 2) {
+      const double* col = colb[(n - 2) & 1];  // column n-2 (published at k = n-3, or initial)
+      dg[n - 2] = col[n - 2];
+      dg[n - 1] = pb[n - 1];
+      const double e = col[n - 1];
+      e2[n - 2] = e * e;
+    } else {
+      dg[0] = colb[0][0];
+    }
+    double lo = 0.0, hi = 0.0;
+    for (int r = 0; r < n; ++r) {
+      double rr = 0.0;
+      if (r > 0) rr += sqrt(e2[r - 1]);
+      if (r + 1 < n) rr += sqrt(e2[r]);
+      const double aa = dg[r] - rr, bb = dg[r] + rr;
+      if (r == 0 || aa < lo) lo = aa;
+      if (r == 0 || bb > hi) hi = bb;
+    }
+    const double span = hi - lo;
+    bnd[0] = lo - span * 1e-3 - 1e-300;
+    bnd[1] = hi + span * 1e-3 + 1e-300;
+  }
+  __syncthreads();
+  // ---- 512-way multisection: 6 rounds of 9 bits
+  double lo = bnd[0], hi = bnd[1];
+  for (int it = 0; it < 7; ++it) {
+    const double width = hi - lo;
+    const double sigma = lo + width * ((double)(tid + 1) / 513.0);
+    const int cnt = sturm_count_fast(dg, e2, n, sigma);
+    const unsigned long long mk = __ballot(cnt >= 1);
+    if (lane == 0) masks[w] = mk;
+    __syncthreads();
+    int f = -1;
+    for (int q = 0; q < 8 && f < 0; ++q)
+      if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
+    __syncthreads();
+    if (f < 0) {
+      lo = lo + width * (512.0 / 513.0);
+    } else {
+      hi = lo + width * ((double)(f + 1) / 513.0);
+      if (f > 0) lo = lo + width * ((double)f / 513.0);
+    }
+  }
+  ER_STAMP(5)
+  if (tid == 0) out[blockIdx.x] = (lo + hi) * 0.5;
+#undef ER_STAMP
+}
+
 #ifdef CLRSDP_EIG_STAMPS
 __device__ unsigned long long g_eig_stamps[8];
 #define EIG_STAMP(slot)                                                     \

@@ -1,0 +1,76 @@
+// Latency probe for the building blocks of the per-column loops of the on-chip factorisation
+// and eigen kernels: workgroup barrier, LDS round trip, DPP wave sum, fp64 sqrt/div chains.
+// Prints cycles (s_memtime) per loop iteration, averaged over the workgroups.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include "../../clustered-low-rank-sdp-solver_amd/csrc/kernels_dense.h"
+using namespace clrsdp;
+#define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP %s @%d\n",hipGetErrorString(e),__LINE__); return 1;} }while(0)
+
+template <int MODE>
+__global__ void probe(double* out, unsigned long long* cyc, int iters) {
+  __shared__ double buf[1024];
+  const int tid = threadIdx.x;
+  double x = tid * 1e-3 + 1.0;
+  buf[tid & 1023] = x;
+  __syncthreads();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    if (MODE == 0) {          // barrier only
+      __syncthreads();
+    } else if (MODE == 1) {   // LDS write -> barrier -> LDS read (dependent)
+      buf[tid & 1023] = x;
+      __syncthreads();
+      x = buf[(tid + 64) & 1023] * 0.5 + 0.5;
+    } else if (MODE == 2) {   // DPP wave sum (dependent chain)
+      x = wave_sum_dpp(x) * 1e-3;
+    } else if (MODE == 3) {   // shfl wave sum
+      x = wave_sum(x) * 1e-3;
+    } else if (MODE == 4) {   // sqrt + div chain
+      x = 2.0 / (sqrt(x) + 1.0) + 0.5;
+    } else if (MODE == 5) {   // dependent fp64 fma chain of 16
+#pragma unroll
+      for (int q = 0; q < 16; ++q) x = fma(x, 0.999, 1e-3);
+    } else if (MODE == 6) {   // LDS read dependent chain (no barrier)
+      x = buf[((int)x + tid) & 1023];
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * blockDim.x + tid] = x;
+  if (tid == 0) atomicAdd(cyc, t1 - t0);
+}
+
+template <int MODE>
+int run(const char* name, int threads, int blocks) {
+  double* o; unsigned long long* c;
+  CK(hipMalloc(&o, 1024 * 1024 * 8)); CK(hipMalloc(&c, 8));
+  CK(hipMemset(c, 0, 8));
+  const int iters = 2000;
+  probe<MODE><<<blocks, threads>>>(o, c, iters);
+  CK(hipDeviceSynchronize());
+  CK(hipMemset(c, 0, 8));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  probe<MODE><<<blocks, threads>>>(o, c, iters);
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long h; CK(hipMemcpy(&h, c, 8, hipMemcpyDeviceToHost));
+  printf("%-28s threads %4d blocks %4d: %8.1f cycles/iter  %8.2f ns/iter (event)\n", name, threads, blocks, (double)h / blocks / iters, ms * 1e6 / iters);
+  CK(hipFree(o)); CK(hipFree(c));
+  return 0;
+}
+
+int main() {
+  for (int th : {64, 256, 512, 1024}) {
+    run<0>("barrier", th, 128);
+    run<1>("lds write+barrier+read", th, 128);
+  }
+  run<2>("dpp wave sum (6 steps)", 512, 128);
+  run<3>("shfl wave sum (6 steps)", 512, 128);
+  run<4>("sqrt+div", 512, 128);
+  run<5>("16 dependent fp64 fma", 512, 128);
+  run<5>("16 dependent fp64 fma", 64, 128);
+  run<6>("dependent LDS read", 512, 128);
+  run<6>("dependent LDS read", 64, 128);
+  return 0;
+}
