@@ -348,6 +348,11 @@ struct Solver final : HandleBase {
   TupleDesc* d_td = nullptr;
   TupleBlock* d_tb = nullptr;
   hipEvent_t ev[CLRSDP_NUM_STAGES + 1];
+  // side stream: the local residuals overlap the Schur factorisation, chol(Q) overlaps the
+  // first part of the predictor (iterate only; run_stage stays serial)
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_s = nullptr, ev_r = nullptr, ev_qa = nullptr, ev_q = nullptr;
+  bool pending_q = false;
   float phase_ms[CLRSDP_NUM_STAGES];
 
   int nb() const { return (int)lb.size(); }
@@ -444,6 +449,9 @@ struct Solver final : HandleBase {
     HIPCHK(hipStreamCreateWithFlags(&own_stream, hipStreamNonBlocking));
     stream = own_stream;
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&ev_s, &ev_r, &ev_qa, &ev_q})
+      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
     build_plans();
   }
@@ -459,6 +467,9 @@ struct Solver final : HandleBase {
     (void)hipFree(rsums);
     (void)hipFree(info);
     for (auto& e : ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ev_s, ev_r, ev_qa, ev_q})
+      if (e) (void)hipEventDestroy(e);
+    if (aux) (void)hipStreamDestroy(aux);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 
@@ -970,6 +981,10 @@ struct Solver final : HandleBase {
                                                                  BY, S, n_pairs);
   }
   void st_factor() {
+    factor_local();
+    factor_q();
+  }
+  void factor_local() {
     if (reg_S) {                              // S_j <- L_j^-1 in place; W_j = L_j^-1 B_j (MFMA)
       ci_S.launch(stream, info + info_S0);
       if (nc2) {                              // 2x2 blocked L^-1 for 128 < dim_S <= 256
@@ -995,6 +1010,9 @@ struct Solver final : HandleBase {
     else fill(xsend, 0.0, q2);
     exchange(2, q2);
     slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(xrecv, world, q2, q2, Q);
+  }
+  void factor_q() {
+    const int64_t q2 = n_y * n_y;
     if (reg_Q) {
       ci_Q.launch(stream, info + info_Q0);    // Qf = L_Q^-1
     } else {
@@ -1003,6 +1021,11 @@ struct Solver final : HandleBase {
     }
   }
   void st_residuals(bool use_AY) {
+    residuals_local(use_AY);
+    residuals_finish();
+  }
+  // P, d, the p-slabs and the local error maxima (no exchange: may run on the side stream)
+  void residuals_local(bool use_AY) {
     // P = sum_i x_i A_i - X - C
     weighted_A(x, p_wA_P, P);
     blk_lin(P, P, 1.0, X, -1.0);
@@ -1014,14 +1037,17 @@ struct Solver final : HandleBase {
       colsums();
     }
     trace_aggregate(use_AY ? AY : tval, cvec, 1.0, tmpv, -1.0, -1.0, dvec);
-    // p partial = sum_j B_j^T x_j ; errors
+    // p partial = sum_j B_j^T x_j (slabs) ; local maxima of |P| and |d| into tmpsc[0..1]
     p_Btx.launch(stream, 1.0, 0.0);
+    local_blk_reduce(P, nullptr, nullptr, nullptr, 2, tmpsc);
+    if (nx > 0) vec_reduce<T><<<1, 256, 0, stream>>>(dvec, nullptr, nx, 2, tmpsc + 1);
+    else fill(tmpsc + 1, 0.0, 1);
+  }
+  void residuals_finish() {
     const int64_t k = n_y + 2;
     if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
     else fill(xsend, 0.0, n_y);
-    local_blk_reduce(P, nullptr, nullptr, nullptr, 2, xsend + n_y);
-    if (nx > 0) vec_reduce<T><<<1, 256, 0, stream>>>(dvec, nullptr, nx, 2, xsend + n_y + 1);
-    else fill(xsend + n_y + 1, 0.0, 1);
+    vlin(xsend + n_y, tmpsc, 1.0, nullptr, 0, nullptr, 0, 2);
     exchange(3, k);
     slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, k, n_y, uvec);
     vlin(pvec, bvec, 1.0, uvec, -1.0, nullptr, 0, n_y);      // p = b - sum B^T x
@@ -1051,6 +1077,10 @@ struct Solver final : HandleBase {
     exchange(tag, n_y);
     slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec);
     vlin(dyv, pvec, 1.0, uvec, -1.0, nullptr, 0, n_y);
+    if (pending_q) {  // L_Q^-1 is being computed on the side stream (iterate)
+      HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
+      pending_q = false;
+    }
     if (reg_Q) {
       q_q1.launch(stream, 1.0, 0.0);          // u = L_Q^-1 r
       q_q2.launch(stream, 1.0, 0.0);          // dy = L_Q^-T u
@@ -1201,9 +1231,42 @@ struct Solver final : HandleBase {
   int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
     HIPCHK(hipMemsetAsync(info, 0, info_count * sizeof(int), stream));
-    for (int s = 0; s < CLRSDP_NUM_STAGES; ++s) {
+    auto mark = [&](int s) {
       if (timing) HIPCHK(hipEventRecord(ev[s], stream));
+    };
+    for (int s = 0; s <= CLRSDP_STAGE_SCHUR; ++s) {
+      mark(s);
       stage(s, prm, pd_feas);
+    }
+    // side stream: P, d, p-slabs (need the state and A_Y only)
+    const hipStream_t main_s = stream;
+    HIPCHK(hipEventRecord(ev_s, main_s));
+    HIPCHK(hipStreamWaitEvent(aux, ev_s, 0));
+    stream = aux;
+    residuals_local(true);
+    HIPCHK(hipEventRecord(ev_r, aux));
+    stream = main_s;
+    mark(CLRSDP_STAGE_FACTOR);
+    factor_local();
+    // side stream: chol(Q) -> L_Q^-1, waited for just before the first Q solve
+    HIPCHK(hipEventRecord(ev_qa, main_s));
+    HIPCHK(hipStreamWaitEvent(aux, ev_qa, 0));
+    stream = aux;
+    factor_q();
+    HIPCHK(hipEventRecord(ev_q, aux));
+    stream = main_s;
+    pending_q = true;
+    mark(CLRSDP_STAGE_RESIDUALS);
+    HIPCHK(hipStreamWaitEvent(main_s, ev_r, 0));
+    residuals_finish();
+    HIPCHK(hipGetLastError());
+    for (int s = CLRSDP_STAGE_PREDICTOR; s < CLRSDP_NUM_STAGES; ++s) {
+      mark(s);
+      stage(s, prm, pd_feas);
+    }
+    if (pending_q) {
+      HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
+      pending_q = false;
     }
     if (timing) HIPCHK(hipEventRecord(ev[CLRSDP_NUM_STAGES], stream));
     std::memset(st, 0, sizeof(*st));
