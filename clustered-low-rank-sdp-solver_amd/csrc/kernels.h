@@ -432,6 +432,46 @@ __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__
 // the rows, LDS combine of the 4 partials in a fixed order).  TA = true: each wave owns 16
 // outputs (columns of A) and sweeps each with 64 lanes along k + a fixed butterfly.
 // ------------------------------------------------------------------------------------------
+// In-register cross-lane sums of doubles (no LDS round trip, unlike __shfl_xor which is a
+// ds_bpermute): DPP quad permutes and row mirrors for lane distances 1..8, v_permlane16/32_swap
+// (CDNA4) for 16 and 32.  Every lane ends with the same, order-independent result.
+template <int CTRL>
+__device__ inline double dpp_d(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ inline double xsum16(double x) {  // x + x[lane ^ 16]
+  const auto rl = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(x), false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(x), false, false);
+  return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+}
+__device__ inline double xsum32(double x) {  // x + x[lane ^ 32]
+  const auto rl = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(x), false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(x), false, false);
+  return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+}
+__device__ inline double row16_sum(double x) {  // sum over the 16 lanes of a DPP row
+  x += dpp_d<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_d<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_d<0x141>(x);  // row_half_mirror
+  x += dpp_d<0x140>(x);  // row_mirror
+  return x;
+}
+__device__ inline double wave_sum_dpp(double x) { return xsum32(xsum16(row16_sum(x))); }
+__device__ inline double readlane_d(double x, int l) {  // l must be wave-uniform
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                          __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+__device__ inline double swap16_d(double x) {  // value of lane ^ 16
+  const auto rl = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(x), false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(x), false, false);
+  // lanes 0-15 / 32-47 keep their value in [0] and receive the partner's in [1]; the odd rows
+  // the other way round
+  const bool low = ((__lane_id() >> 4) & 1) == 0;
+  return low ? __hiloint2double(rh[1], rl[1]) : __hiloint2double(rh[0], rl[0]);
+}
+
 template <class T>
 __device__ __forceinline__ T shfl_xor_t(T v, int o) {
   if constexpr (sizeof(T) == 8) {
@@ -446,6 +486,24 @@ __device__ __forceinline__ T shfl_xor_t(T v, int o) {
   }
 }
 
+// sum over the 16 lanes of a row (lanes 16r..16r+15)
+template <class T>
+__device__ __forceinline__ T row16_sum_t(T v) {
+  if constexpr (sizeof(T) == 8) {
+    return row16_sum(v);
+  } else {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += shfl_xor_t(v, o);
+    return v;
+  }
+}
+
+// y = alpha op(A) x + beta y for every problem; 64 outputs per 256-thread workgroup.
+//  !TA: thread (row r = tid & 63, k-group g = tid >> 6) sums k = g, g+4, ... with 8 loads in
+//       flight; the 4 k-groups are combined through LDS.
+//   TA: wave w owns 16 outputs (columns); lane (k-offset kk = lane & 15, column c4 = lane >> 4)
+//       streams 4 columns at once (16 consecutive k per column per load instruction), 4 column
+//       groups x 2 k-steps of loads in flight; each column sum is a 16-lane DPP reduction.
 template <class T, bool TA>
 __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restrict__ descs,
                                                     const int* __restrict__ t2d, double alpha,
@@ -455,13 +513,28 @@ __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restric
   const int tid = threadIdx.x;
   const T* __restrict__ A = d.A;
   const T* __restrict__ x = d.B;
+  const int K = d.K;
   if (!TA) {
     __shared__ T part[4][64];
     const int r = tid & 63, g = tid >> 6, i = o0 + r;
-    T acc = T(0.0);
-    if (i < d.M)
-      for (int k = g; k < d.K; k += 4) acc += A[i + (size_t)k * d.lda] * x[k];
-    part[g][r] = acc;
+    const int ic = min(i, d.M - 1);
+    T acc0 = T(0.0), acc1 = T(0.0);
+    int k = g;
+    for (; k + 28 < K; k += 32) {
+      T a[8], xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = A[ic + (size_t)(k + 4 * u) * d.lda];
+        xv[u] = x[k + 4 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        acc0 += a[u] * xv[u];
+        acc1 += a[u + 1] * xv[u + 1];
+      }
+    }
+    for (; k < K; k += 4) acc0 += A[ic + (size_t)k * d.lda] * x[k];
+    part[g][r] = acc0 + acc1;
     __syncthreads();
     if (g == 0 && i < d.M) {
       T v = ((part[0][r] + part[1][r]) + (part[2][r] + part[3][r])) * T(alpha);
@@ -469,16 +542,35 @@ __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restric
       d.C[i] = v;
     }
   } else {
-    const int lane = tid & 63, w = tid >> 6;
-    for (int c = 0; c < 16; ++c) {
-      const int j = o0 + w * 16 + c;
-      if (j >= d.M) break;
-      const T* col = A + (size_t)j * d.lda;
-      T acc = T(0.0);
-      for (int k = lane; k < d.K; k += 64) acc += col[k] * x[k];
-      for (int o = 32; o > 0; o >>= 1) acc += shfl_xor_t(acc, o);
-      if (lane == 0) {
-        T v = acc * T(alpha);
+    const int lane = tid & 63, w = tid >> 6, kk = lane & 15, c4 = lane >> 4;
+    const int jb = o0 + w * 16;  // this wave's 16 columns: jb + 4q + c4, q = 0..3
+    const T* col[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) col[q] = A + (size_t)min(jb + 4 * q + c4, d.M - 1) * d.lda;
+    T acc[4] = {T(0.0), T(0.0), T(0.0), T(0.0)};
+    int k = kk;
+    for (; k + 16 < K; k += 32) {
+      T a0[4], a1[4];
+      const T x0 = x[k], x1 = x[k + 16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a0[q] = col[q][k];
+        a1[q] = col[q][k + 16];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += a0[q] * x0 + a1[q] * x1;
+    }
+    if (k < K) {
+      const T x0 = x[k];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += col[q][k] * x0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const T s = row16_sum_t(acc[q]);
+      const int j = jb + 4 * q + c4;
+      if (kk == 0 && j < d.M) {
+        T v = s * T(alpha);
         if (beta != 0.0) v += d.Cin[j] * T(beta);
         d.C[j] = v;
       }

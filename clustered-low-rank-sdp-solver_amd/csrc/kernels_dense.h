@@ -12,34 +12,6 @@
 namespace clrsdp {
 
 // Deterministic block reduction for 512 threads: wave butterfly, then 8 wave sums in order.
-// In-register cross-lane sums of doubles (no LDS round trip, unlike __shfl_xor which is a
-// ds_bpermute): DPP quad permutes and row mirrors for lane distances 1..8, v_permlane16/32_swap
-// (CDNA4) for 16 and 32.  Every lane ends with the same, order-independent result.
-template <int CTRL>
-__device__ inline double dpp_d(double x) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-__device__ inline double xsum16(double x) {  // x + x[lane ^ 16]
-  const auto rl = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(x), false, false);
-  const auto rh = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(x), false, false);
-  return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
-}
-__device__ inline double xsum32(double x) {  // x + x[lane ^ 32]
-  const auto rl = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(x), false, false);
-  const auto rh = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(x), false, false);
-  return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
-}
-__device__ inline double row16_sum(double x) {  // sum over the 16 lanes of a DPP row
-  x += dpp_d<0xB1>(x);   // quad_perm [1,0,3,2]
-  x += dpp_d<0x4E>(x);   // quad_perm [2,3,0,1]
-  x += dpp_d<0x141>(x);  // row_half_mirror
-  x += dpp_d<0x140>(x);  // row_mirror
-  return x;
-}
-__device__ inline double wave_sum_dpp(double x) { return xsum32(xsum16(row16_sum(x))); }
-
 template <class T>
 __device__ T wave_sum(T v) {
   for (int s = 32; s > 0; s >>= 1) {
@@ -738,74 +710,57 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
     // trip: the owners publish column j of A and row j of X (unscaled), every lane reads the
     // pivot, its l_ij, the l_cj of its columns and X_j, and scales by r = 1/sqrt(a_jj)
     // (v_rsq_f64 + one Newton step: no fp64 divide or sqrt on the critical path).
-#ifdef CLRSDP_SKIP_DIAG
-    if (w == 0) { for (int e = lane; e < 256; e += 64) Dinv[e] = ((e & 15) == (e >> 4)) ? 1.0 : 0.0; }
-    if (false) {
-#else
     if (w == 0) {
-#endif
-      const int i = lane & 15, cg = lane >> 4;
-      double a[4], x[4];
+      // Lanes 0-15 hold row i of A_kk (-> L_kk), lanes 16-31 row i of X_kk (-> L_kk^-1), 16
+      // values each in registers; the column loop is unrolled so every index is static and
+      // the cross-lane traffic is v_readlane (uniform source lane) plus one permlane16 swap.
+      const int i = lane & 15, grp = lane >> 4;
+      double v[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = 4 * cg + q;
-        a[q] = (c <= i) ? A[LI::idx(k0 + i, k0 + c)] : 0.0;
-        x[q] = (c == i) ? 1.0 : 0.0;
+      for (int c = 0; c < 16; ++c) {
+        const double av = A[LI::idx(k0 + i, k0 + min(c, i))];
+        v[c] = grp == 0 ? (c <= i ? av : 0.0) : (c == i ? 1.0 : 0.0);
       }
-      double* colL = Dinv;         // 16: column j of the partially factored block
-      double* rowX = Dinv + 16;    // 16: row j of X (unscaled)
       int bad = 0;
-      // publish column 0 and row 0 (non-owners write to a scratch slot: no branches)
-      double* scratch = Dinv + 64;  // 64 dummy slots
-      colL[cg == 0 ? i : 64 + lane] = a[0];
-      if (i == 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) rowX[4 * cg + q] = x[q];
-      }
-#pragma unroll 1
       for (int j = 0; j < 16; ++j) {
-        __builtin_amdgcn_wave_barrier();
-        const double djj = colL[j];
-        const double ci = colL[i];
-        double cc[4], xr[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          cc[q] = colL[4 * cg + q];
-          xr[q] = rowX[4 * cg + q];
-        }
+        const double djj = readlane_d(v[j], j);
         bad |= !(djj > 0.0);
         double r = __builtin_amdgcn_rsq(djj);
         r = r * (1.5 - 0.5 * djj * r * r);  // Newton step: r = 1/sqrt(d) to ~1 ulp
-        const bool diag = (i == j), below = (i > j);
-        const double lij = diag ? djj * r : ci * r;
-        const double lr_ = lij * r;
-        __builtin_amdgcn_wave_barrier();    // every lane has read column j / row j
+        // l_ij (meaningful in lanes 0-15 with i >= j); lanes 16-31 get their row's l_ij by a swap
+        const double lij = (i == j) ? djj * r : v[j] * r;
+        const double lsw = swap16_d(lij);
+        double xj[16];  // row j of X before its scaling (columns <= j), uniform
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int c = 4 * cg + q;
-          const double upd = a[q] - lr_ * cc[q];
-          a[q] = (c == j && i >= j) ? lij : ((below && c > j && c <= i) ? upd : a[q]);
-          x[q] = diag ? x[q] * r : (below ? x[q] - lr_ * xr[q] : x[q]);
+        for (int c = 0; c <= j; ++c) xj[c] = readlane_d(v[c], 16 + j);
+        double lk[16];  // column j of L below the diagonal, uniform
+#pragma unroll
+        for (int t = j + 1; t < 16; ++t) lk[t] = readlane_d(lij, t);
+        // branch-free (selects), so the scheduler can overlap consecutive columns:
+        //   lanes 0-15:  v_j = l_ij (i >= j);  v_t -= l_ij l_tj  (j < t <= i)
+        //   lanes 16-31: row j scaled by r;    v_c -= (l_ij r) x_jc (c <= j, i > j)
+        const bool g0 = grp == 0, below = i > j;
+        const double m = lsw * r;
+        if (j < 16) v[j] = (g0 && i >= j) ? lij : v[j];
+#pragma unroll
+        for (int t = j + 1; t < 16; ++t) {
+          const double u = v[t] - lij * lk[t];
+          v[t] = (g0 && below && t <= i) ? u : v[t];
         }
-        // publish column j+1 of A (rows >= j+1) and row j+1 of X
-        const int jn = j + 1;
-        double an = a[0];
 #pragma unroll
-        for (int q = 1; q < 4; ++q) an = (q == (jn & 3)) ? a[q] : an;
-        const bool own = (cg == (jn >> 2)) && (i >= jn) && (jn < 16);
-        colL[own ? i : 64 + lane] = an;
-        if (i == jn) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) rowX[4 * cg + q] = x[q];
+        for (int c = 0; c <= j; ++c) {
+          const double ux = (i == j) ? v[c] * r : v[c] - m * xj[c];
+          v[c] = (!g0 && i >= j) ? ux : v[c];
         }
       }
-      (void)scratch;
-      __builtin_amdgcn_wave_barrier();
+      if (grp == 0) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = 4 * cg + q;
-        A[LI::idx(k0 + i, k0 + c)] = (c <= i) ? a[q] : 0.0;
-        Dinv[c * 16 + i] = x[q];  // column-major L_kk^-1 (colL/rowX no longer needed)
+        for (int c = 0; c < 16; ++c)
+          if (c <= i) A[LI::idx(k0 + i, k0 + c)] = v[c];
+      } else if (grp == 1) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) Dinv[c * 16 + i] = v[c];  // column-major L_kk^-1
       }
       if (lane == 0 && bad) *flag = k0 + 1;
     }

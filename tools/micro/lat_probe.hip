@@ -60,6 +60,68 @@ int run(const char* name, int threads, int blocks) {
   return 0;
 }
 
+
+// the 16x16 Cholesky + inverse of chol_inv_mfma's diagonal phase, one wave, in a loop
+template <int VAR>
+__global__ void diag16(double* out, unsigned long long* cyc, int iters) {
+  const int lane = threadIdx.x & 63, i = lane & 15, grp = lane >> 4;
+  double v[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) v[c] = grp == 0 ? (c < i ? 0.01 * (c + 1) : (c == i ? 4.0 : 0.0)) : (c == i ? 1.0 : 0.0);
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double djj = VAR == 1 ? 4.0 + v[j] * 1e-30 : readlane_d(v[j], j);
+      double r;
+      if (VAR == 2) r = 0.5 + djj * 1e-30;
+      else { r = __builtin_amdgcn_rsq(djj); r = r * (1.5 - 0.5 * djj * r * r); }
+      const double lij = (i == j) ? djj * r : v[j] * r;
+      const double lsw = VAR == 3 ? lij : swap16_d(lij);
+      double xj[16];
+#pragma unroll
+      for (int c = 0; c <= j; ++c) xj[c] = VAR == 4 ? v[c] : readlane_d(v[c], 16 + j);
+      double lk[16];
+#pragma unroll
+      for (int t = j + 1; t < 16; ++t) lk[t] = VAR == 4 ? lij : readlane_d(lij, t);
+      const bool g0 = grp == 0, below = i > j;
+      const double m = lsw * r;
+      v[j] = (g0 && i >= j) ? lij : v[j];
+#pragma unroll
+      for (int t = j + 1; t < 16; ++t) {
+        const double u = v[t] - lij * lk[t];
+        v[t] = (g0 && below && t <= i) ? u : v[t];
+      }
+#pragma unroll
+      for (int c = 0; c <= j; ++c) {
+        const double ux = (i == j) ? v[c] * r : v[c] - m * xj[c];
+        v[c] = (!g0 && i >= j) ? ux : v[c];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = v[c] * 1e-3 + (c == i ? 4.0 : 0.0);  // keep it finite
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  double acc = 0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc += v[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+  if (threadIdx.x == 0) atomicAdd(cyc, t1 - t0);
+}
+template <int VAR>
+int run_diag(const char* name) {
+  double* o; unsigned long long* c;
+  CK(hipMalloc(&o, 1024 * 1024 * 8)); CK(hipMalloc(&c, 8));
+  CK(hipMemset(c, 0, 8));
+  const int iters = 200;
+  diag16<VAR><<<128, 64>>>(o, c, iters);
+  CK(hipDeviceSynchronize());
+  unsigned long long h; CK(hipMemcpy(&h, c, 8, hipMemcpyDeviceToHost));
+  printf("diag16 %-28s %8.1f cycles per 16-column factorisation\n", name, (double)h / 128 / iters);
+  CK(hipFree(o)); CK(hipFree(c));
+  return 0;
+}
+
 int main() {
   for (int th : {64, 256, 512, 1024}) {
     run<0>("barrier", th, 128);
@@ -72,5 +134,10 @@ int main() {
   run<5>("16 dependent fp64 fma", 64, 128);
   run<6>("dependent LDS read", 512, 128);
   run<6>("dependent LDS read", 64, 128);
+  run_diag<0>("full");
+  run_diag<1>("no pivot readlane");
+  run_diag<2>("no rsq");
+  run_diag<3>("no permlane swap");
+  run_diag<4>("no row/col readlanes");
   return 0;
 }
