@@ -460,12 +460,13 @@ struct Solver final : HandleBase {
     // device memory is released with the process / hipDeviceReset; free what we own explicitly
     T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, BX, BY, AY,
                  tval, S, Wm, Bm, Qslab, Q, Qf, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
-                 bvec, dyv, pvec, uvec, sc, bpart, eigX, tmpsc, tC, Stmp, own_send, Vt};
+                 bvec, dyv, pvec, uvec, bpart, eigX, tmpsc, tC, Stmp, own_send, Vt};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
     (void)hipFree(ksamp);
     (void)hipFree(rsums);
-    (void)hipFree(info);
+    if (stat_dev) (void)hipFree(stat_dev);
+    if (stat_host) (void)hipHostFree(stat_host);
     for (auto& e : ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_s, ev_r, ev_qa, ev_q})
       if (e) (void)hipEventDestroy(e);
@@ -493,7 +494,8 @@ struct Solver final : HandleBase {
     pslab = dmalloc<T>((size_t)std::max(nc(), 1) * n_y);
     y = dmalloc<T>(n_y); bvec = dmalloc<T>(n_y); dyv = dmalloc<T>(n_y); pvec = dmalloc<T>(n_y);
     uvec = dmalloc<T>(n_y);
-    sc = dmalloc<T>(SC_COUNT);
+    // sc and the status words share one allocation (one D2H copy per iteration, pinned host
+    // mirror) -- see stat_alloc()
     bpart = dmalloc<T>(std::max(nb(), 256));
     eigX = dmalloc<T>(2 * std::max(nb(), 1));
     eigY = eigX + std::max(nb(), 1);  // X-side and Y-side minima of one batched eigen launch
@@ -513,7 +515,7 @@ struct Solver final : HandleBase {
     info_Y0 = nb();
     info_S0 = 2 * nb();
     info_Q0 = 2 * nb() + nc() + nc2;
-    info = dmalloc<int>(info_count + 1);  // + the OR of all entries (update guard)
+    stat_alloc();
     xcap = n_y * n_y + n_y + 16;
     own_send = dmalloc<T>(xcap);
     xsend = own_send;
@@ -854,8 +856,17 @@ struct Solver final : HandleBase {
     if (rc != 0) throw ClrsdpError{CLRSDP_E_EXCHANGE, "exchange callback failed"};
   }
   // reduce slot `slot` of every rank's partial vector (length cnt) in rank order into dst
-  void reduce_ranks(int64_t cnt, int64_t slot, int op, T* dst) {
-    ordered_reduce<T><<<1, 1, 0, stream>>>(xrecv + slot, world, cnt, op, dst);
+  // rank-ordered reduction of slot `slot` of every rank's partials into sc[dst]; folded into
+  // the next scalar_kernel launch (flush_scalars() at the latest, before xsend is reused)
+  std::vector<FoldRed<T>> pend;
+  void reduce_ranks(int64_t cnt, int64_t slot, int op, int dst) {
+    pend.push_back(FoldRed<T>{xrecv + slot, cnt, world, op, dst, 0});
+  }
+  void fold(const T* src, int cnt, int op, int dst) {
+    pend.push_back(FoldRed<T>{src, 1, cnt, op, dst, 0});
+  }
+  void flush_scalars() {
+    if (!pend.empty()) scalars(nullptr, 0, -1);
   }
 
   // ---------------- kernels shorthands
@@ -896,8 +907,38 @@ struct Solver final : HandleBase {
     p.pd_feas = pd_feas;
     return p;
   }
+  bool zero_cy = false;
+  // ---- scalar slots + status words: one device block, one pinned host mirror
+  char* stat_dev = nullptr;
+  char* stat_host = nullptr;
+  size_t stat_bytes = 0, stat_info_off = 0;
+  void stat_alloc() {
+    stat_info_off = ((SC_COUNT * sizeof(T)) + 63) / 64 * 64;
+    stat_bytes = stat_info_off + (info_count + 1) * sizeof(int);  // + the OR (update guard)
+    stat_dev = dmalloc<char>(stat_bytes);
+    HIPCHK(hipHostMalloc((void**)&stat_host, stat_bytes, hipHostMallocDefault));
+    sc = reinterpret_cast<T*>(stat_dev);
+    info = reinterpret_cast<int*>(stat_dev + stat_info_off);
+  }
+  // copy scalars + status to the host mirror and wait
+  void stat_fetch() {
+    HIPCHK(hipMemcpyAsync(stat_host, stat_dev, stat_bytes, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
   void scalars(const clrsdp_params* prm, int pd_feas, int which) {
-    scalar_kernel<T><<<1, 1, 0, stream>>>(sc, sparams(prm, pd_feas), which);
+    ScalarParams<T> p = prm ? sparams(prm, pd_feas) : ScalarParams<T>{};
+    p.zero_cy = zero_cy ? 1 : 0;
+    size_t q = 0;
+    while (q < pend.size() || q == 0) {  // at most 6 folded reductions per launch
+      const size_t cnt = std::min<size_t>(6, pend.size() - q);
+      p.nred = (int)cnt;
+      for (size_t i = 0; i < cnt; ++i) p.red[i] = pend[q + i];
+      q += cnt;
+      const bool last = q >= pend.size();
+      scalar_kernel<T><<<1, 1, 0, stream>>>(sc, p, last ? which : -1);
+      if (last) break;
+    }
+    pend.clear();
   }
   // local block-sum (op 0/1) or block-max (op 2) into *dst
   static constexpr int RED_G = 256;  // fixed chunking of the flat reductions (deterministic)
@@ -912,7 +953,7 @@ struct Solver final : HandleBase {
 
   // one-workgroup fixed-tree reduction of n <= 256 partials
   void vec_reduce_tree(const T* in, int n, int op, T* dst) {
-    vec_reduce<T><<<1, 256, 0, stream>>>(in, in, n, op == 2 ? 2 : 3, dst);
+    vec_reduce<T><<<1, 1024, 0, stream>>>(in, in, n, op == 2 ? 2 : 3, dst);
   }
 
   // trace_A with the products U already in TX -> val (tval) -> aggregate
@@ -941,7 +982,7 @@ struct Solver final : HandleBase {
   void st_mu_r(const clrsdp_params* prm, int pd_feas) {
     local_blk_reduce(X, Y, nullptr, nullptr, 0, xsend);
     exchange(1, 1);
-    reduce_ranks(1, 0, 0, sc + SC_DOT_XY);
+    reduce_ranks(1, 0, 0, SC_DOT_XY);
     scalars(prm, pd_feas, 0);
     p_XY.launch(stream, -1.0, 0.0);             // R = -XY
     blk_lin(R, R, 1.0, nullptr, 0.0, sc + SC_MU_P);  // R += mu_p I
@@ -1040,7 +1081,7 @@ struct Solver final : HandleBase {
     // p partial = sum_j B_j^T x_j (slabs) ; local maxima of |P| and |d| into tmpsc[0..1]
     p_Btx.launch(stream, 1.0, 0.0);
     local_blk_reduce(P, nullptr, nullptr, nullptr, 2, tmpsc);
-    if (nx > 0) vec_reduce<T><<<1, 256, 0, stream>>>(dvec, nullptr, nx, 2, tmpsc + 1);
+    if (nx > 0) vec_reduce<T><<<1, 1024, 0, stream>>>(dvec, nullptr, nx, 2, tmpsc + 1);
     else fill(tmpsc + 1, 0.0, 1);
   }
   void residuals_finish() {
@@ -1051,9 +1092,10 @@ struct Solver final : HandleBase {
     exchange(3, k);
     slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, k, n_y, uvec);
     vlin(pvec, bvec, 1.0, uvec, -1.0, nullptr, 0, n_y);      // p = b - sum B^T x
-    reduce_ranks(k, n_y, 2, sc + SC_ERR_PMAT);
-    reduce_ranks(k, n_y + 1, 2, sc + SC_ERR_DVEC);
-    vec_reduce<T><<<1, 256, 0, stream>>>(pvec, nullptr, n_y, 2, sc + SC_ERR_PVEC);
+    reduce_ranks(k, n_y, 2, SC_ERR_PMAT);
+    reduce_ranks(k, n_y + 1, 2, SC_ERR_DVEC);
+    fold(pvec, (int)n_y, 4, SC_ERR_PVEC);
+    flush_scalars();
   }
   void st_direction(int tag) {
     // Z = sym(X^-1 (P Y - R))
@@ -1107,7 +1149,7 @@ struct Solver final : HandleBase {
   void st_corrector_r(const clrsdp_params* prm, int pd_feas) {
     local_blk_reduce(X, Y, dX, dY, 1, xsend);
     exchange(5, 1);
-    reduce_ranks(1, 0, 0, sc + SC_DOT_XDY);
+    reduce_ranks(1, 0, 0, SC_DOT_XDY);
     scalars(prm, pd_feas, 1);
     p_XY.launch(stream, -1.0, 0.0);
     p_dXdY.launch(stream, -1.0, 1.0);
@@ -1137,38 +1179,51 @@ struct Solver final : HandleBase {
       t_sY2.launch(stream, false);
       e_Y.eigmin(stream, eigY);
     }
-    if (nb()) {
-      ordered_reduce<T><<<1, 1, 0, stream>>>(eigX, nb(), 1, 3, xsend);
-      ordered_reduce<T><<<1, 1, 0, stream>>>(eigY, nb(), 1, 3, xsend + 1);
+    if (world == 1 && nb()) {  // min over the blocks straight into the scalar slots
+      fold(eigX, nb(), 3, SC_MINEIG_X);
+      fold(eigY, nb(), 3, SC_MINEIG_Y);
     } else {
-      fill(xsend, 1e300, 2);  // no local blocks: neutral element of min
+      if (nb()) {
+        ordered_reduce<T><<<1, 1, 0, stream>>>(eigX, nb(), 1, 3, xsend);
+        ordered_reduce<T><<<1, 1, 0, stream>>>(eigY, nb(), 1, 3, xsend + 1);
+      } else {
+        fill(xsend, 1e300, 2);  // no local blocks: neutral element of min
+      }
+      exchange(8, 2);
+      reduce_ranks(2, 0, 3, SC_MINEIG_X);
+      reduce_ranks(2, 1, 3, SC_MINEIG_Y);
     }
-    exchange(8, 2);
-    reduce_ranks(2, 0, 3, sc + SC_MINEIG_X);
-    reduce_ranks(2, 1, 3, sc + SC_MINEIG_Y);
     scalars(prm, pd_feas, 2);
   }
   void objectives(const clrsdp_params* prm, int pd_feas) {
-    if (nx > 0) vec_reduce<T><<<1, 256, 0, stream>>>(cvec, x, nx, 0, xsend);
-    else fill(xsend, 0.0, 1);
-    if (hasC) local_blk_reduce(Cm, Y, nullptr, nullptr, 0, xsend + 1);
-    else fill(xsend + 1, 0.0, 1);
-    exchange(9, 2);
-    reduce_ranks(2, 0, 0, sc + SC_DOT_CX);
-    reduce_ranks(2, 1, 0, sc + SC_DOT_CY);
-    vec_reduce<T><<<1, 256, 0, stream>>>(bvec, y, n_y, 0, sc + SC_DOT_BY);
+    zero_cy = !hasC;
+    if (world == 1) {
+      if (nx > 0) vec_reduce<T><<<1, 1024, 0, stream>>>(cvec, x, nx, 0, sc + SC_DOT_CX);
+      else fill(sc + SC_DOT_CX, 0.0, 1);
+      if (hasC) local_blk_reduce(Cm, Y, nullptr, nullptr, 0, sc + SC_DOT_CY);
+    } else {
+      if (nx > 0) vec_reduce<T><<<1, 1024, 0, stream>>>(cvec, x, nx, 0, xsend);
+      else fill(xsend, 0.0, 1);
+      if (hasC) local_blk_reduce(Cm, Y, nullptr, nullptr, 0, xsend + 1);
+      else fill(xsend + 1, 0.0, 1);
+      exchange(9, 2);
+      reduce_ranks(2, 0, 0, SC_DOT_CX);
+      reduce_ranks(2, 1, 0, SC_DOT_CY);
+    }
+    vec_reduce<T><<<1, 1024, 0, stream>>>(bvec, y, n_y, 0, sc + SC_DOT_BY);
     scalars(prm, pd_feas, 3);
+    zero_cy = false;
   }
   void st_update(const clrsdp_params* prm, int pd_feas) {
     int* flag = info + info_count;
     status_reduce<<<1, 256, 0, stream>>>(info, info_count, flag);
-    if (nx > 0) vec_axpy_dev<T><<<cdiv(nx, 256), 256, 0, stream>>>(x, dx, sc + SC_ALPHA_P, nx, flag);
-    vec_axpy_dev<T><<<cdiv(n_y, 256), 256, 0, stream>>>(y, dyv, sc + SC_ALPHA_D, n_y, flag);
-    if (nb()) {
-      const unsigned g = std::min<unsigned>(cdiv(nblk_el, 256), 4096);
-      vec_axpy_dev<T><<<g, 256, 0, stream>>>(X, dX, sc + SC_ALPHA_P, nblk_el, flag);
-      vec_axpy_dev<T><<<g, 256, 0, stream>>>(Y, dY, sc + SC_ALPHA_D, nblk_el, flag);
-    }
+    AxpyList<T> L;
+    L.it[0] = AxpyItem<T>{X, dX, sc + SC_ALPHA_P, nblk_el};
+    L.it[1] = AxpyItem<T>{Y, dY, sc + SC_ALPHA_D, nblk_el};
+    L.it[2] = AxpyItem<T>{x, dx, sc + SC_ALPHA_P, nx};
+    L.it[3] = AxpyItem<T>{y, dyv, sc + SC_ALPHA_D, n_y};
+    const unsigned g = std::max<unsigned>(1, std::min<unsigned>(cdiv(std::max<int64_t>(nblk_el, nx), 256), 2048));
+    vec_axpy_list<T><<<dim3(g, 4), 256, 0, stream>>>(L, flag);
     objectives(prm, pd_feas);
   }
 
@@ -1189,10 +1244,9 @@ struct Solver final : HandleBase {
     HIPCHK(hipGetLastError());
   }
 
+  // both parse the host mirror filled by stat_fetch()
   int check_info() {
-    std::vector<int> h(info_count);
-    HIPCHK(hipMemcpyAsync(h.data(), info, info_count * sizeof(int), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
+    const int* h = reinterpret_cast<const int*>(stat_host + stat_info_off);
     for (int i = 0; i < nb(); ++i)
       if (h[i]) { err = "X block not positive definite (spd_inv! failed)"; return CLRSDP_E_NOT_PD_X; }
     for (int i = 0; i < nc() + nc2; ++i)
@@ -1204,9 +1258,7 @@ struct Solver final : HandleBase {
   }
 
   void read_stats(clrsdp_iter_stats* st) {
-    std::vector<T> h(SC_COUNT);
-    HIPCHK(hipMemcpyAsync(h.data(), sc, SC_COUNT * sizeof(T), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
+    const T* h = reinterpret_cast<const T*>(stat_host);
     auto f = [&](int i) { return Num<T>::hi(h[i]); };
     st->mu = f(SC_MU);
     st->P_err = f(SC_ERR_PMAT);
@@ -1224,6 +1276,7 @@ struct Solver final : HandleBase {
     std::memset(st, 0, sizeof(*st));
     st_residuals(false);
     objectives(prm, 0);
+    stat_fetch();
     read_stats(st);
     return CLRSDP_OK;
   }
@@ -1270,6 +1323,7 @@ struct Solver final : HandleBase {
     }
     if (timing) HIPCHK(hipEventRecord(ev[CLRSDP_NUM_STAGES], stream));
     std::memset(st, 0, sizeof(*st));
+    stat_fetch();
     read_stats(st);
     if (timing)
       for (int s = 0; s < CLRSDP_NUM_STAGES; ++s) {
@@ -1286,7 +1340,8 @@ struct Solver final : HandleBase {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
     if (s == 0) HIPCHK(hipMemsetAsync(info, 0, info_count * sizeof(int), stream));
     stage(s, prm, pd_feas);
-    HIPCHK(hipStreamSynchronize(stream));
+    flush_scalars();
+    stat_fetch();
     return check_info();
   }
 

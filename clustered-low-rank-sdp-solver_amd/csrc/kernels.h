@@ -1312,20 +1312,48 @@ __global__ __launch_bounds__(256) void blk_reduce(const BlkDesc* __restrict__ bd
 
 // vector reductions over [0, n): op 0 = sum a.*b, op 2 = max |a|; single workgroup
 template <class T>
-__global__ __launch_bounds__(256) void vec_reduce(const T* a, const T* b, long long n, int op,
-                                                  T* __restrict__ out) {
-  __shared__ T red[256];
-  T acc = T(0.0);
-  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
-    if (op == 0) acc += a[e] * b[e];
-    else if (op == 3) acc += a[e];
-    else {
-      const T v = Num<T>::abs_(a[e]);
-      if (v > acc) acc = v;
+__global__ __launch_bounds__(1024) void vec_reduce(const T* a, const T* b, long long n, int op,
+                                                   T* __restrict__ out) {
+  __shared__ T red[1024];
+  // fixed assignment: thread t owns elements t + 1024 (4u + q), combined q = 0..3 in order
+  T acc[4] = {T(0.0), T(0.0), T(0.0), T(0.0)};
+  long long e = threadIdx.x;
+  for (; e + 3 * 1024 < n; e += 4 * 1024) {
+    T v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long long f = e + (long long)q * 1024;
+      v[q] = op == 0 ? a[f] * b[f] : (op == 3 ? a[f] : Num<T>::abs_(a[f]));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (op == 2) acc[q] = (v[q] > acc[q]) ? v[q] : acc[q];
+      else acc[q] += v[q];
     }
   }
-  T r = (op == 2) ? block_max(acc, red) : block_sum(acc, red);
-  if (threadIdx.x == 0) *out = r;
+  for (int q = 0; e < n; e += 1024, ++q) {
+    const T v = op == 0 ? a[e] * b[e] : (op == 3 ? a[e] : Num<T>::abs_(a[e]));
+    if (op == 2) acc[q] = (v > acc[q]) ? v : acc[q];
+    else acc[q] += v;
+  }
+  T t;
+  if (op == 2) {
+    t = acc[0];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) t = (acc[q] > t) ? acc[q] : t;
+  } else {
+    t = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int s2 = blockDim.x / 2; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) {
+      const T o = red[threadIdx.x + s2];
+      red[threadIdx.x] = (op == 2) ? ((o > red[threadIdx.x]) ? o : red[threadIdx.x]) : red[threadIdx.x] + o;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0];
 }
 
 // sum or max of `cnt` values spaced `stride` apart (fixed order), single thread -> *out
@@ -1348,7 +1376,15 @@ __global__ void slab_sum(const T* in, int cnt, long long stride, long long n, T*
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   T acc = in[e];
-  for (int i = 1; i < cnt; ++i) acc += in[(size_t)i * stride + e];
+  int i = 1;
+  for (; i + 7 < cnt; i += 8) {  // 8 loads in flight, summed in slab order
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = in[(size_t)(i + u) * stride + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; i < cnt; ++i) acc += in[(size_t)i * stride + e];
   out[e] = acc;
 }
 
@@ -1386,6 +1422,23 @@ __global__ void vec_fill(T* out, double v, long long n) {
 }
 
 // x += (*sc) * dx
+// x_q += alpha_q dx_q for up to 4 vectors (blockIdx.y = q), unless *flag (failed factorisation)
+template <class T> struct AxpyItem {
+  T* x;
+  const T* dx;
+  const T* alpha;
+  long long n;
+};
+template <class T> struct AxpyList { AxpyItem<T> it[4]; };
+template <class T>
+__global__ void vec_axpy_list(AxpyList<T> L, const int* flag) {
+  if (*flag) return;
+  const AxpyItem<T> I = L.it[blockIdx.y];
+  const T a = *I.alpha;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < I.n;
+       e += (long long)gridDim.x * blockDim.x)
+    I.x[e] = I.x[e] + a * I.dx[e];
+}
 template <class T>
 __global__ void vec_axpy_dev(T* x, const T* dx, const T* sc, long long n, const int* flag) {
   if (*flag) return;
@@ -1527,15 +1580,38 @@ enum { SC_MU = 0, SC_MU_P, SC_R, SC_BETA, SC_BETA_C, SC_MU_C, SC_ALPHA_P, SC_ALP
        SC_MINEIG_Y, SC_POBJ, SC_DOBJ, SC_ERR_PMAT, SC_ERR_PVEC, SC_ERR_DVEC, SC_DOT_XY, SC_DOT_XDY,
        SC_DOT_CX, SC_DOT_BY, SC_DOT_CY, SC_TMP0, SC_TMP1, SC_TMP2, SC_TMP3, SC_COUNT };
 
+// A fixed-order reduction folded into scalar_kernel: sc[dst] = op over cnt values spaced
+// `stride` apart (op 0 sum, 2 max, 3 min, 4 max |.|).  Used for the rank-ordered reductions of
+// the exchanged partials and other short vectors, so they cost no launch of their own.
+template <class T> struct FoldRed {
+  const T* src;
+  long long stride;
+  int cnt, op, dst, pad;
+};
 template <class T> struct ScalarParams {
   T beta_inf, beta_feas, gamma, b0;
   double dim;
   int pd_feas;
+  int nred;
+  int zero_cy;  // which == 3 without C: <C,Y> = 0
+  FoldRed<T> red[6];
 };
 
 template <class T>
 __global__ void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
   if (threadIdx.x != 0) return;
+  for (int q = 0; q < p.nred; ++q) {
+    const FoldRed<T> r = p.red[q];
+    T acc = r.op == 4 ? Num<T>::abs_(r.src[0]) : r.src[0];
+    for (int i = 1; i < r.cnt; ++i) {
+      T v = r.src[(size_t)i * r.stride];
+      if (r.op == 4) v = Num<T>::abs_(v);
+      if (r.op == 0) acc += v;
+      else if (r.op == 3) acc = (v < acc) ? v : acc;
+      else acc = (v > acc) ? v : acc;
+    }
+    sc[r.dst] = acc;
+  }
   const T dim = T(p.dim);
   if (which == 0) {  // mu, mu_p
     sc[SC_MU] = sc[SC_DOT_XY] / dim;
@@ -1566,6 +1642,7 @@ __global__ void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
     sc[SC_ALPHA_P] = ap;
     sc[SC_ALPHA_D] = ad;
   } else if (which == 3) {  // objectives
+    if (p.zero_cy) sc[SC_DOT_CY] = T(0.0);
     sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;
     sc[SC_DOBJ] = sc[SC_DOT_CY] + sc[SC_DOT_BY] + p.b0;
   }
