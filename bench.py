@@ -104,7 +104,7 @@ def main():
         from clrsdp_amd import dist as cdist
         dist = cdist.TorchExchange(local_rank)
     dev = pk.DeviceSolver(cons, b, bi, precision_words=args.precision, device=local_rank,
-                          rank=rank, world=world, owned=owned, timing=True)
+                          rank=rank, world=world, owned=owned, timing=False)
     if dist is not None:
         dist.attach(dev)
     prm = pk.make_params("0.3", "0.1", "0.7", 0)
@@ -125,15 +125,22 @@ def main():
 
     barrier_sync()
     t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    # instrumented pass (per-stage HIP events, no graph replay) for the phase breakdown and the
+    # Schur-assembly roofline; not part of the timed region above
+    dev.set_timing(True)
+    n_inst = max(3, min(args.steps, 10))
     schur_ms = 0.0
     phase = np.zeros(_lib.NUM_STAGES)
-    for _ in range(args.steps):
+    for _ in range(n_inst):
         st = step()
         ph = np.array(st.phase_ms[:])
         phase += ph
         schur_ms += ph[_lib.STAGE_SCHUR]
     barrier_sync()
-    dt = time.perf_counter() - t0
     if dist is not None:
         dt = dist.max_over_ranks(dt)
         schur_ms = dist.max_over_ranks(schur_ms)
@@ -146,7 +153,7 @@ def main():
     if world > 1:
         fl /= world   # per-rank share of the Schur work (the roofline is per GPU)
         by /= world
-    sch_s = schur_ms / 1e3 / args.steps
+    sch_s = schur_ms / 1e3 / n_inst
     achieved = fl / sch_s / 1e12
     res = {
         "metric": "interior-point iterations/sec (solverank1sdp loop body, MPMP.jl:755-887)",
@@ -169,7 +176,8 @@ def main():
                      "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
                      "schur_ms_per_iteration": sch_s * 1e3,
                      "schur_alg_gbs": by / sch_s / 1e9},
-        "phase_ms_per_iteration": {n: float(v / args.steps) for n, v in zip(_lib.STAGE_NAMES, phase)},
+        "phase_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.STAGE_NAMES, phase)},
+        "graph_replay": world == 1,
     }
     if world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(cons, b, bi)

@@ -29,7 +29,8 @@ SC = dict(mu=0, mu_p=1, r=2, beta=3, beta_c=4, mu_c=5, alpha_p=6, alpha_d=7, min
 EXPORTS = ["clrsdp_version", "clrsdp_last_error", "clrsdp_create", "clrsdp_upload_constraints",
            "clrsdp_set_state", "clrsdp_get_state", "clrsdp_initial_residuals", "clrsdp_iterate",
            "clrsdp_run_stage", "clrsdp_get_buffer", "clrsdp_exchange_bytes", "clrsdp_set_exchange",
-           "clrsdp_set_stream", "clrsdp_get_stream", "clrsdp_synchronize", "clrsdp_destroy"]
+           "clrsdp_set_stream", "clrsdp_get_stream", "clrsdp_synchronize", "clrsdp_set_timing",
+           "clrsdp_destroy"]
 
 P_i64 = C.POINTER(C.c_int64)
 P_i32 = C.POINTER(C.c_int32)
@@ -91,6 +92,7 @@ def lib():
     L.clrsdp_get_stream.restype = C.c_void_p
     L.clrsdp_get_stream.argtypes = [C.c_void_p]
     L.clrsdp_synchronize.argtypes = [C.c_void_p]
+    L.clrsdp_set_timing.argtypes = [C.c_void_p, C.c_int32]
     L.clrsdp_destroy.argtypes = [C.c_void_p]
     for name in EXPORTS:
         if name not in ("clrsdp_last_error", "clrsdp_get_stream"):

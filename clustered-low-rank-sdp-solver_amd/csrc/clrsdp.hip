@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -273,6 +274,7 @@ struct HandleBase {
   virtual void set_stream(void* s) = 0;
   virtual void* get_stream() const = 0;
   virtual void synchronize() = 0;
+  virtual void set_timing(int on) = 0;
 };
 
 template <class T>
@@ -470,6 +472,8 @@ struct Solver final : HandleBase {
     for (auto& e : ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_s, ev_r, ev_qa, ev_q})
       if (e) (void)hipEventDestroy(e);
+    for (hipGraphExec_t g : gexec)
+      if (g) (void)hipGraphExecDestroy(g);
     if (aux) (void)hipStreamDestroy(aux);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
@@ -1281,8 +1285,8 @@ struct Solver final : HandleBase {
     return CLRSDP_OK;
   }
 
-  int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
-    if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
+  // Enqueue one loop body (all stages) on `stream`, with the side stream joined back in.
+  void enqueue_iteration(const clrsdp_params* prm, int pd_feas) {
     HIPCHK(hipMemsetAsync(info, 0, info_count * sizeof(int), stream));
     auto mark = [&](int s) {
       if (timing) HIPCHK(hipEventRecord(ev[s], stream));
@@ -1322,6 +1326,40 @@ struct Solver final : HandleBase {
       pending_q = false;
     }
     if (timing) HIPCHK(hipEventRecord(ev[CLRSDP_NUM_STAGES], stream));
+  }
+
+  // One hipGraph per pd_feas value replays the whole loop body with a single launch (one
+  // process per GPU with no exchange, and no per-stage timing).  The scalar parameters are
+  // baked into the graph, so a change of them re-captures.
+  hipGraphExec_t gexec[2] = {nullptr, nullptr};
+  clrsdp_params gprm[2];
+  bool use_graph = std::getenv("CLRSDP_NO_GRAPH") == nullptr;
+  void launch_graph(const clrsdp_params* prm, int pd_feas) {
+    const int g = pd_feas ? 1 : 0;
+    if (!gexec[g] || std::memcmp(&gprm[g], prm, sizeof(*prm)) != 0) {
+      if (gexec[g]) HIPCHK(hipGraphExecDestroy(gexec[g]));
+      gexec[g] = nullptr;
+      hipGraph_t graph = nullptr;
+      HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+      try {
+        enqueue_iteration(prm, pd_feas);
+      } catch (...) {
+        (void)hipStreamEndCapture(stream, &graph);
+        if (graph) (void)hipGraphDestroy(graph);
+        throw;
+      }
+      HIPCHK(hipStreamEndCapture(stream, &graph));
+      HIPCHK(hipGraphInstantiate(&gexec[g], graph, nullptr, nullptr, 0));
+      HIPCHK(hipGraphDestroy(graph));
+      gprm[g] = *prm;
+    }
+    HIPCHK(hipGraphLaunch(gexec[g], stream));
+  }
+
+  int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
+    if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
+    if (use_graph && world == 1 && !timing) launch_graph(prm, pd_feas);
+    else enqueue_iteration(prm, pd_feas);
     std::memset(st, 0, sizeof(*st));
     stat_fetch();
     read_stats(st);
@@ -1335,6 +1373,7 @@ struct Solver final : HandleBase {
     st->status = rc;
     return rc;
   }
+  void set_timing(int on) override { timing = on; }
 
   int run_stage(int s, const clrsdp_params* prm, int pd_feas) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
@@ -1490,6 +1529,11 @@ void* clrsdp_get_stream(const clrsdp_handle* h) { return h ? h->impl->get_stream
 int32_t clrsdp_synchronize(clrsdp_handle* h) {
   if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
   GUARD(h, { h->impl->synchronize(); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->set_timing(on); return CLRSDP_OK; })
 }
 
 int32_t clrsdp_destroy(clrsdp_handle* h) {

@@ -176,6 +176,10 @@ class DeviceSolver:
     def synchronize(self):
         self.check(self.L.clrsdp_synchronize(self.h))
 
+    def set_timing(self, on: bool):
+        """Per-stage HIP-event timing on/off (off + one rank: iterate replays a hipGraph)."""
+        self.check(self.L.clrsdp_set_timing(self.h, 1 if on else 0))
+
     def set_stream(self, stream_ptr: int):
         self.check(self.L.clrsdp_set_stream(self.h, C.c_void_p(stream_ptr)))
 

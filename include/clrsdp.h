@@ -203,6 +203,10 @@ int32_t clrsdp_set_stream(clrsdp_handle* h, void* stream);
 void* clrsdp_get_stream(const clrsdp_handle* h);
 int32_t clrsdp_synchronize(clrsdp_handle* h);
 
+/* Turn the per-stage HIP-event timing (clrsdp_iter_stats.phase_ms) on or off.  With timing
+ * off and world_size 1, clrsdp_iterate replays a captured hipGraph of the loop body. */
+int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on);
+
 int32_t clrsdp_destroy(clrsdp_handle* h);
 
 #ifdef __cplusplus
