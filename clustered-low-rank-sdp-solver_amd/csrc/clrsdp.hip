@@ -69,14 +69,26 @@ template <class T> constexpr int reg_nmax() { return std::is_same<T, double>::va
 template <class T> size_t eig_lds_bytes(int n) { return sizeof(T) * ((size_t)n * n + 10 * (size_t)n + 40); }
 constexpr size_t LDS_MAX = 160 * 1024;
 
+// workgroup order for a batched launch: tile-major, problem fastest (see TileRef)
+inline std::vector<TileRef> tile_major(const std::vector<int>& ntiles) {
+  std::vector<TileRef> out;
+  int mx = 0;
+  for (int n : ntiles) mx = std::max(mx, n);
+  for (int t = 0; t < mx; ++t)
+    for (size_t p = 0; p < ntiles.size(); ++p)
+      if (t < ntiles[p]) out.push_back(TileRef{(int)p, t});
+  return out;
+}
+
 template <class T>
 struct GemmPlan {
   bool ta = false, tb = false;
   int tag = 0;  // 1: the Schur-stage V^T X^-1 / V^T Y launch (named separately in profiles)
   std::vector<GemmDesc<T>> h;
-  std::vector<int> t2d;
+  std::vector<int> ntiles;  // per problem
+  std::vector<TileRef> t2d;
   GemmDesc<T>* d = nullptr;
-  int* dt = nullptr;
+  TileRef* dt = nullptr;
   // gemm_f64_lds (fp64) and gemm_valu (multi-word) output tiles
   static constexpr int TILE = std::is_same<T, double>::value ? 64 : 32;
 
@@ -87,10 +99,9 @@ struct GemmPlan {
     g.A = A; g.B = B; g.Cin = Cin; g.C = C;
     g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldcin = ldcin; g.ldc = ldc;
     g.tn = cdiv(N, TILE);
-    g.tile0 = (int)t2d.size();
+    g.tile0 = 0;
     g.pad = 0;
-    const int nt = cdiv(M, TILE) * g.tn;
-    for (int i = 0; i < nt; ++i) t2d.push_back((int)h.size());
+    ntiles.push_back((int)(cdiv(M, TILE) * g.tn));
     h.push_back(g);
   }
   bool gemv = false;
@@ -98,13 +109,9 @@ struct GemmPlan {
     if (h.empty()) return;
     gemv = true;
     for (const auto& g : h) gemv = gemv && g.N == 1;
-    if (gemv) {  // re-tile: one workgroup per 64 outputs
-      t2d.clear();
-      for (size_t q = 0; q < h.size(); ++q) {
-        h[q].tile0 = (int)t2d.size();
-        for (int i = 0; i < (int)cdiv(h[q].M, 64); ++i) t2d.push_back((int)q);
-      }
-    }
+    if (gemv)  // one workgroup per 64 outputs
+      for (size_t q = 0; q < h.size(); ++q) ntiles[q] = (int)cdiv(h[q].M, 64);
+    t2d = tile_major(ntiles);
     d = upload_vec(h);
     dt = upload_vec(t2d);
   }
@@ -336,7 +343,7 @@ struct Solver final : HandleBase {
   bool fast_schur = false;
   GemmPlan<T> p_txy;
   PairTileDesc* d_ptd = nullptr;
-  int* d_pt2d = nullptr;
+  TileRef* d_pt2d = nullptr;
   int n_ptiles = 0;
   SchurClusterDesc* d_gcd = nullptr;  // clusters summed by schur_gsum
   int n_gsum = 0, max_gD = 0;
@@ -744,7 +751,7 @@ struct Solver final : HandleBase {
           p_txy.add(Vt + b.voff, b.K, Y + b.off, b.n, nullptr, 0, TY + b.toff, b.K, b.K, b.del, b.del);
         }
       std::vector<PairTileDesc> ptd;
-      std::vector<int> pt2d;
+      std::vector<int> pnt;
       std::vector<SchurClusterDesc> gcd;
       int bi = 0;
       for (int c = 0; c < nc(); ++c) {
@@ -762,9 +769,9 @@ struct Solver final : HandleBase {
           t.G = direct ? S + c_Soff[c] : BX + b.boff;
           t.ldG = b.K;
           t.AY = AY + b.ayoff;
-          t.K = b.K; t.del = b.del; t.tile0 = (int)pt2d.size();
+          t.K = b.K; t.del = b.del; t.tile0 = 0;
           const int nt = cdiv(b.K, 64);
-          for (int u = 0; u < nt * (nt + 1) / 2; ++u) pt2d.push_back((int)ptd.size());
+          pnt.push_back(nt * (nt + 1) / 2);
           ptd.push_back(t);
         }
         if (!direct) {
@@ -776,6 +783,7 @@ struct Solver final : HandleBase {
         }
         bi += (int)Lc[j];
       }
+      const std::vector<TileRef> pt2d = tile_major(pnt);
       n_ptiles = (int)pt2d.size();
       if (n_ptiles) { d_ptd = upload_vec(ptd); d_pt2d = upload_vec(pt2d); }
       n_gsum = (int)gcd.size();

@@ -22,6 +22,13 @@ using mw::Num;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// workgroup -> (problem, tile).  The batched launches order their workgroups tile-major
+// (problem fastest), so with a problem count divisible by 8 every tile of one problem lands on
+// the same XCD (workgroups go round-robin over the 8 XCDs) and shares its L2.
+struct TileRef {
+  int p, t;
+};
+
 template <class T> struct GemmDesc {
   const T* A;
   const T* B;
@@ -29,7 +36,7 @@ template <class T> struct GemmDesc {
   T* C;
   int M, N, K, lda, ldb, ldcin, ldc;
   int tn;     // tiles along N
-  int tile0;  // first tile index of this problem in the launch
+  int tile0;  // (unused by the TileRef kernels)
   int pad;
 };
 
@@ -46,196 +53,6 @@ template <class T> struct TrsmDesc {
   int pad;
 };
 
-// ------------------------------------------------------------------------------------------
-// GEMM, fp64 matrix cores.  64x64 output tile per 256-thread workgroup (4 waves as 2x2, each
-// wave 32x32 = 2x2 MFMA tiles of 16x16), K-step 16 staged through LDS.
-// v_mfma_f64_16x16x4_f64 lane maps (checked by tools/micro/f64_mfma_probe.hip):
-//   A: lane l holds A[i = l&15][k = l>>4];  B: B[k = l>>4][j = l&15];
-//   C/D: 4 results per lane, reg r at (row = (l>>4) + 4r, col = l&15).
-// LDS rows are padded to 80 doubles so the two 16-lane halves of a ds_read_b64 group land on
-// disjoint banks.
-// ------------------------------------------------------------------------------------------
-template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_f64_mfma(const GemmDesc<double>* __restrict__ descs,
-                                                     const int* __restrict__ t2d, double alpha,
-                                                     double beta) {
-  constexpr int BM = 64, BN = 64, BK = 16, LS = 80;
-  __shared__ double As[BK * LS];
-  __shared__ double Bs[BK * LS];
-  const GemmDesc<double> d = descs[t2d[blockIdx.x]];
-  const int t = blockIdx.x - d.tile0;
-  const int m0 = (t / d.tn) * BM, n0 = (t % d.tn) * BN;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const double* __restrict__ A = d.A;
-  const double* __restrict__ B = d.B;
-  d4 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-
-  for (int k0 = 0; k0 < d.K; k0 += BK) {
-    // ---- stage A tile (rows m0..m0+63, k0..k0+15) as As[k][i]
-    if (!TA) {
-      const int k = tid >> 4, i = (tid & 15) * 4, gk = k0 + k;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gi = m0 + i + q;
-        As[k * LS + i + q] = (gi < d.M && gk < d.K) ? A[gi + (size_t)gk * d.lda] : 0.0;
-      }
-    } else {
-      const int i = tid >> 2, k = (tid & 3) * 4, gi = m0 + i;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gk = k0 + k + q;
-        As[(k + q) * LS + i] = (gi < d.M && gk < d.K) ? A[gk + (size_t)gi * d.lda] : 0.0;
-      }
-    }
-    // ---- stage B tile (k0..k0+15, cols n0..n0+63) as Bs[k][j]
-    if (!TB) {
-      const int j = tid >> 2, k = (tid & 3) * 4, gj = n0 + j;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gk = k0 + k + q;
-        Bs[(k + q) * LS + j] = (gj < d.N && gk < d.K) ? B[gk + (size_t)gj * d.ldb] : 0.0;
-      }
-    } else {
-      const int k = tid >> 4, j = (tid & 15) * 4, gk = k0 + k;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gj = n0 + j + q;
-        Bs[k * LS + j + q] = (gj < d.N && gk < d.K) ? B[gj + (size_t)gk * d.ldb] : 0.0;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      const int kr = (kk + (lane >> 4)) * LS;
-      const double a0 = As[kr + wm * 32 + (lane & 15)];
-      const double a1 = As[kr + wm * 32 + 16 + (lane & 15)];
-      const double b0 = Bs[kr + wn * 32 + (lane & 15)];
-      const double b1 = Bs[kr + wn * 32 + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 32 + mi * 16 + (lane >> 4) + 4 * r;
-        const int col = n0 + wn * 32 + ni * 16 + (lane & 15);
-        if (row < d.M && col < d.N) {
-          double v = alpha * acc[mi][ni][r];
-          if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];
-          d.C[row + (size_t)col * d.ldc] = v;
-        }
-      }
-}
-
-// ------------------------------------------------------------------------------------------
-// GEMM, fp64 matrix cores, LDS-free: one 64-thread workgroup (one wave) per 32x32 output tile
-// (2x2 accumulators of v_mfma_f64_16x16x4).  Every lane loads its MFMA operand fragments
-// straight from L2 (A-op: A[i0+(l&15)][k+(l>>4)], B-op: B[k+(l>>4)][j0+(l&15)]): no LDS, no
-// barrier, and the K loop is unrolled 8 k-steps deep so 32 fragment loads are in flight per lane.
-// Small batched products (128x128 blocks) get 16 independent waves per block -- 4 per CU at the
-// solver's sizes -- instead of one latency-bound workgroup.
-// ------------------------------------------------------------------------------------------
-template <bool TA, bool TB>
-__global__ __launch_bounds__(64) void gemm_f64_direct(const GemmDesc<double>* __restrict__ descs,
-                                                      const int* __restrict__ t2d, double alpha,
-                                                      double beta) {
-  const GemmDesc<double> d = descs[t2d[blockIdx.x]];
-  const int t = blockIdx.x - d.tile0;
-  const int m0 = (t / d.tn) * 32, n0 = (t % d.tn) * 32;
-  const int lane = threadIdx.x, lr = lane & 15, lk = lane >> 4;
-  const int M = d.M, N = d.N, K = d.K;
-  // rows / columns past the edge are clamped to a valid one: they only feed outputs that are
-  // never stored.  Only the K tail needs zero-filled operands.
-  const int ia0 = min(m0 + lr, M - 1), ia1 = min(m0 + 16 + lr, M - 1);
-  const int jb0 = min(n0 + lr, N - 1), jb1 = min(n0 + 16 + lr, N - 1);
-  // per-lane fragment pointers at k = lk, and the step per k-step of 4
-  const double* a0p = TA ? d.A + (size_t)ia0 * d.lda + lk : d.A + ia0 + (size_t)lk * d.lda;
-  const double* a1p = TA ? d.A + (size_t)ia1 * d.lda + lk : d.A + ia1 + (size_t)lk * d.lda;
-  const double* b0p = TB ? d.B + jb0 + (size_t)lk * d.ldb : d.B + (size_t)jb0 * d.ldb + lk;
-  const double* b1p = TB ? d.B + jb1 + (size_t)lk * d.ldb : d.B + (size_t)jb1 * d.ldb + lk;
-  const size_t sa = TA ? 4 : 4 * (size_t)d.lda, sb = TB ? 4 * (size_t)d.ldb : 4;
-  d4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c10 = c00, c11 = c00;
-  constexpr int U = 4, KS = 4 * U;
-  double pa0[U], pa1[U], pb0[U], pb1[U], qa0[U], qa1[U], qb0[U], qb1[U];
-  auto load = [&](double* x0, double* x1, double* y0, double* y1, int kb) {
-    if (kb + KS <= K) {  // interior stage: plain loads
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const size_t ka = (size_t)(kb / 4 + u) * sa, kbb = (size_t)(kb / 4 + u) * sb;
-        x0[u] = a0p[ka];
-        x1[u] = a1p[ka];
-        y0[u] = b0p[kbb];
-        y1[u] = b1p[kbb];
-      }
-    } else {  // K tail
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool ok = kb + 4 * u + lk < K;
-        const size_t ka = (size_t)(kb / 4 + u) * sa, kbb = (size_t)(kb / 4 + u) * sb;
-        x0[u] = ok ? a0p[ka] : 0.0;
-        x1[u] = ok ? a1p[ka] : 0.0;
-        y0[u] = ok ? b0p[kbb] : 0.0;
-        y1[u] = ok ? b1p[kbb] : 0.0;
-      }
-    }
-  };
-  auto mma = [&](const double* x0, const double* x1, const double* y0, const double* y1) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], y0[u], c00, 0, 0, 0);
-      c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], y1[u], c01, 0, 0, 0);
-      c10 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], y0[u], c10, 0, 0, 0);
-      c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], y1[u], c11, 0, 0, 0);
-    }
-  };
-  load(pa0, pa1, pb0, pb1, 0);
-  for (int k0 = 0; k0 < K; k0 += 2 * KS) {
-    if (k0 + KS < K) load(qa0, qa1, qb0, qb1, k0 + KS);
-    mma(pa0, pa1, pb0, pb1);
-    if (k0 + KS >= K) break;
-    if (k0 + 2 * KS < K) load(pa0, pa1, pb0, pb1, k0 + 2 * KS);
-    mma(qa0, qa1, qb0, qb1);
-  }
-  auto store = [&](const d4& c, int ib, int jb) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = ib + lk + 4 * r, col = jb + lr;
-      if (row < M && col < N) {
-        double v = alpha * c[r];
-        if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];
-        d.C[row + (size_t)col * d.ldc] = v;
-      }
-    }
-  };
-  store(c00, m0, n0);
-  store(c01, m0, n0 + 16);
-  store(c10, m0 + 16, n0);
-  store(c11, m0 + 16, n0 + 16);
-}
-
-// ------------------------------------------------------------------------------------------
-// GEMM, fp64 matrix cores, LDS-tiled and software-pipelined: 64x64 tile per 256-thread
-// workgroup (4 waves as 2x2, 2x2 MFMA tiles each), K-step BK (16: 3-4 workgroups per CU).  The next K-slab is loaded into
-// registers (coalesced: each load instruction reads whole 256-512 B column runs) while the
-// current one is multiplied out of LDS, then written behind one barrier.
-// An operand that is contiguous along its 64-wide dimension (A, or B^T) is kept k-major,
-// Os[k*80 + i]; one contiguous along k (A^T, or B) is kept as Os[i*34 + k].  Both pitches make
-// the ds_read_b64 MFMA fragment reads (lanes (k = l>>4, i = l&15)) and the ds_write_b64 stores
-// bank-conflict free (MI355X_MICROARCH.md §LDS: b64 reads bank by (a/4) mod 64 in 32-lane
-// groups, b64 writes by (a/4) mod 32 in 16-lane groups).
-// ------------------------------------------------------------------------------------------
 // Load through an explicitly global pointer.  A pointer read from a descriptor is generic, and
 // hipcc then emits flat_load, which also counts on lgkmcnt: the first LDS wait of the MFMA loop
 // then drains every prefetch load in flight (no overlap of the next slab with the MFMAs).
@@ -298,7 +115,7 @@ __device__ inline int acc_col(int wn, int ni, int lr) { return wn * 32 + ni * 16
 // TAG only names the instantiation (a profile can tell the Schur-stage launch from the others)
 template <bool TA, bool TB, int TAG = 0, int BK = 16>
 __global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
-                                                    const int* __restrict__ t2d, double alpha,
+                                                    const TileRef* __restrict__ t2d, double alpha,
                                                     double beta) {
   using namespace lds_gemm;
   using SL = Slab<BK>;
@@ -306,8 +123,9 @@ __global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __re
   __shared__ double smem[2 * SL::SZ > 64 * TP ? 2 * SL::SZ : 64 * TP];
   double* As = smem;
   double* Bs = smem + SL::SZ;
-  const GemmDesc<double> d = descs[t2d[blockIdx.x]];
-  const int t = blockIdx.x - d.tile0;
+  const TileRef tr = t2d[blockIdx.x];
+  const GemmDesc<double> d = descs[tr.p];
+  const int t = tr.t;
   const int m0 = (t / d.tn) * 64, n0 = (t % d.tn) * 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1, lr = lane & 15, lk = lane >> 4;
@@ -376,13 +194,14 @@ __global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __re
 // ------------------------------------------------------------------------------------------
 template <class T, bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__ descs,
-                                                 const int* __restrict__ t2d, double alpha,
+                                                 const TileRef* __restrict__ t2d, double alpha,
                                                  double beta) {
   constexpr int BM = 32, BN = 32, BK = 8;
   __shared__ T As[BK][BM + 1];
   __shared__ T Bs[BK][BN + 1];
-  const GemmDesc<T> d = descs[t2d[blockIdx.x]];
-  const int t = blockIdx.x - d.tile0;
+  const TileRef tr = t2d[blockIdx.x];
+  const GemmDesc<T> d = descs[tr.p];
+  const int t = tr.t;
   const int m0 = (t / d.tn) * BM, n0 = (t % d.tn) * BN;
   const int tid = threadIdx.x;
   const int ti = (tid & 15) * 2, tj = (tid >> 4) * 2;
@@ -506,10 +325,11 @@ __device__ __forceinline__ T row16_sum_t(T v) {
 //       groups x 2 k-steps of loads in flight; each column sum is a 16-lane DPP reduction.
 template <class T, bool TA>
 __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restrict__ descs,
-                                                    const int* __restrict__ t2d, double alpha,
+                                                    const TileRef* __restrict__ t2d, double alpha,
                                                     double beta) {
-  const GemmDesc<T> d = descs[t2d[blockIdx.x]];
-  const int o0 = (blockIdx.x - d.tile0) * 64;
+  const TileRef tr = t2d[blockIdx.x];
+  const GemmDesc<T> d = descs[tr.p];
+  const int o0 = tr.t * 64;
   const int tid = threadIdx.x;
   const T* __restrict__ A = d.A;
   const T* __restrict__ x = d.B;
@@ -1030,7 +850,7 @@ struct PairTileDesc {
 
 template <int BK = 16>
 __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __restrict__ descs,
-                                                       const int* __restrict__ t2d) {
+                                                       const TileRef* __restrict__ t2d) {
   using namespace lds_gemm;
   using SLB = Slab<BK>;
   constexpr int PER = SLB::PER, SL = BK * LSM;
@@ -1038,8 +858,9 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
   double* As = smem;
   double* Xs = smem + SL;
   double* Ys = smem + 2 * SL;
-  const PairTileDesc d = descs[t2d[blockIdx.x]];
-  const int u = blockIdx.x - d.tile0;
+  const TileRef tr = t2d[blockIdx.x];
+  const PairTileDesc d = descs[tr.p];
+  const int u = tr.t;
   int J = 0;
   while ((J + 1) * (J + 2) / 2 <= u) ++J;
   const int I = u - J * (J + 1) / 2;

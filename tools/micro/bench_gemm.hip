@@ -1,5 +1,5 @@
-// Batched fp64 GEMM timing for the solver's shapes: descriptor kernels (LDS-tiled 64x64 and
-// LDS-free 32x32 direct) on 64 x (M x N x K), alpha=1, beta=0.
+// Batched fp64 GEMM timing for the solver's shapes: gemm_f64_lds (NN/TN/NT, BK 32 and 16) on
+// nb x (M x N x K), alpha=1, beta=0; workgroups tile-major as in the library.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -38,27 +38,26 @@ int main(int argc, char** argv) {
     float us = timeit([&] { empty_kernel<<<1024, 256>>>(nullptr, nullptr); });
     printf("empty kernel 1024x256: %.2f us\n", us);
   }
-  for (int variant : {0, 1, 2, 3, 4, 5, 6, 7}) {
-    const int TILE = variant == 1 ? 32 : 64;
+  for (int variant : {2, 3, 4, 5, 6, 7}) {
+    const int TILE = 64;
     std::vector<GemmDesc<double>> d;
-    std::vector<int> t2d;
+    std::vector<TileRef> t2d;
     for (int b = 0; b < nb; ++b) {
       // lda/ldb as each variant reads them: TA -> A is K x M (ld K), TB -> B is N x K (ld N)
       const bool ta = variant == 3 || variant == 6, tb = variant == 4 || variant == 7;
-      GemmDesc<double> g{A + sa * b, B + sb * b, nullptr, C + sc * b, M, N, K, ta ? K : M, tb ? N : K, M, M, (N + TILE - 1) / TILE, (int)t2d.size(), 0};
-      int nt = ((M + TILE - 1) / TILE) * g.tn;
-      for (int i = 0; i < nt; ++i) t2d.push_back(b);
+      GemmDesc<double> g{A + sa * b, B + sb * b, nullptr, C + sc * b, M, N, K, ta ? K : M, tb ? N : K, M, M, (N + TILE - 1) / TILE, 0, 0};
       d.push_back(g);
     }
-    GemmDesc<double>* dd; int* dt;
-    CK(hipMalloc(&dd, d.size() * sizeof(d[0]))); CK(hipMalloc(&dt, t2d.size() * 4));
+    const int nt = ((M + TILE - 1) / TILE) * d[0].tn;
+    for (int t = 0; t < nt; ++t)
+      for (int b = 0; b < nb; ++b) t2d.push_back(TileRef{b, t});
+    GemmDesc<double>* dd; TileRef* dt;
+    CK(hipMalloc(&dd, d.size() * sizeof(d[0]))); CK(hipMalloc(&dt, t2d.size() * sizeof(TileRef)));
     CK(hipMemcpy(dd, d.data(), d.size() * sizeof(d[0]), hipMemcpyHostToDevice));
-    CK(hipMemcpy(dt, t2d.data(), t2d.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dt, t2d.data(), t2d.size() * sizeof(TileRef), hipMemcpyHostToDevice));
     unsigned grid = t2d.size();
     float us;
-    if (variant == 0) us = timeit([&] { gemm_f64_mfma<false, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
-    else if (variant == 1) us = timeit([&] { gemm_f64_direct<false, false><<<grid, 64>>>(dd, dt, 1.0, 0.0); });
-    else if (variant == 2) us = timeit([&] { gemm_f64_lds<false, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    if (variant == 2) us = timeit([&] { gemm_f64_lds<false, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
     else if (variant == 3) us = timeit([&] { gemm_f64_lds<true, false><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
     else if (variant == 4) us = timeit([&] { gemm_f64_lds<false, true><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
     else if (variant == 5) us = timeit([&] { gemm_f64_lds<false, false, 0, 16><<<grid, 256>>>(dd, dt, 1.0, 0.0); });

@@ -34,22 +34,24 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(Y, h.data(), sx * nb * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(lam, h.data(), (size_t)K * nb * 8, hipMemcpyHostToDevice));
   // TXt/TYt GEMM
-  std::vector<GemmDesc<double>> gd; std::vector<int> gt;
+  std::vector<GemmDesc<double>> gd; std::vector<TileRef> gt;
   for (int b = 0; b < nb; ++b)
     for (int w = 0; w < 2; ++w) {
-      GemmDesc<double> g{Vt + sv * b, (w ? Y : X) + sx * b, nullptr, (w ? TY : TX) + sv * b, K, del, del, K, del, 0, K, (del + 63) / 64, (int)gt.size(), 0};
-      for (int i = 0; i < ((K + 63) / 64) * g.tn; ++i) gt.push_back((int)gd.size());
+      GemmDesc<double> g{Vt + sv * b, (w ? Y : X) + sx * b, nullptr, (w ? TY : TX) + sv * b, K, del, del, K, del, 0, K, (del + 63) / 64, 0, 0};
       gd.push_back(g);
     }
-  GemmDesc<double>* dgd = up(gd); int* dgt = up(gt);
-  std::vector<PairTileDesc> pd; std::vector<int> pt;
+  for (int t = 0; t < ((K + 63) / 64) * gd[0].tn; ++t)
+    for (int p = 0; p < (int)gd.size(); ++p) gt.push_back(TileRef{p, t});
+  GemmDesc<double>* dgd = up(gd); TileRef* dgt = up(gt);
+  std::vector<PairTileDesc> pd; std::vector<TileRef> pt;
   const int nt = (K + 63) / 64;
   for (int b = 0; b < nb; ++b) {
-    PairTileDesc t{Vt + sv * b, TX + sv * b, TY + sv * b, lam + (size_t)K * b, G + (size_t)K * K * b, AY + (size_t)K * b, K, del, K, (int)pt.size()};
-    for (int u = 0; u < nt * (nt + 1) / 2; ++u) pt.push_back((int)pd.size());
+    PairTileDesc t{Vt + sv * b, TX + sv * b, TY + sv * b, lam + (size_t)K * b, G + (size_t)K * K * b, AY + (size_t)K * b, K, del, K, 0};
     pd.push_back(t);
   }
-  PairTileDesc* dpd = up(pd); int* dpt = up(pt);
+  for (int u = 0; u < nt * (nt + 1) / 2; ++u)
+    for (int b = 0; b < nb; ++b) pt.push_back(TileRef{b, u});
+  PairTileDesc* dpd = up(pd); TileRef* dpt = up(pt);
   const double fl_txy = 2.0 * 2 * K * del * del * nb, fl_pairs = 2.0 * 2 * del * 64.0 * 64 * pt.size();
   const double alg = 4.0 * del * K * (del + K) * nb + 8.0 * K * (K + 1) / 2.0 * nb;
   printf("blocks %d delta %d K %d\n", nb, del, K);
