@@ -51,6 +51,21 @@ def schur_flops_bytes(bi, word=8):
     return fl, by
 
 
+def schur_pmc_traffic(config, precision, world):
+    """HBM bytes per iteration of the Schur stage (FETCH_SIZE + WRITE_SIZE of its two launches)
+    from the newest committed PMC summary, profiles/rNN_schur_pmc.json, written by
+    tools/profile_round.sh for the default C3 fp64 1-GPU run.  None for other runs."""
+    import glob
+    if config != "c3" or precision != 1 or world != 1:
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_schur_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_iteration"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cons, b, bi, budget_s=20.0):
     """Time the oracle (numpy fp64 restatement of MPMP.jl) on this instance: one loop body."""
     from oracle import mpmp_oracle as O
@@ -154,6 +169,7 @@ def main():
         fl /= world   # per-rank share of the Schur work (the roofline is per GPU)
         by /= world
     sch_s = schur_ms / 1e3 / n_inst
+    traffic, traffic_src = schur_pmc_traffic(args.config, args.precision, world)
     achieved = fl / sch_s / 1e12
     res = {
         "metric": "interior-point iterations/sec (solverank1sdp loop body, MPMP.jl:755-887)",
@@ -173,7 +189,9 @@ def main():
                    "parallelism": f"clusters sharded over {world} GPU(s)" if world > 1 else "1 GPU"},
         "roofline": {"bound": "mfma", "kernel": "Schur assembly (stage SCHUR)",
                      "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "alg_bytes_per_iteration": by,
                      "schur_ms_per_iteration": sch_s * 1e3,
                      "schur_alg_gbs": by / sch_s / 1e9},
         "phase_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.STAGE_NAMES, phase)},

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Profile the C3 bench on the GPU box (run through gpurun from the repo root):
+#   1. rocprofv3 --kernel-trace --stats      -> per-kernel durations (rocprof agrees with bench.py's events)
+#   2. rocprofv3 --pmc FETCH_SIZE            -> HBM read bytes per dispatch   (own pass)
+#   3. rocprofv3 --pmc WRITE_SIZE            -> HBM write bytes per dispatch  (own pass)
+# Outputs go to gpurun_out/prof_$TAG; copy the summaries into profiles/ afterwards.
+set -euo pipefail
+TAG=${1:-r01}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
+  python3 bench.py --steps 20 --warmup 3 --no-cpu > $OUT/bench_kt.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
+  python3 bench.py --steps 5 --warmup 1 --no-cpu > $OUT/bench_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
+  python3 bench.py --steps 5 --warmup 1 --no-cpu > $OUT/bench_write.log 2>&1
+python3 tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv \
+  $OUT/write/run_counter_collection.csv $OUT/schur_pmc.json > /dev/null
+python3 tools/prof_summary.py $OUT/kt/run_kernel_stats.csv 33 > $OUT/kernel_summary.txt
+echo done
