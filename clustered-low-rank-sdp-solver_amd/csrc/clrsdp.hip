@@ -126,11 +126,11 @@ struct GemmPlan {
       return;
     }
     if constexpr (std::is_same<T, double>::value) {
-      if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
-      else if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
-      else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
-      else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
-      else gemm_f64_lds<true, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
+      else if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
+      else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
+      else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
+      else gemm_f64_lds<true, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
     } else {
       if (!ta && !tb) gemm_valu<T, false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else if (ta && !tb) gemm_valu<T, true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);

@@ -65,13 +65,13 @@ namespace lds_gemm {
 // else at P[i + k*ld], kept as S[k*80 + i].  Rows i beyond `rows` are clamped (their products
 // are never stored); k beyond K is zeroed.
 constexpr int LSM = 80;
-template <int BK> struct Slab {
-  static constexpr int PER = BK / 4, LSK = BK + 2;
+template <int BK, int NTH = 256> struct Slab {
+  static constexpr int PER = 64 * BK / NTH, LSK = BK + 2;
   static constexpr int SZ = 64 * LSK > BK * LSM ? 64 * LSK : BK * LSM;  // doubles per image
   template <bool kcontig>
   __device__ static inline void kk(int tid, int q, int& i, int& k) {
-    if (!kcontig) { i = tid & 63; k = (tid >> 6) + 4 * q; }
-    else { k = tid & (BK - 1); i = tid / BK + (256 / BK) * q; }
+    if (!kcontig) { i = tid & 63; k = (tid >> 6) + (NTH / 64) * q; }
+    else { k = tid & (BK - 1); i = tid / BK + (NTH / BK) * q; }
   }
   // Unconditional loads from clamped addresses; the k >= K tail is zeroed in store(), after
   // the MFMAs (a select right after the load would make the compiler wait for it there, and a
@@ -109,16 +109,19 @@ template <int BK> struct Slab {
 // accumulator layout puts 16 consecutive lanes on 16 different columns.
 constexpr int TP = 65;
 __device__ inline int acc_row(int wm, int mi, int lk, int r) { return wm * 32 + mi * 16 + lk + 4 * r; }
-__device__ inline int acc_col(int wn, int ni, int lr) { return wn * 32 + ni * 16 + lr; }
+__device__ inline int acc_col(int wn, int ni, int lr, int wcols = 32) { return wn * wcols + ni * 16 + lr; }
 }  // namespace lds_gemm
 
-// TAG only names the instantiation (a profile can tell the Schur-stage launch from the others)
-template <bool TA, bool TB, int TAG = 0, int BK = 16>
-__global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
-                                                    const TileRef* __restrict__ t2d, double alpha,
-                                                    double beta) {
+// TAG only names the instantiation (a profile can tell the Schur-stage launch from the others).
+// NW = 4 (2x2 waves, 32x32 each) or 8 (2x4 waves, 32x16 each: twice the waves per tile, for
+// batches of small products that leave the CUs latency-bound).
+template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
+                                                        const TileRef* __restrict__ t2d,
+                                                        double alpha, double beta) {
   using namespace lds_gemm;
-  using SL = Slab<BK>;
+  constexpr int NTH = 64 * NW, WN = NW / 2, NI = 4 / WN, WC = 64 / WN;
+  using SL = Slab<BK, NTH>;
   constexpr int PER = SL::PER;
   __shared__ double smem[2 * SL::SZ > 64 * TP ? 2 * SL::SZ : 64 * TP];
   double* As = smem;
@@ -128,16 +131,16 @@ __global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __re
   const int t = tr.t;
   const int m0 = (t / d.tn) * 64, n0 = (t % d.tn) * 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1, lr = lane & 15, lk = lane >> 4;
+  const int wm = w / WN, wn = w % WN, lr = lane & 15, lk = lane >> 4;
   const int M = d.M, N = d.N, K = d.K;
   // A is (i, k) with i along M: contiguous along k iff TA.  B is (j, k): contiguous along k iff !TB.
   constexpr bool AK = TA, BKc = !TB;
   double ra[PER], rb[PER];
-  d4 acc[2][2];
+  d4 acc[2][NI];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int b = 0; b < NI; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
   SL::template load<AK>(ra, d.A, d.lda, m0, M, 0, K, tid);
   SL::template load<BKc>(rb, d.B, d.ldb, n0, N, 0, K, tid);
   SL::template store<AK>(ra, As, tid, 0, K);
@@ -151,14 +154,16 @@ __global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __re
     }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      const double a0 = SL::template frag<AK>(As, wm * 32 + lr, kk + lk);
-      const double a1 = SL::template frag<AK>(As, wm * 32 + 16 + lr, kk + lk);
-      const double b0 = SL::template frag<BKc>(Bs, wn * 32 + lr, kk + lk);
-      const double b1 = SL::template frag<BKc>(Bs, wn * 32 + 16 + lr, kk + lk);
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      double af[2], bf[NI];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) af[mi] = SL::template frag<AK>(As, wm * 32 + mi * 16 + lr, kk + lk);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bf[ni] = SL::template frag<BKc>(Bs, wn * WC + ni * 16 + lr, kk + lk);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
     }
     if (!more) break;
     __syncthreads();
@@ -170,16 +175,17 @@ __global__ __launch_bounds__(256) void gemm_f64_lds(const GemmDesc<double>* __re
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        smem[acc_row(wm, mi, lk, r) * TP + acc_col(wn, ni, lr)] = acc[mi][ni][r];
+        smem[acc_row(wm, mi, lk, r) * TP + acc_col(wn, ni, lr, WC)] = acc[mi][ni][r];
   __syncthreads();
   const int row = m0 + lane;
   if (row < M) {
+    constexpr int CPW = 64 / NW;  // output columns stored per wave
 #pragma unroll 4
-    for (int c = 0; c < 16; ++c) {
-      const int cl = w * 16 + c, col = n0 + cl;
+    for (int c = 0; c < CPW; ++c) {
+      const int cl = w * CPW + c, col = n0 + cl;
       if (col < N) {
         double v = alpha * smem[lane * TP + cl];
         if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];

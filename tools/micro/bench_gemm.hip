@@ -38,13 +38,13 @@ int main(int argc, char** argv) {
     float us = timeit([&] { empty_kernel<<<1024, 256>>>(nullptr, nullptr); });
     printf("empty kernel 1024x256: %.2f us\n", us);
   }
-  for (int variant : {2, 3, 4, 5, 6, 7}) {
+  for (int variant : {5, 7, 8, 10, 11, 12, 13, 14}) {
     const int TILE = 64;
     std::vector<GemmDesc<double>> d;
     std::vector<TileRef> t2d;
     for (int b = 0; b < nb; ++b) {
       // lda/ldb as each variant reads them: TA -> A is K x M (ld K), TB -> B is N x K (ld N)
-      const bool ta = variant == 3 || variant == 6, tb = variant == 4 || variant == 7;
+      const bool ta = variant == 3 || variant == 6 || variant == 9, tb = variant == 4 || variant == 7 || variant == 10 || variant == 12 || variant == 14;
       GemmDesc<double> g{A + sa * b, B + sb * b, nullptr, C + sc * b, M, N, K, ta ? K : M, tb ? N : K, M, M, (N + TILE - 1) / TILE, 0, 0};
       d.push_back(g);
     }
@@ -62,8 +62,15 @@ int main(int argc, char** argv) {
     else if (variant == 4) us = timeit([&] { gemm_f64_lds<false, true><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
     else if (variant == 5) us = timeit([&] { gemm_f64_lds<false, false, 0, 16><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
     else if (variant == 6) us = timeit([&] { gemm_f64_lds<true, false, 0, 16><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
-    else us = timeit([&] { gemm_f64_lds<false, true, 0, 16><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
-    const char* nm[] = {"mfma64 (LDS) ", "direct32     ", "lds NN       ", "lds TN       ", "lds NT       ", "lds16 NN     ", "lds16 TN     ", "lds16 NT     "};
+    else if (variant == 7) us = timeit([&] { gemm_f64_lds<false, true, 0, 16><<<grid, 256>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 8) us = timeit([&] { gemm_f64_lds<false, false, 0, 16, 8><<<grid, 512>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 9) us = timeit([&] { gemm_f64_lds<true, false, 0, 16, 8><<<grid, 512>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 10) us = timeit([&] { gemm_f64_lds<false, true, 0, 16, 8><<<grid, 512>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 11) us = timeit([&] { gemm_f64_lds<false, false, 0, 32, 8><<<grid, 512>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 12) us = timeit([&] { gemm_f64_lds<false, true, 0, 32, 8><<<grid, 512>>>(dd, dt, 1.0, 0.0); });
+    else if (variant == 13) us = timeit([&] { gemm_f64_lds<false, false, 0, 64, 8><<<grid, 512>>>(dd, dt, 1.0, 0.0); });
+    else us = timeit([&] { gemm_f64_lds<false, true, 0, 64, 8><<<grid, 512>>>(dd, dt, 1.0, 0.0); });
+    const char* nm[] = {"", "", "lds NN       ", "lds TN       ", "lds NT       ", "lds16 NN     ", "lds16 TN     ", "lds16 NT     ", "lds16w8 NN   ", "lds16w8 TN   ", "lds16w8 NT   ", "lds32w8 NN   ", "lds32w8 NT   ", "lds64w8 NN   ", "lds64w8 NT   "};
     printf("%s  batch %d x (%d x %d x %d): %.1f us  %.1f TFLOP/s  (grid %u)\n", nm[variant], nb, M, N, K, us, flops / us / 1e6, grid);
   }
   return 0;
