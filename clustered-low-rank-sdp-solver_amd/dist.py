@@ -13,16 +13,23 @@ import os
 
 
 class TorchExchange:
-    def __init__(self, local_rank: int, backend: str = "nccl", device: str = "cuda"):
+    def __init__(self, local_rank: int, backend: str = None, device: str = "cuda"):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
+        backend = backend or os.environ.get("CLRSDP_EXCHANGE_BACKEND", "nccl")
         self.backend = backend
         if device == "cuda":
             torch.cuda.set_device(local_rank)
         if not dist.is_initialized():
             if backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+                try:
+                    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+                except Exception as e:  # keep the run alive: host-staged gloo exchange instead
+                    print(f"[clrsdp] RCCL process group failed ({e!r}); falling back to gloo",
+                          flush=True)
+                    self.backend = "gloo"
+                    dist.init_process_group("gloo")
             else:
                 dist.init_process_group(backend)
         self.world = dist.get_world_size()
