@@ -657,6 +657,72 @@ __device__ __forceinline__ void tile_of(int t, int& i, int& j) {
   j = t - i * (i + 1) / 2;
 }
 
+// One wave: Cholesky factor and inverse of the 16x16 diagonal tile at (k0, k0) of the LDS image.
+// Lanes 0-15 hold row i of A_kk (-> L_kk), lanes 16-31 row i of X_kk (-> L_kk^-1), 16 values each
+// in registers; the column loop is unrolled so every index is static and the cross-lane traffic
+// is v_readlane (uniform source lane) plus one permlane16 swap.  Writes L_kk back into the image
+// and L_kk^-1 column-major into Dinv; a non-positive pivot sets *flag = k0 + 1.
+template <int NP>
+__device__ inline void chol_diag16(double* __restrict__ A, int k0, double* __restrict__ Dinv,
+                                   int* flag, int lane) {
+  using LI = CholLds<NP>;
+  const int i = lane & 15, grp = lane >> 4;
+  double v[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double av = A[LI::idx(k0 + i, k0 + min(c, i))];
+    v[c] = grp == 0 ? (c <= i ? av : 0.0) : (c == i ? 1.0 : 0.0);
+  }
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double djj = readlane_d(v[j], j);
+    bad |= !(djj > 0.0);
+    double r = __builtin_amdgcn_rsq(djj);
+    r = r * (1.5 - 0.5 * djj * r * r);  // Newton step: r = 1/sqrt(d) to ~1 ulp
+    // l_ij (meaningful in lanes 0-15 with i >= j); lanes 16-31 get their row's l_ij by a swap
+    const double lij = (i == j) ? djj * r : v[j] * r;
+    const double lsw = swap16_d(lij);
+    double xj[16];  // row j of X before its scaling (columns <= j), uniform
+#pragma unroll
+    for (int c = 0; c <= j; ++c) xj[c] = readlane_d(v[c], 16 + j);
+    double lk[16];  // column j of L below the diagonal, uniform
+#pragma unroll
+    for (int t = j + 1; t < 16; ++t) lk[t] = readlane_d(lij, t);
+    // branch-free: lanes 0-15: v_j = l_ij, v_t -= l_ij l_tj (j < t <= i);
+    //              lanes 16-31: row j scaled by r, v_c -= (l_ij r) x_jc (c <= j, i > j)
+    const bool g0 = grp == 0, below = i > j;
+    const double m = lsw * r;
+    v[j] = (g0 && i >= j) ? lij : v[j];
+#pragma unroll
+    for (int t = j + 1; t < 16; ++t) {
+      const double u = v[t] - lij * lk[t];
+      v[t] = (g0 && below && t <= i) ? u : v[t];
+    }
+#pragma unroll
+    for (int c = 0; c <= j; ++c) {
+      const double ux = (i == j) ? v[c] * r : v[c] - m * xj[c];
+      v[c] = (!g0 && i >= j) ? ux : v[c];
+    }
+  }
+  if (grp == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (c <= i) A[LI::idx(k0 + i, k0 + c)] = v[c];
+  } else if (grp == 1) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) Dinv[c * 16 + i] = v[c];  // column-major L_kk^-1
+  }
+  if (lane == 0 && bad) *flag = k0 + 1;
+}
+
+// A = L L^T and L^-1 of one SPD block (n <= NP) per 512-thread workgroup, on chip.
+// Wave 0 factors the 16x16 diagonal tiles; waves 1-7 own the 16x16 tiles of the lower triangle
+// (round robin) and keep the tiles of X = L^-1 in MFMA accumulators.  Per 16-column panel k:
+//   (b) waves 1-7: L_ik = A_ik L_kk^-T (panel) and X_kj <- L_kk^-1 X_kj (row block, also to LDS)
+//   (c) waves 1-7: trailing A_ij -= L_ik L_jk^T and X_ij -= L_ik X_kj, except the next diagonal
+//       tile, which wave 0 updates and factors at the same time (look-ahead), so the sequential
+//       16-column diagonal factorisation overlaps the trailing update.
 template <int NP>
 __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __restrict__ in,
                                                      const MatDesc<double>* __restrict__ out_inv,
@@ -668,12 +734,12 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
 #else
 #define CH_STAMP(slot)
 #endif
-  constexpr int NT = NP / 16, NTILES = NT * (NT + 1) / 2, NW = 8, SLOTS = (NTILES + NW - 1) / NW;
+  constexpr int NT = NP / 16, NTILES = NT * (NT + 1) / 2, NWK = 7, SLOTS = (NTILES + NWK - 1) / NWK;
   constexpr int XLD = NP + 16;  // X row-block buffer: 16 x NP, padded rows
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   double* A = reinterpret_cast<double*>(smem_raw);  // NP * NP
-  double* Dinv = A + NP * NP;                         // 16 x 16, column-major
-  double* Xr = Dinv + 256;                            // 16 x XLD, row-major
+  double* Dinv0 = A + NP * NP;                        // 2 x (16 x 16), column-major, by k parity
+  double* Xr = Dinv0 + 512;                           // 16 x XLD, row-major
   int* flag = reinterpret_cast<int*>(Xr + 16 * XLD);
   using LI = CholLds<NP>;
   const MatDesc<double> d = in[blockIdx.x];
@@ -691,164 +757,129 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
       A[LI::idx(i, j)] = v;
     }
   if (tid == 0) *flag = 0;
-  // ---- X accumulators: identity on diagonal tiles
+  // ---- X accumulators of the worker waves: identity on diagonal tiles
+  const int wk = w - 1;  // worker index, -1 for wave 0
   d4 X[SLOTS];
 #pragma unroll
   for (int q = 0; q < SLOTS; ++q) {
-    const int t = w + NW * q;
+    const int t = wk + NWK * q;
     int ti = 0, tj = 0;
-    if (t < NTILES) tile_of(t, ti, tj);
+    if (wk >= 0 && t < NTILES) tile_of(t, ti, tj);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) X[q][r] = (t < NTILES && ti == tj && (lk + 4 * r) == lr) ? 1.0 : 0.0;
+    for (int r = 0; r < 4; ++r)
+      X[q][r] = (wk >= 0 && t < NTILES && ti == tj && (lk + 4 * r) == lr) ? 1.0 : 0.0;
   }
+  __syncthreads();
+  if (w == 0) chol_diag16<NP>(A, 0, Dinv0, flag, lane);
   __syncthreads();
   CH_STAMP(3)
   for (int k = 0; k < nt; ++k) {
     const int k0 = 16 * k;
-    // ---------------- (a) diagonal block: wave 0; lane (i = lane & 15, cg = lane >> 4) keeps row
-    // i, columns 4cg..4cg+3 of A_kk and of X_kk = L_kk^-1 in registers.  Per column one LDS round
-    // trip: the owners publish column j of A and row j of X (unscaled), every lane reads the
-    // pivot, its l_ij, the l_cj of its columns and X_j, and scales by r = 1/sqrt(a_jj)
-    // (v_rsq_f64 + one Newton step: no fp64 divide or sqrt on the critical path).
-    if (w == 0) {
-      // Lanes 0-15 hold row i of A_kk (-> L_kk), lanes 16-31 row i of X_kk (-> L_kk^-1), 16
-      // values each in registers; the column loop is unrolled so every index is static and
-      // the cross-lane traffic is v_readlane (uniform source lane) plus one permlane16 swap.
-      const int i = lane & 15, grp = lane >> 4;
-      double v[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double av = A[LI::idx(k0 + i, k0 + min(c, i))];
-        v[c] = grp == 0 ? (c <= i ? av : 0.0) : (c == i ? 1.0 : 0.0);
-      }
-      int bad = 0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const double djj = readlane_d(v[j], j);
-        bad |= !(djj > 0.0);
-        double r = __builtin_amdgcn_rsq(djj);
-        r = r * (1.5 - 0.5 * djj * r * r);  // Newton step: r = 1/sqrt(d) to ~1 ulp
-        // l_ij (meaningful in lanes 0-15 with i >= j); lanes 16-31 get their row's l_ij by a swap
-        const double lij = (i == j) ? djj * r : v[j] * r;
-        const double lsw = swap16_d(lij);
-        double xj[16];  // row j of X before its scaling (columns <= j), uniform
-#pragma unroll
-        for (int c = 0; c <= j; ++c) xj[c] = readlane_d(v[c], 16 + j);
-        double lk[16];  // column j of L below the diagonal, uniform
-#pragma unroll
-        for (int t = j + 1; t < 16; ++t) lk[t] = readlane_d(lij, t);
-        // branch-free (selects), so the scheduler can overlap consecutive columns:
-        //   lanes 0-15:  v_j = l_ij (i >= j);  v_t -= l_ij l_tj  (j < t <= i)
-        //   lanes 16-31: row j scaled by r;    v_c -= (l_ij r) x_jc (c <= j, i > j)
-        const bool g0 = grp == 0, below = i > j;
-        const double m = lsw * r;
-        if (j < 16) v[j] = (g0 && i >= j) ? lij : v[j];
-#pragma unroll
-        for (int t = j + 1; t < 16; ++t) {
-          const double u = v[t] - lij * lk[t];
-          v[t] = (g0 && below && t <= i) ? u : v[t];
-        }
-#pragma unroll
-        for (int c = 0; c <= j; ++c) {
-          const double ux = (i == j) ? v[c] * r : v[c] - m * xj[c];
-          v[c] = (!g0 && i >= j) ? ux : v[c];
-        }
-      }
-      if (grp == 0) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c)
-          if (c <= i) A[LI::idx(k0 + i, k0 + c)] = v[c];
-      } else if (grp == 1) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) Dinv[c * 16 + i] = v[c];  // column-major L_kk^-1
-      }
-      if (lane == 0 && bad) *flag = k0 + 1;
-    }
-    __syncthreads();
-    CH_STAMP(0)
     if (*flag) break;
-    // ---------------- (b) panel and X row block
-    // Linv_kk operands: A-op  a[r] = Linv[lr][4r+lk]  (Dinv column-major: Dinv[c*16 + i])
-    //                   B-op of Linv^T: b[r] = Linv^T[4r+lk][lr] = Linv[lr][4r+lk]  (same value)
-    double lopA[4];
+    const double* Dinv = Dinv0 + 256 * (k & 1);
+    // ---------------- (b) panel and X row block (waves 1-7)
+    if (wk >= 0) {
+      // Linv_kk operands: A-op a[r] = Linv[lr][4r+lk] (Dinv column-major: Dinv[c*16 + i]);
+      // the B-op of Linv^T for K-chunk r, B[4r+lk][lr] = Linv[lr][4r+lk], is the same value
+      double lopA[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) lopA[r] = Dinv[(4 * r + lk) * 16 + lr];
+      for (int r = 0; r < 4; ++r) lopA[r] = Dinv[(4 * r + lk) * 16 + lr];
 #pragma unroll
-    for (int q = 0; q < SLOTS; ++q) {
-      const int t = w + NW * q;
-      if (t >= NTILES) continue;
-      int ti, tj;
-      tile_of(t, ti, tj);
-      if (ti >= nt) continue;
-      if (tj == k && ti > k) {  // panel tile: L21_i = A_ik Linv^T
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
+      for (int q = 0; q < SLOTS; ++q) {
+        const int t = wk + NWK * q;
+        if (t >= NTILES) continue;
+        int ti, tj;
+        tile_of(t, ti, tj);
+        if (ti >= nt) continue;
+        if (tj == k && ti > k) {  // panel tile: L21_i = A_ik Linv^T
+          d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc = mfma64(A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)], lopA[r], acc);
-        // (B-op of Linv^T for K-chunk r: B[4r+lk][lr] = Linv[lr][4r+lk] = lopA[r])
+          for (int r = 0; r < 4; ++r)
+            acc = mfma64(A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)], lopA[r], acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, k0 + lr)] = acc[r];
-      }
-      if (ti == k && tj <= k) {  // X_kj <- Linv_kk X_kj
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
+          for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, k0 + lr)] = acc[r];
+        }
+        if (ti == k && tj <= k) {  // X_kj <- Linv_kk X_kj
+          d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc = mfma64(lopA[r], X[q][r], acc);
-        X[q] = acc;
+          for (int r = 0; r < 4; ++r) acc = mfma64(lopA[r], X[q][r], acc);
+          X[q] = acc;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Xr[(lk + 4 * r) * XLD + 16 * tj + lr] = acc[r];
+          for (int r = 0; r < 4; ++r) Xr[(lk + 4 * r) * XLD + 16 * tj + lr] = acc[r];
+        }
       }
     }
     __syncthreads();
     CH_STAMP(1)
-    // ---------------- (c) trailing updates
+    // ---------------- (c) trailing updates (waves 1-7) || next diagonal tile (wave 0)
+    if (wk >= 0) {
 #pragma unroll
-    for (int q = 0; q < SLOTS; ++q) {
-      const int t = w + NW * q;
-      if (t >= NTILES) continue;
-      int ti, tj;
-      tile_of(t, ti, tj);
-      if (ti >= nt || ti <= k) continue;
-      if (tj > k) {  // A_ij -= L21_i L21_j^T
-        d4 acc;
+      for (int q = 0; q < SLOTS; ++q) {
+        const int t = wk + NWK * q;
+        if (t >= NTILES) continue;
+        int ti, tj;
+        tile_of(t, ti, tj);
+        if (ti >= nt || ti <= k) continue;
+        if (tj > k) {  // A_ij -= L21_i L21_j^T  (the next diagonal tile is wave 0's)
+          if (ti == k + 1 && tj == k + 1) continue;
+          d4 acc;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = A[LI::idx(16 * ti + lk + 4 * r, 16 * tj + lr)];
+          for (int r = 0; r < 4; ++r) acc[r] = A[LI::idx(16 * ti + lk + 4 * r, 16 * tj + lr)];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc = mfma64(-A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)],
-                       A[LI::idx(16 * tj + lr, k0 + 4 * r + lk)], acc);
+          for (int r = 0; r < 4; ++r)
+            acc = mfma64(-A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)],
+                         A[LI::idx(16 * tj + lr, k0 + 4 * r + lk)], acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, 16 * tj + lr)] = acc[r];
-      } else {  // X_ij -= L21_i X_kj  (tj <= k)
+          for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, 16 * tj + lr)] = acc[r];
+        } else {  // X_ij -= L21_i X_kj  (tj <= k)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          X[q] = mfma64(-A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)],
-                        Xr[(4 * r + lk) * XLD + 16 * tj + lr], X[q]);
+          for (int r = 0; r < 4; ++r)
+            X[q] = mfma64(-A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)],
+                          Xr[(4 * r + lk) * XLD + 16 * tj + lr], X[q]);
+        }
       }
+    } else if (k + 1 < nt) {
+      // look-ahead: A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T, then factor it
+      const int t1 = 16 * (k + 1);
+      d4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = A[LI::idx(t1 + lk + 4 * r, t1 + lr)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc = mfma64(-A[LI::idx(t1 + lr, k0 + 4 * r + lk)], A[LI::idx(t1 + lr, k0 + 4 * r + lk)], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) A[LI::idx(t1 + lk + 4 * r, t1 + lr)] = acc[r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // own LDS writes before the reads
+      __builtin_amdgcn_wave_barrier();
+      chol_diag16<NP>(A, t1, Dinv0 + 256 * ((k + 1) & 1), flag, lane);
     }
     __syncthreads();
     CH_STAMP(2)
   }
   if (tid == 0 && info) info[blockIdx.x] = *flag;
-  // ---- write L^-1 (lower tiles from registers, zeros above)
+  // ---- write L^-1 (lower tiles from the workers' registers, zeros above)
   const MatDesc<double> o = out_inv[blockIdx.x];
+  if (wk >= 0) {
 #pragma unroll
-  for (int q = 0; q < SLOTS; ++q) {
-    const int t = w + NW * q;
-    if (t >= NTILES) continue;
-    int ti, tj;
-    tile_of(t, ti, tj);
+    for (int q = 0; q < SLOTS; ++q) {
+      const int t = wk + NWK * q;
+      if (t >= NTILES) continue;
+      int ti, tj;
+      tile_of(t, ti, tj);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gi = 16 * ti + lk + 4 * r, gj = 16 * tj + lr;
-      if (gi < n && gj < n) o.A[gi + (size_t)gj * o.lda] = X[q][r];
+      for (int r = 0; r < 4; ++r) {
+        const int gi = 16 * ti + lk + 4 * r, gj = 16 * tj + lr;
+        if (gi < n && gj < n) o.A[gi + (size_t)gj * o.lda] = X[q][r];
+      }
     }
   }
   for (int j = tid >> 4; j < n; j += 32)
     for (int i = (tid & 15); i < (j & ~15); i += 16) o.A[i + (size_t)j * o.lda] = 0.0;  // tiles above
+  CH_STAMP(4)
 }
 
 template <int NP>
-size_t chol_inv_mfma_lds() { return sizeof(double) * ((size_t)NP * NP + 256 + 16 * (NP + 16)) + 16; }
+size_t chol_inv_mfma_lds() { return sizeof(double) * ((size_t)NP * NP + 512 + 16 * (NP + 16)) + 16; }
 
 }  // namespace clrsdp
 

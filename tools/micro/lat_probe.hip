@@ -122,6 +122,28 @@ int run_diag(const char* name) {
   return 0;
 }
 
+// launch cost of a 512-thread workgroup with a large dynamic LDS allocation
+__global__ __launch_bounds__(512) void big_lds_kernel(double* out) {
+  extern __shared__ double dyn[];
+  dyn[threadIdx.x] = threadIdx.x;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = dyn[5];
+}
+int run_biglds(size_t lds, int blocks) {
+  double* o; CK(hipMalloc(&o, 4096 * 8));
+  CK(hipFuncSetAttribute((const void*)big_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  big_lds_kernel<<<blocks, 512, lds>>>(o);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < 20; ++r) big_lds_kernel<<<blocks, 512, lds>>>(o);
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  printf("512-thread kernel, %6zu B dynamic LDS, %4d blocks: %.2f us per launch\n", lds, blocks, ms * 1e3 / 20);
+  CK(hipFree(o));
+  return 0;
+}
+
 int main() {
   for (int th : {64, 256, 512, 1024}) {
     run<0>("barrier", th, 128);
@@ -134,6 +156,9 @@ int main() {
   run<5>("16 dependent fp64 fma", 64, 128);
   run<6>("dependent LDS read", 512, 128);
   run<6>("dependent LDS read", 64, 128);
+  run_biglds(1024, 128);
+  run_biglds(150 * 1024, 128);
+  run_biglds(150 * 1024, 1);
   run_diag<0>("full");
   run_diag<1>("no pivot readlane");
   run_diag<2>("no rsq");
