@@ -115,8 +115,12 @@ struct GemmPlan {
     d = upload_vec(h);
     dt = upload_vec(t2d);
   }
-  void launch(hipStream_t s, double alpha, double beta) const {
+  // C = alpha op(A) op(B) + beta Cin (+ dmult * *dscal on the diagonal of square problems)
+  void launch(hipStream_t s, double alpha, double beta, const T* dscal = nullptr,
+              double dmult = 0.0) const {
     if (h.empty()) return;
+    if (dscal && !std::is_same<T, double>::value)
+      throw ClrsdpError{CLRSDP_E_ARG, "fused diagonal epilogue is fp64 only"};
     const unsigned grid = (unsigned)t2d.size();
     if (gemv) {
       if (tb) throw ClrsdpError{CLRSDP_E_ARG, "gemv with transposed vector"};
@@ -126,11 +130,12 @@ struct GemmPlan {
       return;
     }
     if constexpr (std::is_same<T, double>::value) {
-      if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
-      else if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
-      else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
-      else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
-      else gemm_f64_lds<true, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
+      const double* ds = reinterpret_cast<const double*>(dscal);
+      if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
+      else if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
+      else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
+      else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
+      else gemm_f64_lds<true, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
     } else {
       if (!ta && !tb) gemm_valu<T, false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else if (ta && !tb) gemm_valu<T, true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
@@ -919,7 +924,7 @@ struct Solver final : HandleBase {
     p.pd_feas = pd_feas;
     return p;
   }
-  bool zero_cy = false;
+  bool zero_cy = false, zero_info = false;
   // ---- scalar slots + status words: one device block, one pinned host mirror
   char* stat_dev = nullptr;
   char* stat_host = nullptr;
@@ -940,6 +945,9 @@ struct Solver final : HandleBase {
   void scalars(const clrsdp_params* prm, int pd_feas, int which) {
     ScalarParams<T> p = prm ? sparams(prm, pd_feas) : ScalarParams<T>{};
     p.zero_cy = zero_cy ? 1 : 0;
+    p.zero_n = zero_info ? info_count : 0;  // status words of this iteration
+    p.zero_ptr = info;
+    zero_info = false;
     size_t q = 0;
     while (q < pend.size() || q == 0) {  // at most 6 folded reductions per launch
       const size_t cnt = std::min<size_t>(6, pend.size() - q);
@@ -947,7 +955,8 @@ struct Solver final : HandleBase {
       for (size_t i = 0; i < cnt; ++i) p.red[i] = pend[q + i];
       q += cnt;
       const bool last = q >= pend.size();
-      scalar_kernel<T><<<1, 1, 0, stream>>>(sc, p, last ? which : -1);
+      scalar_kernel<T><<<1, 64, 0, stream>>>(sc, p, last ? which : -1);
+      p.zero_n = 0;
       if (last) break;
     }
     pend.clear();
@@ -992,12 +1001,30 @@ struct Solver final : HandleBase {
 
   // ---------------- stages
   void st_mu_r(const clrsdp_params* prm, int pd_feas) {
-    local_blk_reduce(X, Y, nullptr, nullptr, 0, xsend);
-    exchange(1, 1);
-    reduce_ranks(1, 0, 0, SC_DOT_XY);
+    blk_dot(X, Y, nullptr, nullptr, 0, SC_DOT_XY, 1);
+    zero_info = true;  // the first scalar launch of an iteration clears the status words
     scalars(prm, pd_feas, 0);
-    p_XY.launch(stream, -1.0, 0.0);             // R = -XY
-    blk_lin(R, R, 1.0, nullptr, 0.0, sc + SC_MU_P);  // R += mu_p I
+    gemm_diag(p_XY, -1.0, 0.0, SC_MU_P);         // R = mu_p I - XY
+  }
+  // sum/max over the local blocks into sc[slot], all-gathered and rank-reduced when world > 1
+  void blk_dot(const T* A, const T* B_, const T* dA, const T* dB, int op, int slot, int tag) {
+    if (world == 1 && nb()) {
+      flat_reduce<T><<<RED_G, 256, 0, stream>>>(A, B_, dA, dB, nblk_el, op, bpart);
+      fold(bpart, RED_G, op == 2 ? 2 : 0, slot);  // partials folded into the next scalar launch
+      return;
+    }
+    local_blk_reduce(A, B_, dA, dB, op, xsend);
+    exchange(tag, 1);
+    reduce_ranks(1, 0, op == 2 ? 2 : 0, slot);
+  }
+  // plan.launch + "s I" on the block diagonals (fused into the fp64 GEMM epilogue)
+  void gemm_diag(const GemmPlan<T>& plan, double alpha, double beta, int slot) {
+    if constexpr (std::is_same<T, double>::value) {
+      plan.launch(stream, alpha, beta, sc + slot, 1.0);
+    } else {
+      plan.launch(stream, alpha, beta);
+      if (nb()) diag_add<T><<<nb(), 128, 0, stream>>>(d_blk, R, sc + slot, 1.0);
+    }
   }
   void st_xinv() {
     if (reg_blk) {  // L_X^-1 and L_Y^-1 on chip in one launch, X^-1 = L^-T L^-1 on MFMA
@@ -1059,10 +1086,14 @@ struct Solver final : HandleBase {
     }
     p_Q.launch(stream, 1.0, 0.0);             // slab_j = W_j^T W_j
     const int64_t q2 = n_y * n_y;
-    if (nc()) slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(Qslab, nc(), q2, q2, xsend);
-    else fill(xsend, 0.0, q2);
-    exchange(2, q2);
-    slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(xrecv, world, q2, q2, Q);
+    if (world == 1 && nc()) {
+      slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(Qslab, nc(), q2, q2, Q);
+    } else {
+      if (nc()) slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(Qslab, nc(), q2, q2, xsend);
+      else fill(xsend, 0.0, q2);
+      exchange(2, q2);
+      slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(xrecv, world, q2, q2, Q);
+    }
   }
   void factor_q() {
     const int64_t q2 = n_y * n_y;
@@ -1098,6 +1129,14 @@ struct Solver final : HandleBase {
   }
   void residuals_finish() {
     const int64_t k = n_y + 2;
+    if (world == 1 && nc()) {  // p = b - sum_j B_j^T x_j in one launch; maxima folded
+      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, pvec, bvec, 1.0, -1.0);
+      fold(tmpsc, 1, 2, SC_ERR_PMAT);
+      fold(tmpsc + 1, 1, 2, SC_ERR_DVEC);
+      fold(pvec, (int)n_y, 4, SC_ERR_PVEC);
+      flush_scalars();
+      return;
+    }
     if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
     else fill(xsend, 0.0, n_y);
     vlin(xsend + n_y, tmpsc, 1.0, nullptr, 0, nullptr, 0, 2);
@@ -1113,7 +1152,9 @@ struct Solver final : HandleBase {
     // Z = sym(X^-1 (P Y - R))
     p_PY.launch(stream, 1.0, -1.0);
     p_Z.launch(stream, 1.0, 0.0);
-    sym(Z, Z, 0);
+    // Z is only consumed by trace_A: v^T Z v = v^T sym(Z) v, so the symmetrisation
+    // (MPMP.jl:1704-1716) matters only for the off-diagonal (r != s) blocks of m > 1
+    if (anyMgt1) sym(Z, Z, 0);
     // rhs_x = -d - Tr(A_* Z)
     p_trU_Z.launch(stream, 1.0, 0.0);
     colsums();
@@ -1126,11 +1167,15 @@ struct Solver final : HandleBase {
       t_t.launch(stream, false);
     }
     p_Wt.launch(stream, 1.0, 0.0);
-    if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
-    else fill(xsend, 0.0, n_y);
-    exchange(tag, n_y);
-    slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec);
-    vlin(dyv, pvec, 1.0, uvec, -1.0, nullptr, 0, n_y);
+    if (world == 1 && nc()) {  // dy <- p - sum_j W_j^T t_j in one launch
+      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, dyv, pvec, 1.0, -1.0);
+    } else {
+      if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+      else fill(xsend, 0.0, n_y);
+      exchange(tag, n_y);
+      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec);
+      vlin(dyv, pvec, 1.0, uvec, -1.0, nullptr, 0, n_y);
+    }
     if (pending_q) {  // L_Q^-1 is being computed on the side stream (iterate)
       HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
       pending_q = false;
@@ -1159,13 +1204,10 @@ struct Solver final : HandleBase {
     sym(dY, dY, 0);
   }
   void st_corrector_r(const clrsdp_params* prm, int pd_feas) {
-    local_blk_reduce(X, Y, dX, dY, 1, xsend);
-    exchange(5, 1);
-    reduce_ranks(1, 0, 0, SC_DOT_XDY);
+    blk_dot(X, Y, dX, dY, 1, SC_DOT_XDY, 5);
     scalars(prm, pd_feas, 1);
     p_XY.launch(stream, -1.0, 0.0);
-    p_dXdY.launch(stream, -1.0, 1.0);
-    blk_lin(R, R, 1.0, nullptr, 0.0, sc + SC_MU_C);
+    gemm_diag(p_dXdY, -1.0, 1.0, SC_MU_C);      // R = mu_c I - XY - dX dY
   }
   void st_step(const clrsdp_params* prm, int pd_feas) {
     if (reg_blk) {
@@ -1295,7 +1337,7 @@ struct Solver final : HandleBase {
 
   // Enqueue one loop body (all stages) on `stream`, with the side stream joined back in.
   void enqueue_iteration(const clrsdp_params* prm, int pd_feas) {
-    HIPCHK(hipMemsetAsync(info, 0, info_count * sizeof(int), stream));
+    // (the status words are cleared by the first scalar launch of MU_R)
     auto mark = [&](int s) {
       if (timing) HIPCHK(hipEventRecord(ev[s], stream));
     };

@@ -118,7 +118,9 @@ __device__ inline int acc_col(int wn, int ni, int lr, int wcols = 32) { return w
 template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8>
 __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
                                                         const TileRef* __restrict__ t2d,
-                                                        double alpha, double beta) {
+                                                        double alpha, double beta,
+                                                        const double* __restrict__ dscal = nullptr,
+                                                        double dmult = 0.0) {
   using namespace lds_gemm;
   constexpr int NTH = 64 * NW, WN = NW / 2, NI = 4 / WN, WC = 64 / WN;
   using SL = Slab<BK, NTH>;
@@ -189,6 +191,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* 
       if (col < N) {
         double v = alpha * smem[lane * TP + cl];
         if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];
+        if (dscal && row == col) v += dmult * *dscal;  // fused "+ s I" (square diagonal blocks)
         d.C[row + (size_t)col * d.ldc] = v;
       }
     }
@@ -1198,8 +1201,10 @@ __global__ void ordered_reduce(const T* in, int cnt, long long stride, int op, T
 }
 
 // out[e] = sum_{i<cnt} in[i*stride + e]  (fixed order), e < n
+// (optionally out[e] = cbase*base[e] + csum*sum, the two vector updates that follow a slab sum)
 template <class T>
-__global__ void slab_sum(const T* in, int cnt, long long stride, long long n, T* out) {
+__global__ void slab_sum(const T* in, int cnt, long long stride, long long n, T* out,
+                         const T* base = nullptr, double cbase = 0.0, double csum = 1.0) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   T acc = in[e];
@@ -1212,6 +1217,7 @@ __global__ void slab_sum(const T* in, int cnt, long long stride, long long n, T*
     for (int u = 0; u < 8; ++u) acc += v[u];
   }
   for (; i < cnt; ++i) acc += in[(size_t)i * stride + e];
+  if (base) acc = base[e] * T(cbase) + acc * T(csum);
   out[e] = acc;
 }
 
@@ -1421,24 +1427,47 @@ template <class T> struct ScalarParams {
   int pd_feas;
   int nred;
   int zero_cy;  // which == 3 without C: <C,Y> = 0
+  int zero_n;   // zero the status words zero_ptr[0..zero_n) (start of an iteration)
+  int* zero_ptr;
   FoldRed<T> red[6];
 };
 
+// one wave: lane l folds elements l, l+64, ... in order, then a fixed xor butterfly
 template <class T>
-__global__ void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
-  if (threadIdx.x != 0) return;
-  for (int q = 0; q < p.nred; ++q) {
-    const FoldRed<T> r = p.red[q];
-    T acc = r.op == 4 ? Num<T>::abs_(r.src[0]) : r.src[0];
-    for (int i = 1; i < r.cnt; ++i) {
-      T v = r.src[(size_t)i * r.stride];
-      if (r.op == 4) v = Num<T>::abs_(v);
-      if (r.op == 0) acc += v;
-      else if (r.op == 3) acc = (v < acc) ? v : acc;
-      else acc = (v > acc) ? v : acc;
-    }
-    sc[r.dst] = acc;
+__device__ T fold_wave(const FoldRed<T>& r, int lane) {
+  const bool sum = r.op == 0;
+  const bool mn = r.op == 3;
+  T acc;
+  bool have = false;
+  for (int i = lane; i < r.cnt; i += 64) {
+    T v = r.src[(size_t)i * r.stride];
+    if (r.op == 4) v = Num<T>::abs_(v);
+    if (!have) { acc = v; have = true; }
+    else if (sum) acc += v;
+    else if (mn) acc = (v < acc) ? v : acc;
+    else acc = (v > acc) ? v : acc;
   }
+  // lanes without elements hold the first element (neutral for min/max) or 0 (sum)
+  if (!have) acc = sum ? T(0.0) : (r.op == 4 ? Num<T>::abs_(r.src[0]) : r.src[0]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const T v = shfl_xor_t(acc, o);
+    if (sum) acc += v;
+    else if (mn) acc = (v < acc) ? v : acc;
+    else acc = (v > acc) ? v : acc;
+  }
+  return acc;
+}
+
+template <class T>
+__global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
+  const int lane = threadIdx.x;
+  for (int e = lane; e < p.zero_n; e += 64) p.zero_ptr[e] = 0;
+  for (int q = 0; q < p.nred; ++q) {
+    const T v = fold_wave(p.red[q], lane);
+    if (lane == 0) sc[p.red[q].dst] = v;
+  }
+  if (lane != 0) return;
   const T dim = T(p.dim);
   if (which == 0) {  // mu, mu_p
     sc[SC_MU] = sc[SC_DOT_XY] / dim;
