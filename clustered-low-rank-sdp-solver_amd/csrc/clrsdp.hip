@@ -598,10 +598,11 @@ struct Solver final : HandleBase {
       f_Y.add(LY + b.off, n, n);
       ci_XY.add(X + b.off, n, n, LX + b.off, n);
       q_xinv.add(LX + b.off, n, LX + b.off, n, nullptr, n, Xinv + b.off, n, n, n, n);
+      // step length: L^-1 dM L^-T for X and Y in the same two launches (Y's middle product in Z)
       q_sx1.add(LX + b.off, n, dX + b.off, n, nullptr, n, tA + b.off, n, n, n, n);
+      q_sx1.add(LY + b.off, n, dY + b.off, n, nullptr, n, Z + b.off, n, n, n, n);
       q_sx2.add(tA + b.off, n, LX + b.off, n, nullptr, n, tB + b.off, n, n, n, n);
-      q_sy1.add(LY + b.off, n, dY + b.off, n, nullptr, n, tA + b.off, n, n, n, n);
-      q_sy2.add(tA + b.off, n, LY + b.off, n, nullptr, n, tC + b.off, n, n, n, n);
+      q_sx2.add(Z + b.off, n, LY + b.off, n, nullptr, n, tC + b.off, n, n, n, n);
       e_X.add(tB + b.off, n, n);
       e_Y.add(tB + b.off, n, n);
       e_XY.add(tB + b.off, n, n);
@@ -638,10 +639,12 @@ struct Solver final : HandleBase {
           s_.a_off = (int)(xo + (int64_t)rsi * b.N);
           s_.scale = (r != s) ? 0.5 : 1.0;
           sd.push_back(s_);
-          p_wA_P.add(TY + uoff, del, V + b.voff, del, nullptr, 0,
-                     P + b.off + s * del + (int64_t)r * del * n, n, del, del, K);
-          p_wA_dX.add(TY + uoff, del, V + b.voff, del, nullptr, 0,
-                      dX + b.off + s * del + (int64_t)r * del * n, n, del, del, K);
+          // P = WA(x) - X and dX = WA(dx) + P: the second term rides in the GEMM's Cin
+          const int64_t so = s * del + (int64_t)r * del * n;
+          p_wA_P.add(TY + uoff, del, V + b.voff, del, X + b.off + so, n, P + b.off + so, n, del,
+                     del, K);
+          p_wA_dX.add(TY + uoff, del, V + b.voff, del, P + b.off + so, n, dX + b.off + so, n,
+                      del, del, K);
         }
     }
     for (const LBlk& b : lb) ci_XY.add(Y + b.off, b.n, b.n, LY + b.off, b.n);
@@ -990,12 +993,12 @@ struct Solver final : HandleBase {
       colsum_dot<T><<<g, 256, 0, stream>>>(d_pair, TX, V, tval);
     }
   }
-  void weighted_A(const T* a, const GemmPlan<T>& plan, T* out) {
+  void weighted_A(const T* a, const GemmPlan<T>& plan, T* out, double beta = 0.0) {
     if (n_pair) {
       dim3 g(64, n_pair);
       scale_cols<T><<<g, 256, 0, stream>>>(d_scale, V, lam, ksamp, a, TY);
     }
-    plan.launch(stream, 1.0, 0.0);
+    plan.launch(stream, 1.0, beta);
     if (anyMgt1) sym(out, out, 1, true);  // Symmetric(.) on blocks with m != 1 (MPMP.jl:1671-1674)
   }
 
@@ -1111,8 +1114,7 @@ struct Solver final : HandleBase {
   // P, d, the p-slabs and the local error maxima (no exchange: may run on the side stream)
   void residuals_local(bool use_AY) {
     // P = sum_i x_i A_i - X - C
-    weighted_A(x, p_wA_P, P);
-    blk_lin(P, P, 1.0, X, -1.0);
+    weighted_A(x, p_wA_P, P, -1.0);
     if (hasC) blk_lin(P, P, 1.0, Cm, -1.0);
     // d = c - B y - Tr(A_* Y)
     p_By.launch(stream, 1.0, 0.0);
@@ -1196,8 +1198,7 @@ struct Solver final : HandleBase {
       t_dx.launch(stream, true);
     }
     // dX = P + sum_i dx_i A_i
-    weighted_A(dx, p_wA_dX, dX);
-    blk_lin(dX, dX, 1.0, P, 1.0);
+    weighted_A(dx, p_wA_dX, dX, 1.0);
     // dY = sym(X^-1 (R - dX Y))
     p_dXY.launch(stream, -1.0, 1.0);
     p_dY.launch(stream, 1.0, 0.0);
@@ -1212,10 +1213,8 @@ struct Solver final : HandleBase {
   void st_step(const clrsdp_params* prm, int pd_feas) {
     if (reg_blk) {
       // L_X^-1, L_Y^-1 from the X^-1 stage;  M = L^-1 dM L^-T on MFMA; one eigen launch
-      q_sx1.launch(stream, 1.0, 0.0);
+      q_sx1.launch(stream, 1.0, 0.0);             // X and Y blocks together
       q_sx2.launch(stream, 1.0, 0.0);
-      q_sy1.launch(stream, 1.0, 0.0);
-      q_sy2.launch(stream, 1.0, 0.0);
       e_XY.eigmin(stream, eigX);
     } else {
       // X: L_X from the X^-1 stage
