@@ -315,7 +315,7 @@ struct Solver final : HandleBase {
   // ---------------- device memory
   hipStream_t own_stream = nullptr, stream = nullptr;
   T *X, *Y, *Xinv, *LX, *LY, *R, *P, *dX, *dY, *Z, *tA, *tB, *Cm;
-  T *V, *lam, *TX, *TY, *BX, *BY, *AY, *tval, *S, *Wm, *Bm, *Qslab, *Q, *Qf;
+  T *V, *lam, *TX, *TY, *BX, *BY, *AY, *tval, *S, *Wm, *Bm, *Qslab, *Q, *Qf, *Qinv;
   T *cvec, *x, *dx, *dvec, *rhs, *tvec, *tmpv, *pslab, *y, *bvec, *dyv, *pvec, *uvec;
   T *sc, *bpart, *eigX, *eigY, *tmpsc, *tC = nullptr, *Stmp = nullptr;
   T* Vt = nullptr;  // per block V^T (K x delta), fused Schur path only
@@ -335,7 +335,7 @@ struct Solver final : HandleBase {
   // on-chip factorisation path (all sizes <= reg_nmax<T>()): L^-1 and MFMA products
   bool reg_blk = false, reg_S = false, reg_Q = false;
   CholInvPlan<T> ci_XY, ci_S, ci_S11, ci_S22, ci_Q;
-  GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2;
+  GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2, q_qinv, q_qdy;
   GemmPlan<T> q_L21, q_S22, q_M, q_X21;  // 2x2 blocked L^-1 of S (dim_S in (128, 256])
   MatPlan<T> e_XY;                        // both step-length eigenproblems in one launch
   RectDesc* d_zero = nullptr;            // upper-right blocks of the 2x2 S factors
@@ -473,7 +473,7 @@ struct Solver final : HandleBase {
   ~Solver() override {
     // device memory is released with the process / hipDeviceReset; free what we own explicitly
     T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, BX, BY, AY,
-                 tval, S, Wm, Bm, Qslab, Q, Qf, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
+                 tval, S, Wm, Bm, Qslab, Q, Qf, Qinv, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
                  bvec, dyv, pvec, uvec, bpart, eigX, tmpsc, tC, Stmp, own_send, Vt};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
@@ -504,7 +504,7 @@ struct Solver final : HandleBase {
     AY = dmalloc<T>(nAY); tval = dmalloc<T>(nAY);
     S = dmalloc<T>(nS); Wm = dmalloc<T>(nB); Bm = dmalloc<T>(nB);
     Qslab = dmalloc<T>((size_t)std::max(nc(), 1) * n_y * n_y);
-    Q = dmalloc<T>(n_y * n_y); Qf = dmalloc<T>(n_y * n_y);
+    Q = dmalloc<T>(n_y * n_y); Qf = dmalloc<T>(n_y * n_y); Qinv = dmalloc<T>(n_y * n_y);
     cvec = dmalloc<T>(nx); x = dmalloc<T>(nx); dx = dmalloc<T>(nx); dvec = dmalloc<T>(nx);
     rhs = dmalloc<T>(nx); tvec = dmalloc<T>(nx); tmpv = dmalloc<T>(nx);
     pslab = dmalloc<T>((size_t)std::max(nc(), 1) * n_y);
@@ -728,6 +728,10 @@ struct Solver final : HandleBase {
     ci_Q.add(Q, (int)n_y, (int)n_y, Qf, (int)n_y);
     q_q1.add(Qf, (int)n_y, dyv, (int)n_y, nullptr, 0, uvec, (int)n_y, (int)n_y, 1, (int)n_y);
     q_q2.add(Qf, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
+    // Q^-1 = L_Q^-T L_Q^-1 once per iteration (side stream), then one GEMV per direction
+    q_qinv.ta = true;
+    q_qinv.add(Qf, (int)n_y, Qf, (int)n_y, nullptr, 0, Qinv, (int)n_y, (int)n_y, (int)n_y, (int)n_y);
+    q_qdy.add(Qinv, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
     n_zero = (int)zr.size();
     if (n_zero) d_zero = upload_vec(zr);
     if (nc()) {
@@ -740,7 +744,7 @@ struct Solver final : HandleBase {
     for (GemmPlan<T>* g : {&p_txy, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
-                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_L21, &q_S22, &q_M, &q_X21})
+                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &q_L21, &q_S22, &q_M, &q_X21})
       g->finalize();
     for (CholInvPlan<T>* c : {&ci_XY, &ci_S, &ci_S11, &ci_S22, &ci_Q}) c->finalize();
     e_XY.finalize();
@@ -1102,6 +1106,7 @@ struct Solver final : HandleBase {
     const int64_t q2 = n_y * n_y;
     if (reg_Q) {
       ci_Q.launch(stream, info + info_Q0);    // Qf = L_Q^-1
+      q_qinv.launch(stream, 1.0, 0.0);        // Q^-1 = L_Q^-T L_Q^-1
     } else {
       vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
       f_Q.potrf(stream, info + info_Q0);
@@ -1161,7 +1166,7 @@ struct Solver final : HandleBase {
     p_trU_Z.launch(stream, 1.0, 0.0);
     colsums();
     trace_aggregate(tval, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
-    // t_j = L_j^-1 rhs_j ;  u = sum_j W_j^T t_j ;  dy = Q^-1 (p - u)
+    // t_j = L_j^-1 rhs_j ;  u = sum_j W_j^T t_j ;  dy = Q^-1 (p - u) ; dx_j = L_j^-T (t_j + W_j dy)
     if (reg_S) {
       q_t.launch(stream, 1.0, 0.0);
     } else {
@@ -1169,22 +1174,22 @@ struct Solver final : HandleBase {
       t_t.launch(stream, false);
     }
     p_Wt.launch(stream, 1.0, 0.0);
-    if (world == 1 && nc()) {  // dy <- p - sum_j W_j^T t_j in one launch
-      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, dyv, pvec, 1.0, -1.0);
+    // r = p - sum_j W_j^T t_j  (-> uvec with the explicit Q^-1, -> dyv for the two solves)
+    T* rv = reg_Q ? uvec : dyv;
+    if (world == 1 && nc()) {  // one launch
+      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, rv, pvec, 1.0, -1.0);
     } else {
       if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
       else fill(xsend, 0.0, n_y);
       exchange(tag, n_y);
-      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec);
-      vlin(dyv, pvec, 1.0, uvec, -1.0, nullptr, 0, n_y);
+      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, rv, pvec, 1.0, -1.0);
     }
-    if (pending_q) {  // L_Q^-1 is being computed on the side stream (iterate)
+    if (pending_q) {  // L_Q^-1 and Q^-1 are being computed on the side stream (iterate)
       HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
       pending_q = false;
     }
     if (reg_Q) {
-      q_q1.launch(stream, 1.0, 0.0);          // u = L_Q^-1 r
-      q_q2.launch(stream, 1.0, 0.0);          // dy = L_Q^-T u
+      q_qdy.launch(stream, 1.0, 0.0);         // dy = Q^-1 r
     } else {
       t_Q.launch(stream, false);
       t_Q.launch(stream, true);
