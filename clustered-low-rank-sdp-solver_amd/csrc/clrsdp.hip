@@ -357,6 +357,7 @@ struct Solver final : HandleBase {
   long long n_pairs = 0;
   AYDesc* d_ayd = nullptr;
   PairDesc* d_pair = nullptr;
+  bool trivial_tuples = false;
   int n_pair = 0, max_K = 0;
   ScaleDesc* d_scale = nullptr;
   TupleDesc* d_td = nullptr;
@@ -631,7 +632,8 @@ struct Solver final : HandleBase {
                       TX + uoff, del, del, K, del);
           p_trU_Y.add(Y + b.off + r * del + (int64_t)s * del * n, n, V + b.voff, del, nullptr, 0,
                       TX + uoff, del, del, K, del);
-          pd.push_back(PairDesc{uoff, b.voff, b.ayoff + (int64_t)rsi * K, del, K});
+          pd.push_back(PairDesc{uoff, b.voff, b.ayoff + (int64_t)rsi * K, del, K, (int)b.koff,
+                                -1});
           // weighted A: block (s, r) = Vs V^T  (MPMP.jl:1659-1667)
           ScaleDesc s_;
           s_.v_off = b.voff; s_.vs_off = uoff; s_.delta = del; s_.K = K;
@@ -654,6 +656,20 @@ struct Solver final : HandleBase {
     if (n_blk_m) d_blk_m = upload_vec(bdm);
     d_ayd = upload_vec(ayd);
     n_pair = (int)pd.size();
+    // tuples <-> columns 1:1 in every local cluster (m = L = 1, every rank 1): fused trace_A
+    trivial_tuples = n_pair > 0;
+    {
+      int bi = 0, pi = 0;
+      for (int c = 0; c < nc() && trivial_tuples; ++c) {
+        const int j = oc[c];
+        trivial_tuples = m[j] == 1 && Lc[j] == 1;
+        for (int k = 0; k < Ns[j] && trivial_tuples; ++k)
+          trivial_tuples = ranks_all[rkoff_g[lb[bi].gjl] + k] == 1;
+        if (trivial_tuples) pd[pi].x_off = (int)c_xoff[c];
+        bi += (int)Lc[j];
+        pi += 1;
+      }
+    }
     d_pair = upload_vec(pd);
     d_scale = upload_vec(sd);
     // per cluster plans
@@ -1164,8 +1180,13 @@ struct Solver final : HandleBase {
     if (anyMgt1) sym(Z, Z, 0);
     // rhs_x = -d - Tr(A_* Z)
     p_trU_Z.launch(stream, 1.0, 0.0);
-    colsums();
-    trace_aggregate(tval, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
+    if (trivial_tuples) {
+      dim3 g(cdiv(max_K, 4), n_pair);
+      colsum_rhs<T><<<g, 256, 0, stream>>>(d_pair, TX, V, lam, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
+    } else {
+      colsums();
+      trace_aggregate(tval, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
+    }
     // t_j = L_j^-1 rhs_j ;  u = sum_j W_j^T t_j ;  dy = Q^-1 (p - u) ; dx_j = L_j^-T (t_j + W_j dy)
     if (reg_S) {
       q_t.launch(stream, 1.0, 0.0);
@@ -1273,15 +1294,21 @@ struct Solver final : HandleBase {
     zero_cy = false;
   }
   void st_update(const clrsdp_params* prm, int pd_feas) {
-    int* flag = info + info_count;
-    status_reduce<<<1, 256, 0, stream>>>(info, info_count, flag);
+    // every launch checks the status words itself (no update after a failed factorisation)
+    const bool small = world == 1 && !hasC;  // x, y and the objectives in one workgroup
     AxpyList<T> L;
     L.it[0] = AxpyItem<T>{X, dX, sc + SC_ALPHA_P, nblk_el};
     L.it[1] = AxpyItem<T>{Y, dY, sc + SC_ALPHA_D, nblk_el};
     L.it[2] = AxpyItem<T>{x, dx, sc + SC_ALPHA_P, nx};
     L.it[3] = AxpyItem<T>{y, dyv, sc + SC_ALPHA_D, n_y};
     const unsigned g = std::max<unsigned>(1, std::min<unsigned>(cdiv(std::max<int64_t>(nblk_el, nx), 256), 2048));
-    vec_axpy_list<T><<<dim3(g, 4), 256, 0, stream>>>(L, flag);
+    vec_axpy_list<T><<<dim3(g, small ? 2 : 4), 256, 0, stream>>>(L, info, info_count);
+    if (small) {
+      const ScalarParams<T> p = sparams(prm, pd_feas);
+      update_small<T><<<1, 1024, 0, stream>>>(x, dx, nx, y, dyv, n_y, cvec, bvec, sc, info,
+                                              info_count, p.b0);
+      return;
+    }
     objectives(prm, pd_feas);
   }
 

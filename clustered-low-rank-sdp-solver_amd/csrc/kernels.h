@@ -1263,9 +1263,16 @@ template <class T> struct AxpyItem {
   long long n;
 };
 template <class T> struct AxpyList { AxpyItem<T> it[4]; };
+// guard: skip when any status word info[0..ninfo) is set (a factorisation failed)
 template <class T>
-__global__ void vec_axpy_list(AxpyList<T> L, const int* flag) {
-  if (*flag) return;
+__global__ void vec_axpy_list(AxpyList<T> L, const int* info, int ninfo) {
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < ninfo; i += blockDim.x)
+    if (info[i]) any = 1;
+  __syncthreads();
+  if (any) return;
   const AxpyItem<T> I = L.it[blockIdx.y];
   const T a = *I.alpha;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < I.n;
@@ -1291,7 +1298,46 @@ struct PairDesc {
   long long v_off;    // V_b
   long long val_off;  // val_{b,rs} (K)
   int delta, K;
+  int lam_off;        // lambda_b (K)
+  int x_off;          // tuple of column 0 when the cluster's tuples map 1:1 to columns (m = L =
+                      // rank = 1), else -1
 };
+
+template <class T>
+__device__ __forceinline__ T wave_sum_t(T v) {
+  if constexpr (sizeof(T) == 8) {
+    return wave_sum_dpp(v);
+  } else {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += shfl_xor_t(v, o);
+    return v;
+  }
+}
+
+// trace_A + tuple aggregation in one launch for clusters with m = L = rank = 1 (tuple k <->
+// column k): out[x_off + col] = c_agg lambda_col (U[:,col] . V[:,col]) + c_in in[.] + c_in2 in2[.]
+template <class T>
+__global__ __launch_bounds__(256) void colsum_rhs(const PairDesc* __restrict__ pd, const T* U,
+                                                  const T* V, const T* lam, const T* in,
+                                                  double c_in, const T* in2, double c_in2,
+                                                  double c_agg, T* out) {
+  const PairDesc P = pd[blockIdx.y];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = blockIdx.x * 4 + wave;
+  if (col >= P.K) return;
+  const T* u = U + P.u_off + (size_t)col * P.delta;
+  const T* v = V + P.v_off + (size_t)col * P.delta;
+  T acc = T(0.0);
+  for (int i = lane; i < P.delta; i += 64) acc += u[i] * v[i];
+  acc = wave_sum_t(acc);
+  if (lane == 0) {
+    const long long g = (long long)P.x_off + col;
+    T o = lam[P.lam_off + col] * acc * T(c_agg);
+    if (in) o += in[g] * T(c_in);
+    if (in2) o += in2[g] * T(c_in2);
+    out[g] = o;
+  }
+}
 template <class T>
 __global__ __launch_bounds__(256) void colsum_dot(const PairDesc* __restrict__ pd, const T* U,
                                                   const T* V, T* val) {
@@ -1501,6 +1547,58 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     if (p.zero_cy) sc[SC_DOT_CY] = T(0.0);
     sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;
     sc[SC_DOBJ] = sc[SC_DOT_CY] + sc[SC_DOT_BY] + p.b0;
+  }
+}
+
+// x += alpha_p dx, y += alpha_d dy (guarded), then <c,x>, <b,y> and the objectives
+// (MPMP.jl:877-878, 940-941; one rank, C = 0).  One 1024-thread workgroup.
+template <class T>
+__global__ __launch_bounds__(1024) void update_small(T* x, const T* dx, long long nx, T* y,
+                                                     const T* dy, long long ny, const T* c,
+                                                     const T* b, T* sc, const int* info, int ninfo,
+                                                     T b0) {
+  __shared__ T red[1024];
+  __shared__ int any;
+  const int tid = threadIdx.x;
+  if (tid == 0) any = 0;
+  __syncthreads();
+  for (int i = tid; i < ninfo; i += 1024)
+    if (info[i]) any = 1;
+  __syncthreads();
+  const bool upd = !any;
+  const T ap = sc[SC_ALPHA_P], ad = sc[SC_ALPHA_D];
+  T acc = T(0.0);
+  for (long long e = tid; e < nx; e += 1024) {
+    T v = x[e];
+    if (upd) { v = v + ap * dx[e]; x[e] = v; }
+    acc += c[e] * v;
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int s2 = 512; s2 > 0; s2 >>= 1) {
+    if (tid < s2) red[tid] = red[tid] + red[tid + s2];
+    __syncthreads();
+  }
+  const T cx = red[0];
+  __syncthreads();
+  acc = T(0.0);
+  for (long long e = tid; e < ny; e += 1024) {
+    T v = y[e];
+    if (upd) { v = v + ad * dy[e]; y[e] = v; }
+    acc += b[e] * v;
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int s2 = 512; s2 > 0; s2 >>= 1) {
+    if (tid < s2) red[tid] = red[tid] + red[tid + s2];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    sc[SC_DOT_CX] = cx;
+    sc[SC_DOT_CY] = T(0.0);
+    sc[SC_DOT_BY] = red[0];
+    sc[SC_POBJ] = cx + b0;
+    sc[SC_DOBJ] = red[0] + b0;
   }
 }
 
