@@ -756,7 +756,11 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
       else v = (i == j) ? 1.0 : 0.0;
       A[LI::idx(i, j)] = v;
     }
-  if (tid == 0) *flag = 0;
+  if (tid == 0) {
+    flag[0] = 0;  // first failing pivot + 1
+    flag[1] = 0;  // panels whose A_{k+1,k} wave 0 has read
+    flag[2] = 0;  // worker arrivals at the (b)->(c) barrier
+  }
   // ---- X accumulators of the worker waves: identity on diagonal tiles
   const int wk = w - 1;  // worker index, -1 for wave 0
   d4 X[SLOTS];
@@ -777,7 +781,9 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
     const int k0 = 16 * k;
     if (*flag) break;
     const double* Dinv = Dinv0 + 256 * (k & 1);
-    // ---------------- (b) panel and X row block (waves 1-7)
+    // ---------------- (b) panel and X row block (waves 1-7)   ||   wave 0 runs ahead:
+    //   L_{k+1,k} = A_{k+1,k} L_kk^-T in registers, A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T, and the
+    //   factorisation of that tile, while the workers do (b) and (c) of panel k.
     if (wk >= 0) {
       // Linv_kk operands: A-op a[r] = Linv[lr][4r+lk] (Dinv column-major: Dinv[c*16 + i]);
       // the B-op of Linv^T for K-chunk r, B[4r+lk][lr] = Linv[lr][4r+lk], is the same value
@@ -796,6 +802,10 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             acc = mfma64(A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)], lopA[r], acc);
+          if (ti == k + 1) {  // wave 0 reads this tile's input first (in place update)
+            while (__hip_atomic_load(flag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
+              __builtin_amdgcn_s_sleep(1);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, k0 + lr)] = acc[r];
         }
@@ -808,11 +818,12 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
           for (int r = 0; r < 4; ++r) Xr[(lk + 4 * r) * XLD + 16 * tj + lr] = acc[r];
         }
       }
-    }
-    __syncthreads();
-    CH_STAMP(1)
-    // ---------------- (c) trailing updates (waves 1-7) || next diagonal tile (wave 0)
-    if (wk >= 0) {
+      // workers-only barrier (wave 0 is busy with the next diagonal tile)
+      if (lane == 0) __hip_atomic_fetch_add(flag + 2, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      while (__hip_atomic_load(flag + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NWK * (k + 1))
+        __builtin_amdgcn_s_sleep(1);
+      CH_STAMP(1)
+      // ---------------- (c) trailing updates (the next diagonal tile is wave 0's)
 #pragma unroll
       for (int q = 0; q < SLOTS; ++q) {
         const int t = wk + NWK * q;
@@ -820,7 +831,7 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
         int ti, tj;
         tile_of(t, ti, tj);
         if (ti >= nt || ti <= k) continue;
-        if (tj > k) {  // A_ij -= L21_i L21_j^T  (the next diagonal tile is wave 0's)
+        if (tj > k) {  // A_ij -= L21_i L21_j^T
           if (ti == k + 1 && tj == k + 1) continue;
           d4 acc;
 #pragma unroll
@@ -839,19 +850,34 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
         }
       }
     } else if (k + 1 < nt) {
-      // look-ahead: A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T, then factor it
       const int t1 = 16 * (k + 1);
+      double* scr = Dinv0 + 256 * ((k + 1) & 1);  // free until diag(k+1) writes it
+      double af[4], lop[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        af[r] = A[LI::idx(t1 + lr, k0 + 4 * r + lk)];
+        lop[r] = Dinv[(4 * r + lk) * 16 + lr];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(flag + 1, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      d4 l = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) l = mfma64(af[r], lop[r], l);  // L_{k+1,k}
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scr[lr * 16 + lk + 4 * r] = l[r];  // column-major 16x16
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       d4 acc;
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[r] = A[LI::idx(t1 + lk + 4 * r, t1 + lr)];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        acc = mfma64(-A[LI::idx(t1 + lr, k0 + 4 * r + lk)], A[LI::idx(t1 + lr, k0 + 4 * r + lk)], acc);
+      for (int r = 0; r < 4; ++r) {
+        const double f = scr[(4 * r + lk) * 16 + lr];  // L_{k+1,k}[lr][4r+lk]
+        acc = mfma64(-f, f, acc);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) A[LI::idx(t1 + lk + 4 * r, t1 + lr)] = acc[r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // own LDS writes before the reads
-      __builtin_amdgcn_wave_barrier();
-      chol_diag16<NP>(A, t1, Dinv0 + 256 * ((k + 1) & 1), flag, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      chol_diag16<NP>(A, t1, scr, flag, lane);
     }
     __syncthreads();
     CH_STAMP(2)
