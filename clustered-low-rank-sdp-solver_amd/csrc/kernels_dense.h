@@ -658,60 +658,67 @@ __device__ __forceinline__ void tile_of(int t, int& i, int& j) {
 }
 
 // One wave: Cholesky factor and inverse of the 16x16 diagonal tile at (k0, k0) of the LDS image.
-// Lanes 0-15 hold row i of A_kk (-> L_kk), lanes 16-31 row i of X_kk (-> L_kk^-1), 16 values each
-// in registers; the column loop is unrolled so every index is static and the cross-lane traffic
-// is v_readlane (uniform source lane) plus one permlane16 swap.  Writes L_kk back into the image
-// and L_kk^-1 column-major into Dinv; a non-positive pivot sets *flag = k0 + 1.
+// Lane (i = l & 15, g = l >> 4) holds row i, columns 4g..4g+3 of A_kk (-> L_kk) and of
+// X_kk (-> L_kk^-1).  Per column j: the pivot by v_readlane, column j of L and the scaled row j
+// of X through a 32-double LDS scratch (one wave: LDS order is program order, no barrier), then
+// four FMAs each for L and X (entries above the diagonal of L carry junk and are never used).
+// Writes L_kk back into the image and L_kk^-1 column-major into Dinv; a non-positive pivot sets
+// *flag = k0 + 1.
 template <int NP>
 __device__ inline void chol_diag16(double* __restrict__ A, int k0, double* __restrict__ Dinv,
-                                   int* flag, int lane) {
+                                   int* flag, double* sc, int lane) {
   using LI = CholLds<NP>;
-  const int i = lane & 15, grp = lane >> 4;
-  double v[16];
+  const int i = lane & 15, g = lane >> 4;
+  double a[4], x[4];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    const double av = A[LI::idx(k0 + i, k0 + min(c, i))];
-    v[c] = grp == 0 ? (c <= i ? av : 0.0) : (c == i ? 1.0 : 0.0);
+  for (int c = 0; c < 4; ++c) {
+    const int k = 4 * g + c;
+    a[c] = A[LI::idx(k0 + i, k0 + min(k, i))];
+    x[c] = (k == i) ? 1.0 : 0.0;
   }
+  // scratch traffic as relaxed atomics: with plain accesses the compiler may turn a predicated
+  // store into select + unconditional store, or forward a lane's own earlier value to a later
+  // load (both legal for one thread, wrong between lanes that share an address)
+  double* lsc = sc;       // column j of L below the diagonal (zeros at rows <= j)
+  double* xsc = sc + 16;  // row j of X after its scaling
   int bad = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const double djj = readlane_d(v[j], j);
-    bad |= !(djj > 0.0);
-    double r = __builtin_amdgcn_rsq(djj);
-    r = r * (1.5 - 0.5 * djj * r * r);  // Newton step: r = 1/sqrt(d) to ~1 ulp
-    // l_ij (meaningful in lanes 0-15 with i >= j); lanes 16-31 get their row's l_ij by a swap
-    const double lij = (i == j) ? djj * r : v[j] * r;
-    const double lsw = swap16_d(lij);
-    double xj[16];  // row j of X before its scaling (columns <= j), uniform
+    const int gj = j >> 2, cj = j & 3;
+    const double d = readlane_d(a[cj], 16 * gj + j);
+    bad |= !(d > 0.0);
+    double r = __builtin_amdgcn_rsq(d);
+    r = r * (1.5 - 0.5 * d * r * r);  // Newton step: r = 1/sqrt(d) to ~1 ulp
+    // l_ij = a_ij r (i >= j; l_jj = sqrt(d)) in the lanes of column group gj
+    a[cj] = (g == gj) ? a[cj] * r : a[cj];
+    if (g == gj)
+      __hip_atomic_store(lsc + i, (i > j) ? a[cj] : 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const double s = (i == j) ? r : 1.0;
 #pragma unroll
-    for (int c = 0; c <= j; ++c) xj[c] = readlane_d(v[c], 16 + j);
-    double lk[16];  // column j of L below the diagonal, uniform
+    for (int c = 0; c < 4; ++c) x[c] *= s;
+    if (i == j) {
 #pragma unroll
-    for (int t = j + 1; t < 16; ++t) lk[t] = readlane_d(lij, t);
-    // branch-free: lanes 0-15: v_j = l_ij, v_t -= l_ij l_tj (j < t <= i);
-    //              lanes 16-31: row j scaled by r, v_c -= (l_ij r) x_jc (c <= j, i > j)
-    const bool g0 = grp == 0, below = i > j;
-    const double m = lsw * r;
-    v[j] = (g0 && i >= j) ? lij : v[j];
+      for (int c = 0; c < 4; ++c)
+        __hip_atomic_store(xsc + 4 * g + c, x[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    const double li = __hip_atomic_load(lsc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    double lk[4], xr[4];
 #pragma unroll
-    for (int t = j + 1; t < 16; ++t) {
-      const double u = v[t] - lij * lk[t];
-      v[t] = (g0 && below && t <= i) ? u : v[t];
+    for (int c = 0; c < 4; ++c) {
+      lk[c] = __hip_atomic_load(lsc + 4 * g + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      xr[c] = __hip_atomic_load(xsc + 4 * g + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
 #pragma unroll
-    for (int c = 0; c <= j; ++c) {
-      const double ux = (i == j) ? v[c] * r : v[c] - m * xj[c];
-      v[c] = (!g0 && i >= j) ? ux : v[c];
+    for (int c = 0; c < 4; ++c) {
+      a[c] = fma(-li, lk[c], a[c]);
+      x[c] = fma(-li, xr[c], x[c]);
     }
   }
-  if (grp == 0) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c)
-      if (c <= i) A[LI::idx(k0 + i, k0 + c)] = v[c];
-  } else if (grp == 1) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) Dinv[c * 16 + i] = v[c];  // column-major L_kk^-1
+  for (int c = 0; c < 4; ++c) {
+    const int k = 4 * g + c;
+    if (k <= i) A[LI::idx(k0 + i, k0 + k)] = a[c];
+    Dinv[k * 16 + i] = x[c];  // column-major L_kk^-1
   }
   if (lane == 0 && bad) *flag = k0 + 1;
 }
@@ -741,6 +748,7 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
   double* Dinv0 = A + NP * NP;                        // 2 x (16 x 16), column-major, by k parity
   double* Xr = Dinv0 + 512;                           // 16 x XLD, row-major
   int* flag = reinterpret_cast<int*>(Xr + 16 * XLD);
+  double* dsc = reinterpret_cast<double*>(flag + 4);  // 32-double scratch of chol_diag16
   using LI = CholLds<NP>;
   const MatDesc<double> d = in[blockIdx.x];
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -748,14 +756,28 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
   const int lr = lane & 15, lk = lane >> 4;
   // ---- load the lower triangle (coalesced along columns); identity padding.  Nothing above
   // the diagonal tiles is ever read, and the upper halves of diagonal tiles only carry junk.
-  for (int j = tid >> 6; j < NP; j += 8)
-    for (int i = (tid & 63); i < NP; i += 64) {
-      if (i < j) continue;
-      double v;
-      if (i < n && j < n) v = d.A[i + (size_t)j * d.lda];
-      else v = (i == j) ? 1.0 : 0.0;
-      A[LI::idx(i, j)] = v;
+  {
+    // all NP*NP/512 loads in flight (clamped, unconditional), then the masked LDS stores
+    constexpr int PER = NP * NP / 512;
+    static_assert(PER * 512 == NP * NP, "NP*NP multiple of the workgroup");
+    double vl[PER];
+    const int nc = n > 0 ? n - 1 : 0;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int x = tid + 512 * e, i = x % NP, j = x / NP;
+#ifdef CLRSDP_CHOL_FULL_LOAD
+      vl[e] = gload(d.A + min(i, nc) + (size_t)min(j, nc) * d.lda);
+#else
+      vl[e] = 0.0;
+      if (i >= j) vl[e] = gload(d.A + min(i, nc) + (size_t)min(j, nc) * d.lda);  // lower only
+#endif
     }
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int x = tid + 512 * e, i = x % NP, j = x / NP;
+      if (i >= j) A[LI::idx(i, j)] = (i < n && j < n) ? vl[e] : (i == j ? 1.0 : 0.0);
+    }
+  }
   if (tid == 0) {
     flag[0] = 0;  // first failing pivot + 1
     flag[1] = 0;  // panels whose A_{k+1,k} wave 0 has read
@@ -774,7 +796,8 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
       X[q][r] = (wk >= 0 && t < NTILES && ti == tj && (lk + 4 * r) == lr) ? 1.0 : 0.0;
   }
   __syncthreads();
-  if (w == 0) chol_diag16<NP>(A, 0, Dinv0, flag, lane);
+  CH_STAMP(0)
+  if (w == 0) chol_diag16<NP>(A, 0, Dinv0, flag, dsc, lane);
   __syncthreads();
   CH_STAMP(3)
   for (int k = 0; k < nt; ++k) {
@@ -877,7 +900,7 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
 #pragma unroll
       for (int r = 0; r < 4; ++r) A[LI::idx(t1 + lk + 4 * r, t1 + lr)] = acc[r];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      chol_diag16<NP>(A, t1, scr, flag, lane);
+      chol_diag16<NP>(A, t1, scr, flag, dsc, lane);
     }
     __syncthreads();
     CH_STAMP(2)
@@ -905,7 +928,7 @@ __global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __re
 }
 
 template <int NP>
-size_t chol_inv_mfma_lds() { return sizeof(double) * ((size_t)NP * NP + 512 + 16 * (NP + 16)) + 16; }
+size_t chol_inv_mfma_lds() { return sizeof(double) * ((size_t)NP * NP + 512 + 16 * (NP + 16) + 32) + 16; }
 
 }  // namespace clrsdp
 

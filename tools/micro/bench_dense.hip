@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
 #ifdef CLRSDP_EIG_STAMPS
     unsigned long long st[8];
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_eig_stamps), sizeof(st)));
-    printf("  chol stamps per matrix: load %.0f diag %.0f  panel %.0f  trailing %.0f  output %.0f\n", st[3] / (3.0 * nb), st[0] / (3.0 * nb), st[1] / (3.0 * nb), st[2] / (3.0 * nb), st[4] / (3.0 * nb));
+    printf("  chol stamps per matrix: diag0 %.0f load %.0f  panel %.0f  trailing %.0f  output %.0f\n", st[3] / (3.0 * nb), st[0] / (3.0 * nb), st[1] / (3.0 * nb), st[2] / (3.0 * nb), st[4] / (3.0 * nb));
     unsigned long long z[8] = {0};
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_eig_stamps), z, sizeof(z)));
 #endif
