@@ -23,6 +23,7 @@
 
 using namespace clrsdp;
 using mw::dd;
+using mw::qd;
 using mw::Num;
 
 namespace {
@@ -65,6 +66,7 @@ inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) /
 // register-tile shapes of chol_inv_reg per word type (NMAX = TR * GR)
 template <class T> struct RegCfg { static constexpr int TR = 4, TC = 8, GR = 32, GC = 16; };
 template <> struct RegCfg<dd> { static constexpr int TR = 2, TC = 4, GR = 32, GC = 16; };
+template <> struct RegCfg<qd> { static constexpr int TR = 1, TC = 2, GR = 32, GC = 16; };
 template <class T> constexpr int reg_nmax() { return std::is_same<T, double>::value ? 128 : RegCfg<T>::TR * RegCfg<T>::GR; }
 template <class T> size_t eig_lds_bytes(int n) { return sizeof(T) * ((size_t)n * n + 10 * (size_t)n + 40); }
 constexpr size_t LDS_MAX = 160 * 1024;
@@ -1543,7 +1545,8 @@ int32_t clrsdp_create(const clrsdp_desc* desc, const clrsdp_config* cfg, clrsdp_
     auto* hh = new clrsdp_handle();
     if (cfg->precision_words == 1) hh->impl.reset(new Solver<double>(desc, cfg));
     else if (cfg->precision_words == 2) hh->impl.reset(new Solver<dd>(desc, cfg));
-    else { delete hh; g_last_error = "precision_words must be 1 or 2"; return CLRSDP_E_ARG; }
+    else if (cfg->precision_words == 4) hh->impl.reset(new Solver<qd>(desc, cfg));
+    else { delete hh; g_last_error = "precision_words must be 1, 2 or 4"; return CLRSDP_E_ARG; }
     *out = hh;
     return CLRSDP_OK;
   })

@@ -284,20 +284,17 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
   for (int k = 0; k + 2 < n; ++k) {
     if (((k + 1) & 7) == 0) { EIG_SHIFT_SLOTS(); ++q; }
     const double* col = colb[k & 1];
-    const int m = n - k - 1;
     const int ns = NS - q;  // slots that hold existing columns
-    // ---- all LDS reads of this column first (one wait)
+    // ---- LDS reads: the column tail for the norm first (rows > k+128 read the zero padding),
+    // then the slot values, so the norm's wait does not cover the slot reads
+    const double xa = col[k + 1 + lane], xb = col[k + 65 + lane];
     double2 cv[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       cv[s] = *reinterpret_cast<const double2*>(col + 2 * c + 8 * (s + q));
     const double xi = col[i < 128 ? i : 0];
     // ---- reflector of column k (every wave, redundantly)
-    double ss = 0.0;
-    for (int t = lane; t < m; t += 64) {
-      const double x = col[k + 1 + t];
-      ss += x * x;
-    }
+    double ss = fma(xa, xa, xb * xb);
     ss = wave_sum_dpp(ss);
     const double x0 = col[k + 1];
     const double tail = ss - x0 * x0;
@@ -328,7 +325,7 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
       }
       const double vi = i > k ? (i == jn ? v0 : xi) : 0.0;
       const bool wave_live = w * 16 + 15 > k;  // wave-uniform: some row of this wave is active
-      double pp = 0.0;
+      double pp = 0.0, pq = 0.0;  // two FMA chains
       // slots in groups of 4 behind one uniform branch each (a per-slot condition gets
       // if-converted into computing everything plus selects)
       if (wave_live) {
@@ -336,10 +333,14 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
         for (int g = 0; g < NS / 4; ++g) {
           if (4 * g < ns) {
 #pragma unroll
-            for (int s = 4 * g; s < 4 * g + 4; ++s) pp += a[s][0] * cv[s].x + a[s][1] * cv[s].y;
+            for (int s = 4 * g; s < 4 * g + 4; ++s) {
+              pp = fma(a[s][0], cv[s].x, pp);
+              pq = fma(a[s][1], cv[s].y, pq);
+            }
           }
         }
       }
+      pp += pq;
       ER_STAMP(7)
       pp = xsum32(xsum16(pp));
       double t = 0.0;

@@ -131,13 +131,25 @@ def test_stage_parity_dd_vs_256bit(pk, oracle):
     _stage_compare(pk, oracle, consm, ar.asarray(b), words=2, ar=ar, tol=1e-25)
 
 
+def test_stage_parity_qd_vs_256bit(pk, oracle):
+    """quad-double kernels against the 256-bit oracle (qd carries ~212 bits; the state is
+    well-conditioned, so 1e-50 leaves three to six orders of magnitude for conditioning)."""
+    cons, b = pk.synth(seed=3, J=2, delta=4, rank=1, n_y=4)
+    ar = oracle.Mp(256)
+    consm = [pk.Cluster([[[ar.asarray(v) for v in vk] for vk in Al] for Al in cl.A],
+                        ar.asarray(cl.B), ar.asarray(cl.c),
+                        [[[ar.num(x) for x in hk] for hk in Hl] for Hl in cl.H]) for cl in cons]
+    _stage_compare(pk, oracle, consm, ar.asarray(b), words=4, ar=ar, tol=1e-50)
+
+
 def _golden(name):
     return json.load(open(os.path.join(GOLDEN, name + ".json")))
 
 
 @pytest.mark.parametrize("name,words,tol", [("c1_fp64_seed3", 1, 1e-9), ("m2L2_fp64_seed4", 1, 1e-9),
                                             ("c1_mp256_seed3", 1, 1e-9), ("c1_mp256_seed3", 2, 1e-24),
-                                            ("rank2_mp256_seed5", 2, 1e-24)])
+                                            ("rank2_mp256_seed5", 2, 1e-24), ("c1_mp256_seed3", 4, 1e-45),
+                                            ("rank2_mp256_seed5", 4, 1e-45)])
 def test_full_run_matches_golden(pk, name, words, tol):
     """solverank1sdp on the GPU reproduces the golden iteration log (mu, alpha_p, alpha_d, beta)."""
     import mpmath

@@ -94,3 +94,59 @@ def test_bench_algorithmic_counts():
     d, K, D = 8, 15, 15
     assert fl == 2 * (4.0 * d * K * (d + K) + 8.0 * D * (D + 1) / 2)
     assert by == 2 * 8 * (2 * d * d + d * K + K + D * (D + 1) / 2 + K)
+
+
+MW_PROBE = r"""
+#include "mwfloat.h"
+#include <cstdio>
+#include <cstdlib>
+using namespace mw;
+template <class T> T rnd(unsigned& s) {
+  T v = T(0.0); double sc = 1.0;
+  for (int q = 0; q < Num<T>::W; ++q) {
+    s = s * 1664525u + 1013904223u;
+    v += T(((double)(s >> 8) / 16777216.0 - 0.5) * sc); sc *= 1e-16;
+  }
+  return v;
+}
+template <class T> void pr(const T& v) {
+  const double* d = reinterpret_cast<const double*>(&v);
+  for (int q = 0; q < Num<T>::W; ++q) printf(" %a", d[q]);
+}
+template <class T> void run(unsigned s) {
+  for (int t = 0; t < 40; ++t) {
+    T a = rnd<T>(s), b = rnd<T>(s);
+    T acc = a; for (int k = 0; k < 5; ++k) acc += b;   // loop-carried sums
+    T r[7] = {a + b, a - b, a * b, a / b, Num<T>::sqrt_(a * a), a * T(-3.0), acc};
+    pr(a); pr(b); for (auto& v : r) pr(v); printf("\n");
+  }
+}
+int main() { run<dd>(7u); run<qd>(11u); }
+"""
+
+
+def test_multiword_arithmetic_against_mpmath(tmp_path):
+    """dd / qd arithmetic of mwfloat.h (host build of the device code) against 320-bit mpmath:
+    add/sub/mul/div/sqrt within a few units of 2^-104 (dd) and 2^-208 (qd)."""
+    import shutil
+    import subprocess
+    import mpmath
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no host C++ compiler")
+    src = tmp_path / "mw.cpp"
+    src.write_text(MW_PROBE)
+    exe = tmp_path / "mw"
+    inc = os.path.join(ROOT, "clustered-low-rank-sdp-solver_amd", "csrc")
+    subprocess.run([cxx, "-x", "c++", "-std=c++17", "-O2", "-D__HIP_PLATFORM_AMD__",
+                    "-I/opt/rocm/include", "-I" + inc, str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    mpmath.mp.prec = 320
+    for words, lines, tol in ((2, out[:40], 2.0 ** -100), (4, out[40:80], 2.0 ** -203)):
+        for ln in lines:
+            v = [mpmath.mpf(float.fromhex(t)) for t in ln.split()]
+            vals = [sum(v[i:i + words]) for i in range(0, len(v), words)]
+            a, b = vals[0], vals[1]
+            exp = [a + b, a - b, a * b, a / b, abs(a), a * -3, a + 5 * b]
+            for got, e in zip(vals[2:], exp):
+                assert abs(got - e) <= tol * max(abs(e), abs(a), abs(b)), (words, float(got), float(e))
