@@ -29,7 +29,11 @@ CONFIGS = {
     "c3": dict(J=64, delta=128, rank=1, n_y=128),
     "c2": dict(J=16, delta=64, rank=2, n_y=64),
     "c1": dict(J=2, delta=4, rank=1, n_y=4),
+    # config 5 shape (sphere packing): 7 clusters, blocks {2}, {18,16}, {9,8}x3,
+    # {1}x2, dim_S {3,51,17,17,17,1,1}, n_y = 52 -- run with --precision 4 (quad-double)
+    "c5": dict(kind="sphere_packing_shape"),
 }
+DTYPES = {1: "f64", 2: "dd(f64x2)", 4: "qd(f64x4)"}
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X fp64 matrix spec; measured ceiling 72.4 (profiles/r01_f64_mfma_probe.log)
 HBM_PEAK_GBS = 8000.0
 
@@ -66,28 +70,43 @@ def schur_pmc_traffic(config, precision, world):
     return d.get("traffic_bytes_per_iteration"), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(cons, b, bi, budget_s=20.0):
-    """Time the oracle (numpy fp64 restatement of MPMP.jl) on this instance: one loop body."""
+MP_BITS = {2: 106, 4: 212}   # significand bits of dd / qd, for the multi-precision CPU baseline
+MP_BASELINE_MAX_ELEMS = 20000  # mpmath is ~1 us per operation: small instances only (config 5)
+
+
+def cpu_baseline(cons, b, bi, precision=1, budget_s=20.0):
+    """Time the oracle on this instance: the numpy fp64 restatement of MPMP.jl, or for a
+    multi-word run on a small instance (config 5) the mpmath restatement at the significand
+    width of the device words (single-threaded, as mpmath is)."""
     from oracle import mpmp_oracle as O
     try:
         from threadpoolctl import threadpool_info
         cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
     except Exception:
         cores = 1
+    label = "numpy/scipy fp64 restatement (oracle/mpmp_oracle.py), BLAS threads=%d" % cores
     ar = O.Fp64()
+    elems = sum(n * n for bl in bi.Y_blocksizes for n in bl) + sum(d * d for d in bi.dim_S)
+    if precision > 1 and elems <= MP_BASELINE_MAX_ELEMS:
+        ar = O.Mp(MP_BITS[precision])
+        cons = [O.Cluster([[[ar.asarray(v) for v in vk] for vk in Al] for Al in cl.A],
+                          ar.asarray(cl.B), ar.asarray(cl.c),
+                          [[[ar.num(x) for x in hk] for hk in Hl] for Hl in cl.H]) for cl in cons]
+        b = ar.asarray(b)
+        cores = 1
+        label = "mpmath restatement at %d bits (oracle/mpmp_oracle.py), 1 thread" % MP_BITS[precision]
     prm = {k: O._param(ar, v) for k, v in O.DEFAULTS.items()}
     state = O.initial_point(ar, bi, 100.0, 100.0)
     t0 = time.time()
     n = 0
     while True:
-        state, _ = O.iteration(ar, cons, bi, b, None, 0.0, state, False, prm)
+        state, _ = O.iteration(ar, cons, bi, b, None, ar.num(0), state, False, prm)
         n += 1
         if time.time() - t0 > budget_s * 0.5 or n >= 3:
             break
     dt = time.time() - t0
     return {"value": n / dt, "unit": "iterations/s", "cores": int(cores), "kind": "port",
-            "sample": f"{n} loop bodies of the same instance from the initial point, numpy/scipy "
-                      f"fp64 restatement (oracle/mpmp_oracle.py), BLAS threads={cores}"}
+            "sample": f"{n} loop bodies of the same instance from the initial point, {label}"}
 
 
 def main():
@@ -109,7 +128,10 @@ def main():
     from clrsdp_amd import _lib
 
     cfg = CONFIGS[args.config]
-    cons, b = pk.synth(seed=args.seed, **cfg)
+    if cfg.get("kind") == "sphere_packing_shape":
+        cons, b = pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, seed=args.seed)
+    else:
+        cons, b = pk.synth(seed=args.seed, **cfg)
     bi = pk.get_block_info(cons)
     parts = pk.partition_clusters(bi, world)
     owned = parts[rank] if world > 1 else None
@@ -182,10 +204,13 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f64" if args.precision == 1 else "dd(f64x2)",
+        "dtype": DTYPES[args.precision],
         "data": "synthetic (seeded splitmix64 instance, SURVEY.md §8d)",
-        "config": {"workload": f"{args.config}: J={cfg['J']} clusters, {cfg['delta']}x{cfg['delta']} blocks, "
-                               f"rank {cfg['rank']}, N={2 * cfg['delta'] - 1} samples, n_y={cfg['n_y']}",
+        "config": {"workload": (f"{args.config}: J={cfg['J']} clusters, {cfg['delta']}x{cfg['delta']} blocks, "
+                                f"rank {cfg['rank']}, N={2 * cfg['delta'] - 1} samples, n_y={cfg['n_y']}")
+                               if "J" in cfg else
+                               f"{args.config}: sphere-packing shape, J={bi.J} clusters, blocks "
+                               f"{bi.Y_blocksizes}, dim_S {bi.dim_S}, n_y={bi.n_y}",
                    "parallelism": f"clusters sharded over {world} GPU(s)" if world > 1 else "1 GPU"},
         "roofline": {"bound": "mfma", "kernel": "Schur assembly (stage SCHUR)",
                      "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -198,7 +223,7 @@ def main():
         "graph_replay": world == 1,
     }
     if world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(cons, b, bi)
+        res["cpu_baseline"] = cpu_baseline(cons, b, bi, args.precision)
     print(json.dumps(res))
     if dist is not None:
         dist.close()

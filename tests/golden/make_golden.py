@@ -32,8 +32,16 @@ def to_mp(ar, cons):
                        [[[ar.num(x) for x in hk] for hk in Hl] for Hl in cl.H]) for cl in cons]
 
 
+def make_instance(inst):
+    """synth(**inst), or synth_mixed for inst["kind"] == "sphere_packing_shape" (config 5)."""
+    inst = dict(inst)
+    if inst.pop("kind", None) == "sphere_packing_shape":
+        return pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, **inst)
+    return pk.synth(**inst)
+
+
 def run(name, inst, iters, prec=None, tol=1e-9):
-    cons, b = pk.synth(**inst)
+    cons, b = make_instance(inst)
     bi = O.get_block_info(cons)
     if prec:
         ar = O.Mp(prec)
@@ -59,7 +67,11 @@ def run(name, inst, iters, prec=None, tol=1e-9):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "sp":  # only the config-5-shape vector (~40 s)
+        run("sp_mp256_seed1", dict(kind="sphere_packing_shape", seed=1), 12, prec=256)
+        sys.exit(0)
     run("c1_fp64_seed3", dict(J=2, delta=4, rank=1, n_y=4, seed=3), 10)
     run("m2L2_fp64_seed4", dict(J=2, delta=3, rank=1, n_y=3, m=2, L=2, seed=4), 10)
     run("c1_mp256_seed3", dict(J=2, delta=4, rank=1, n_y=4, seed=3), 10, prec=256)
     run("rank2_mp256_seed5", dict(J=2, delta=3, rank=2, n_y=3, seed=5), 8, prec=256)
+    run("sp_mp256_seed1", dict(kind="sphere_packing_shape", seed=1), 12, prec=256)

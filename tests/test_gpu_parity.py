@@ -142,6 +142,17 @@ def test_stage_parity_qd_vs_256bit(pk, oracle):
     _stage_compare(pk, oracle, consm, ar.asarray(b), words=4, ar=ar, tol=1e-50)
 
 
+def test_stage_parity_sphere_packing_shape_qd(pk, oracle):
+    """Config 5 (sphere-packing shape: blocks 1..18, dim_S up to 51, n_y = 52) at quad-double
+    against the 256-bit oracle."""
+    cons, b = pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, seed=1)
+    ar = oracle.Mp(256)
+    consm = [pk.Cluster([[[ar.asarray(v) for v in vk] for vk in Al] for Al in cl.A],
+                        ar.asarray(cl.B), ar.asarray(cl.c),
+                        [[[ar.num(x) for x in hk] for hk in Hl] for Hl in cl.H]) for cl in cons]
+    _stage_compare(pk, oracle, consm, ar.asarray(b), iters_before=3, words=4, ar=ar, tol=1e-45)
+
+
 def _golden(name):
     return json.load(open(os.path.join(GOLDEN, name + ".json")))
 
@@ -149,13 +160,18 @@ def _golden(name):
 @pytest.mark.parametrize("name,words,tol", [("c1_fp64_seed3", 1, 1e-9), ("m2L2_fp64_seed4", 1, 1e-9),
                                             ("c1_mp256_seed3", 1, 1e-9), ("c1_mp256_seed3", 2, 1e-24),
                                             ("rank2_mp256_seed5", 2, 1e-24), ("c1_mp256_seed3", 4, 1e-45),
-                                            ("rank2_mp256_seed5", 4, 1e-45)])
+                                            ("rank2_mp256_seed5", 4, 1e-45), ("sp_mp256_seed1", 1, 1e-8),
+                                            ("sp_mp256_seed1", 2, 1e-22), ("sp_mp256_seed1", 4, 1e-40)])
 def test_full_run_matches_golden(pk, name, words, tol):
     """solverank1sdp on the GPU reproduces the golden iteration log (mu, alpha_p, alpha_d, beta)."""
     import mpmath
     mpmath.mp.prec = 256
     g = _golden(name)
-    cons, b = pk.synth(**g["instance"])
+    inst = dict(g["instance"])
+    if inst.pop("kind", None) == "sphere_packing_shape":   # config 5 shape (synth_mixed)
+        cons, b = pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, **inst)
+    else:
+        cons, b = pk.synth(**inst)
     bi = pk.get_block_info(cons)
     res = pk.solverank1sdp(cons, b, bi, maxiterations=g["iterations"] + 1, precision_words=words,
                            verbose=False, return_info=True, record_exact=True, **g["params"])
