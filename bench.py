@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--precision", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--clusters", type=int, default=0,
+                    help="override J of the config (per-rank sizing experiments; not a bench line)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,7 +129,9 @@ def main():
     pk = _clrsdp_pkg.load()
     from clrsdp_amd import _lib
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.clusters:
+        cfg["J"] = args.clusters
     if cfg.get("kind") == "sphere_packing_shape":
         cons, b = pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, seed=args.seed)
     else:

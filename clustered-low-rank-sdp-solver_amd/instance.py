@@ -164,12 +164,31 @@ def to_planes(values, words: int) -> np.ndarray:
     import mpmath
     out = np.zeros((words, vals.size))
     for i, v in enumerate(vals):
-        r = mpmath.mpf(v)
+        # exact remainders (independent of mpmath.mp.prec): limb w is the nearest double of
+        # what the previous limbs leave over
+        if isinstance(v, mpmath.mpf):
+            r = v
+        else:  # strings, lazy constants (mpmath.pi): convert well beyond 4 limbs
+            with mpmath.workprec(1024):
+                r = mpmath.mpf(v)
         for w in range(words):
             h = float(r)
             out[w, i] = h
-            r = r - h
+            r = mpmath.fsub(r, h, exact=True)
     return out.reshape(-1)
+
+
+def from_planes(planes: np.ndarray, n: int, words: int) -> np.ndarray:
+    """Inverse of :func:`to_planes`: the exact sums of the limbs as ``mpmath.mpf``."""
+    import mpmath
+    P = np.asarray(planes).reshape(words, -1)
+    out = np.empty(n, dtype=object)
+    for i in range(n):
+        s = mpmath.mpf(0)
+        for q in range(words):
+            s = mpmath.fadd(s, float(P[q, i]), exact=True)
+        out[i] = s
+    return out
 
 
 @dataclass

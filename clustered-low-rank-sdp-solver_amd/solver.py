@@ -16,7 +16,8 @@ import numpy as np
 
 from . import _lib
 from .blockinfo import BlockInfo
-from .instance import Flat, blocks_to_flat, concat_colmajor, flat_to_blocks, flatten, to_planes
+from .instance import Flat, blocks_to_flat, concat_colmajor, flat_to_blocks, flatten, from_planes, \
+    to_planes
 
 DEFAULTS = dict(beta_infeasible="0.3", beta_feasible="0.1", gamma="0.7", omega_p="1e10",
                 omega_d="1e10", duality_gap_threshold="1e-15", primal_error_threshold="1e-30",
@@ -116,15 +117,7 @@ class DeviceSolver:
     def _from_planes(self, planes: np.ndarray, n: int, exact=False):
         if self.w == 1 or not exact:
             return planes[:n].copy()
-        import mpmath
-        out = np.empty(n, dtype=object)
-        P = planes.reshape(self.w, n)
-        for i in range(n):
-            s = mpmath.mpf(0)
-            for q in range(self.w):
-                s += mpmath.mpf(P[q, i])
-            out[i] = s
-        return out
+        return from_planes(planes, n, self.w)
 
     # ------------------------------------------------------------------ state
     def set_state(self, x, X, y, Y):

@@ -150,3 +150,22 @@ def test_multiword_arithmetic_against_mpmath(tmp_path):
             exp = [a + b, a - b, a * b, a / b, abs(a), a * -3, a + 5 * b]
             for got, e in zip(vals[2:], exp):
                 assert abs(got - e) <= tol * max(abs(e), abs(a), abs(b)), (words, float(got), float(e))
+
+
+def test_planar_limbs_exact_at_default_mpmath_precision(pk):
+    """to_planes/from_planes must not depend on the global mpmath precision (prepareabc output
+    carries its own 512-bit values; a 53-bit remainder would silently drop limbs 3 and 4)."""
+    import mpmath
+    from clrsdp_amd.instance import from_planes, to_planes
+    old = mpmath.mp.prec
+    try:
+        with mpmath.workprec(512):
+            v = np.array([mpmath.sqrt(2) / 3, -mpmath.mpf(1) / 7, mpmath.exp(40)], dtype=object)
+        mpmath.mp.prec = 53
+        back = from_planes(to_planes(v, 4), 3, 4)
+        with mpmath.workprec(512):
+            err = max(abs(a - b) / abs(a) for a, b in zip(v, back))
+        assert err < mpmath.mpf(2) ** -205
+        assert float(to_planes(np.array([mpmath.pi], dtype=object), 4)[3]) != 0.0
+    finally:
+        mpmath.mp.prec = old
