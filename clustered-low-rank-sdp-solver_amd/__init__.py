@@ -11,6 +11,8 @@ from .poly import Poly, create_sample_points, create_sample_points_1d, create_sa
     create_sample_points_3d, create_sample_points_chebyshev, create_sample_points_chebyshev_mod, \
     gegenbauer_basis, jacobi_basis, laguerrebasis, make_monomial_basis, points_X_general
 from .prep import prepareabc, solvempmp
+from .sdpfiles import read_files, write_files
+from .sphere_packing import Nsphere_packing_2point, test_bound_sphere_packing
 from . import _lib
 
 __all__ = ["BlockInfo", "block_info", "get_block_info", "distribute_weights_swapping",
@@ -18,4 +20,5 @@ __all__ = ["BlockInfo", "block_info", "get_block_info", "distribute_weights_swap
            "make_params", "solverank1sdp", "prepareabc", "solvempmp", "Poly", "laguerrebasis",
            "jacobi_basis", "gegenbauer_basis", "make_monomial_basis", "create_sample_points",
            "create_sample_points_1d", "create_sample_points_2d", "create_sample_points_3d",
-           "create_sample_points_chebyshev", "create_sample_points_chebyshev_mod", "points_X_general"]
+           "create_sample_points_chebyshev", "create_sample_points_chebyshev_mod", "points_X_general", "write_files", "read_files",
+           "Nsphere_packing_2point", "test_bound_sphere_packing"]

@@ -97,7 +97,8 @@ def sphere_packing_program(n: int, d: int, r: Sequence, N: int = 2):
     return M, G, q, sample_points, delta, b
 
 
-def sphere_packing_constraints(n: int = 3, d: int = 8, r=None, N: int = 2, prec: int = 512):
+def sphere_packing_constraints(n: int = 3, d: int = 8, r=None, N: int = 2, prec: int = 512,
+                               reorder: bool = True):
     """Sampled constraints and BlockInfo of SP.jl:88-105 (with the N = 2 reordering)."""
     with mpmath.workprec(prec):
         if r is None:
@@ -105,20 +106,28 @@ def sphere_packing_constraints(n: int = 3, d: int = 8, r=None, N: int = 2, prec:
         r = [mpf(v) for v in r]
         M, G, q, pts, delta, b = sphere_packing_program(n, d, r, N)
         cons = [prepareabc(M[j], G[j], q, pts[j], delta[j]) for j in range(len(G))]
-        if len(M) == 7:
+        if reorder and len(M) == 7:
             cons = [cons[i - 1] for i in (3, 6, 5, 7, 4, 1, 2)]
         bi = get_block_info(cons)
     return cons, b, bi
 
 
-def Nsphere_packing_2point(n: int, d: int, r=None, N: int = 2, omega=100, prec: int = 512,
-                           **kwargs):
+def Nsphere_packing_2point(n: int, d: int, r=None, N: int = 2, file_path: str = "",
+                           write_only: bool = False, omega=100, prec: int = 512, **kwargs):
     """Build and solve the N-radii two-point program (SP.jl:29-110) on the device.
 
-    ``kwargs`` go to :func:`solver.solverank1sdp` (``precision_words=4`` runs quad-double).
-    Returns the 11-tuple of ``solverank1sdp`` (plus RunInfo with ``return_info``).
+    ``file_path``: also write the sampled instance there (:func:`sdpfiles.write_files`, before
+    the reordering, as SP.jl:95-98); ``write_only`` returns True after writing.  ``kwargs`` go to
+    :func:`solver.solverank1sdp` (``precision_words=4`` runs quad-double).  Returns the 11-tuple
+    of ``solverank1sdp`` (plus RunInfo with ``return_info``).
     """
     from .solver import solverank1sdp
+    if file_path:
+        from .sdpfiles import write_files
+        c0, b0_, bi0 = sphere_packing_constraints(n, d, r, N, prec, reorder=False)
+        write_files(file_path, c0, bi0, b0_)
+        if write_only:
+            return True
     cons, b, bi = sphere_packing_constraints(n, d, r, N, prec)
     return solverank1sdp(cons, b, bi, omega_p=omega, omega_d=omega, **kwargs)
 

@@ -35,12 +35,17 @@ def to_mp(ar, cons):
 def make_instance(inst):
     """synth(**inst), or synth_mixed for inst["kind"] == "sphere_packing_shape" (config 5)."""
     inst = dict(inst)
+    if inst.get("kind") == "sphere_packing":
+        # the real SpherePacking.jl instance (SP.jl:29-105), sampled at 512 bits by prepareabc
+        from clrsdp_amd import sphere_packing as S
+        cons, b, _ = S.sphere_packing_constraints(inst["n"], inst["d"], prec=inst.get("prep_bits", 512))
+        return cons, b
     if inst.pop("kind", None) == "sphere_packing_shape":
         return pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, **inst)
     return pk.synth(**inst)
 
 
-def run(name, inst, iters, prec=None, tol=1e-9):
+def run(name, inst, iters, prec=None, tol=1e-9, params=None):
     cons, b = make_instance(inst)
     bi = O.get_block_info(cons)
     if prec:
@@ -50,11 +55,12 @@ def run(name, inst, iters, prec=None, tol=1e-9):
     else:
         ar = O.Fp64()
         consr, br = cons, b
-    res = O.solverank1sdp(consr, br, bi, ar=ar, maxiterations=iters + 1, **PARAMS)
+    params = params or PARAMS
+    res = O.solverank1sdp(consr, br, bi, ar=ar, maxiterations=iters + 1, **params)
     fmt = (lambda v: mpmath.nstr(v, 70)) if prec else (lambda v: repr(float(v)))
     out = {
         "generator": "tests/golden/make_golden.py (oracle/mpmp_oracle.py, %s)" % ar.name,
-        "instance": inst, "params": PARAMS, "iterations": iters, "tolerance_fp64": tol,
+        "instance": inst, "params": params, "iterations": iters, "tolerance_fp64": tol,
         "log": [{k: fmt(getattr(r, k)) for k in ("mu", "p_obj", "d_obj", "gap", "P_err", "p_err",
                                                   "d_err", "alpha_p", "alpha_d", "beta")}
                 for r in res.log],
@@ -67,6 +73,10 @@ def run(name, inst, iters, prec=None, tol=1e-9):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "sp_real":  # real sphere-packing instance (~15 min)
+        run("sp_real_d8_mp256", dict(kind="sphere_packing", n=3, d=8), 40, prec=256,
+            params=dict(omega_p=100.0, omega_d=100.0, duality_gap_threshold=1e-30))
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "sp":  # only the config-5-shape vector (~40 s)
         run("sp_mp256_seed1", dict(kind="sphere_packing_shape", seed=1), 12, prec=256)
         sys.exit(0)

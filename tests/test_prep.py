@@ -160,3 +160,31 @@ def test_sphere_packing_program_shape(pk):
         want = [-v1, -mpmath.sqrt(v1 * v2), -v2]
         assert all(abs(cons[5].c[t] - want[t]) < mpf(10) ** -70 for t in range(3))
         assert abs(S.spherevolume(3, 1) - 4 * mpmath.pi / 3) < mpf(10) ** -70
+
+
+def test_write_read_files_round_trip_exact(pk, tmp_path):
+    from clrsdp_amd import sdpfiles
+    from clrsdp_amd import sphere_packing as S
+    # multi-precision data (the real sphere-packing instance, 512-bit prepareabc output)
+    cons, b, bi = S.sphere_packing_constraints(3, 4, prec=512, reorder=False)
+    sdpfiles.write_files(str(tmp_path / "sp"), cons, bi, b)
+    c2, b2, bi2 = sdpfiles.read_files(str(tmp_path / "sp"))
+    assert bi2.Y_blocksizes == bi.Y_blocksizes and bi2.dim_S == bi.dim_S and bi2.ranks == bi.ranks
+    assert list(b2) == list(b)
+    for c1, cc in zip(cons, c2):
+        assert all(x == y for x, y in zip(c1.c, cc.c))
+        assert all(x == y for x, y in zip(np.asarray(c1.B).ravel(), np.asarray(cc.B).ravel()))
+        for Al1, Al2 in zip(c1.A, cc.A):
+            for Ak1, Ak2 in zip(Al1, Al2):
+                assert all((v1 == v2).all() for v1, v2 in zip(Ak1, Ak2))
+        assert c1.H == cc.H
+    # float data
+    cons, b = pk.synth(J=2, delta=3, rank=2, n_y=3, seed=2, m=2, L=2)
+    bi = pk.get_block_info(cons)
+    sdpfiles.write_files(str(tmp_path / "f"), cons, bi, b)
+    c2, b2, bi2 = sdpfiles.read_files(str(tmp_path / "f"), exact=False)
+    assert np.array_equal(b2, b) and all(np.array_equal(x.B, y.B) for x, y in zip(cons, c2))
+    assert all(np.array_equal(np.stack(x.A[1][2]), np.stack(y.A[1][2])) for x, y in zip(cons, c2))
+    # the driver's write_only path (SP.jl:95-98, 107)
+    assert S.Nsphere_packing_2point(3, 2, file_path=str(tmp_path / "w"), write_only=True) is True
+    assert sdpfiles.read_files(str(tmp_path / "w"))[2].J == 7
