@@ -270,3 +270,52 @@ def test_c3_full_size_newton_identities(pk, oracle):
     for j in range(0, bi.J, 7):
         assert rel_err(dX[j][0], WA[j][0] + Pm[j][0]) < 1e-12
     dev.close()
+
+
+def _sp_real_deviation(pk, words):
+    """Per-iteration relative deviation of the GPU run on the real sphere-packing instance
+    (prepareabc at 512 bits, SP.jl:29-105) from the 256-bit oracle log."""
+    import mpmath
+    from clrsdp_amd import sphere_packing as S
+    g = _golden("sp_real_d8_mp256")
+    inst = g["instance"]
+    cons, b, bi = S.sphere_packing_constraints(inst["n"], inst["d"], prec=512)
+    res = pk.solverank1sdp(cons, b, bi, maxiterations=g["iterations"] + 1, precision_words=words,
+                           verbose=False, return_info=True, record_exact=True, **g["params"])
+    info = res[-1]
+    dev = []
+    with mpmath.workprec(256):
+        for sc, ref in zip(info.exact, g["log"]):
+            dev.append(max(abs(mpmath.mpf(sc[s]) - mpmath.mpf(ref[k])) / max(1, abs(mpmath.mpf(ref[k])))
+                           for k, s in (("mu", "mu"), ("alpha_p", "alpha_p"),
+                                        ("alpha_d", "alpha_d"), ("beta", "beta_c"))))
+    return dev, len(g["log"])
+
+
+def test_sphere_packing_real_instance_qd_matches_256bit_log(pk):
+    """Config 5 with the real constraint data at quad-double against the 256-bit oracle log.
+    The instance is ill-conditioned (cond S_j ~ 1e23 at the start, Q worse, growing as mu -> 0):
+    the 212-bit mpmath oracle itself deviates from the 256-bit log by 1.9e-31 / 4.3e-30 / 5.9e-30
+    at iterations 1-3 (measured), so qd (~212 bits) is held to the same class: 1e-29 through
+    iteration 12, 1e-17 through 25, 1e-13 through 30.  The reference runs it at 512 bits
+    (SP.jl:30-31)."""
+    dev, n = _sp_real_deviation(pk, 4)
+    print("deviation per iteration:", " ".join("%.1e" % float(d) for d in dev))
+    assert len(dev) >= 30
+    assert max(dev[:12]) < 1e-29, dev[:12]
+    assert max(dev[:25]) < 1e-17, dev[:25]
+    assert max(dev[:30]) < 1e-13, dev[:30]
+
+
+def test_sphere_packing_bound_qd(pk):
+    """Application anchor: the two-point bound for radii {1, sqrt2 - 1} in R^3 at d = 8.  The
+    reference's example quotes de Laat et al.'s 0.813 and the NaCl density 0.793 (SP.jl:124-127);
+    the 256-bit oracle run on the same samples reaches -0.81500746 (tests/golden)."""
+    from clrsdp_amd import sphere_packing as S
+    res = S.Nsphere_packing_2point(3, 8, precision_words=4, duality_gap_threshold=1e-6,
+                                   primal_error_threshold=1e-15, dual_error_threshold=1e-8,
+                                   verbose=False, return_info=True)
+    assert res[-1].status == "terminated"
+    bound = -res[9]
+    assert S.NACL_DENSITY < bound < 0.82
+    assert abs(bound - 0.8150074605) < 3e-6
