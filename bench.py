@@ -118,6 +118,10 @@ def main():
     ap.add_argument("--precision", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--loop", choices=["auto", "sync", "pipelined"], default="auto",
+                    help="host loop: wait for every loop body (sync; hipGraph replay, faster at one "
+                         "GPU: 1.13-1.15 vs 1.15-1.17 ms measured) or stay one body behind "
+                         "(pipelined; auto = pipelined when the clusters are sharded)")
     ap.add_argument("--clusters", type=int, default=0,
                     help="override J of the config (per-rank sizing experiments; not a bench line)")
     args = ap.parse_args()
@@ -149,15 +153,41 @@ def main():
     if dist is not None:
         dist.attach(dev)
     prm = pk.make_params("0.3", "0.1", "0.7", 0)
+    from clrsdp_amd.solver import make_control
+    # the reference's default thresholds (MPMP.jl:607-609); loop control on the device
+    dev.set_control(make_control("1e-15", "1e-30", "1e-30"))
     x0, X0, y0, Y0 = pk.initial_point(bi, 100.0, 100.0)
     dev.set_state(x0, X0, y0, Y0)
     dev.initial_residuals(prm)
 
-    def step(pd_feas=False):
+    def step(pd_feas=False):   # synchronous loop body (instrumented pass)
         return dev.iterate(prm, pd_feas)
 
-    for _ in range(args.warmup):
-        step()
+    pipelined = args.loop == "pipelined" or (args.loop == "auto" and world > 1)
+
+    def run_bodies(n):
+        """n loop bodies as solverank1sdp runs them: the host one body behind the device
+        (clrsdp_iterate_async / _wait), every log row read back."""
+        if not pipelined:
+            for _ in range(n):
+                step()
+            return
+        inflight = 0
+        for _ in range(n):
+            dev.iterate_async(prm)
+            inflight += 1
+            if inflight == 2:
+                _, ran = dev.iterate_wait()
+                inflight -= 1
+                if not ran:
+                    raise RuntimeError("solver terminated inside the benchmark window")
+        while inflight:
+            _, ran = dev.iterate_wait()
+            inflight -= 1
+            if not ran:
+                raise RuntimeError("solver terminated inside the benchmark window")
+
+    run_bodies(args.warmup)
 
     def barrier_sync():
         dev.synchronize()
@@ -166,8 +196,7 @@ def main():
 
     barrier_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_bodies(args.steps)
     barrier_sync()
     dt = time.perf_counter() - t0
     # instrumented pass (per-stage HIP events, no graph replay) for the phase breakdown and the
@@ -225,6 +254,8 @@ def main():
                      "schur_alg_gbs": by / sch_s / 1e9},
         "phase_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.STAGE_NAMES, phase)},
         "graph_replay": world == 1,
+        "host_loop": "pipelined (host one loop body behind, device-side pd_feas/terminate)"
+                     if pipelined else "synchronous (one hipGraph replay per loop body)",
     }
     if world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(cons, b, bi, args.precision)

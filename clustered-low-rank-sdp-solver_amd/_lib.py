@@ -24,13 +24,14 @@ STAGE_NAMES = ["mu_R", "Xinv", "schur", "factor", "residuals", "predictor", "cor
  BUF_DXMAT, BUF_DY, BUF_DYMAT, BUF_XVEC, BUF_YVEC, BUF_SCALARS) = range(17)
 
 SC = dict(mu=0, mu_p=1, r=2, beta=3, beta_c=4, mu_c=5, alpha_p=6, alpha_d=7, mineig_X=8,
-          mineig_Y=9, p_obj=10, d_obj=11, err_P=12, err_p=13, err_d=14, dot_XY=15, dot_XdY=16)
+          mineig_Y=9, p_obj=10, d_obj=11, err_P=12, err_p=13, err_d=14, dot_XY=15, dot_XdY=16,
+          pd_feas=24, halt=25, gap=26)
 
 EXPORTS = ["clrsdp_version", "clrsdp_last_error", "clrsdp_create", "clrsdp_upload_constraints",
            "clrsdp_set_state", "clrsdp_get_state", "clrsdp_initial_residuals", "clrsdp_iterate",
            "clrsdp_run_stage", "clrsdp_get_buffer", "clrsdp_exchange_bytes", "clrsdp_set_exchange",
            "clrsdp_set_stream", "clrsdp_get_stream", "clrsdp_synchronize", "clrsdp_set_timing",
-           "clrsdp_destroy"]
+           "clrsdp_destroy", "clrsdp_set_control", "clrsdp_iterate_async", "clrsdp_iterate_wait"]
 
 P_i64 = C.POINTER(C.c_int64)
 P_i32 = C.POINTER(C.c_int32)
@@ -51,6 +52,12 @@ class Config(C.Structure):
 class Params(C.Structure):
     _fields_ = [("beta_infeasible", C.c_double * 4), ("beta_feasible", C.c_double * 4),
                 ("gamma", C.c_double * 4), ("b0", C.c_double * 4)]
+
+
+class Control(C.Structure):
+    _fields_ = [("duality_gap_threshold", C.c_double * 4), ("primal_error_threshold", C.c_double * 4),
+                ("dual_error_threshold", C.c_double * 4), ("need_primal_feasible", C.c_int32),
+                ("need_dual_feasible", C.c_int32)]
 
 
 class IterStats(C.Structure):
@@ -94,6 +101,9 @@ def lib():
     L.clrsdp_synchronize.argtypes = [C.c_void_p]
     L.clrsdp_set_timing.argtypes = [C.c_void_p, C.c_int32]
     L.clrsdp_destroy.argtypes = [C.c_void_p]
+    L.clrsdp_set_control.argtypes = [C.c_void_p, C.POINTER(Control)]
+    L.clrsdp_iterate_async.argtypes = [C.c_void_p, C.POINTER(Params)]
+    L.clrsdp_iterate_wait.argtypes = [C.c_void_p, C.POINTER(IterStats), P_i32]
     for name in EXPORTS:
         if name not in ("clrsdp_last_error", "clrsdp_get_stream"):
             getattr(L, name).restype = C.c_int32

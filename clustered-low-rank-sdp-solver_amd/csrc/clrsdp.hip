@@ -281,6 +281,9 @@ struct HandleBase {
   virtual void get_state(double* x, double* X, double* y, double* Y) = 0;
   virtual int initial(const clrsdp_params* prm, clrsdp_iter_stats* st) = 0;
   virtual int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) = 0;
+  virtual void set_control(const clrsdp_control* c) = 0;
+  virtual int iterate_async(const clrsdp_params* prm) = 0;
+  virtual int iterate_wait(clrsdp_iter_stats* st, int* ran) = 0;
   virtual int run_stage(int stage, const clrsdp_params* prm, int pd_feas) = 0;
   virtual void get_buffer(int buf, double* host, int64_t* count) = 0;
   virtual int64_t exchange_bytes() const = 0;
@@ -327,7 +330,12 @@ struct Solver final : HandleBase {
   clrsdp_exchange_fn xfn = nullptr;
   void* xctx = nullptr;
   bool uploaded = false;
-  int info_count = 0, info_S0 = 0, info_Q0 = 0, info_Y0 = 0;
+  int info_count = 0, info_S0 = 0, info_Q0 = 0, info_Y0 = 0, info_H = 0;
+  // pipelined loop (iterate_async / iterate_wait): device-side loop control and results copy
+  T gap_thr{}, p_thr{}, d_thr{};
+  int need_p = 0, need_d = 0;
+  T *Pres = nullptr, *pres = nullptr, *dres = nullptr;  // P, p, d of the last loop body that ran
+  bool res_from_copy = false;
 
   // ---------------- plans
   GemmPlan<T> p_XY, p_dXdY, p_xinv, p_s1x, p_s1y, p_s2x, p_s2y, p_Q, p_wA_P, p_wA_dX, p_trU_Z,
@@ -477,15 +485,17 @@ struct Solver final : HandleBase {
     // device memory is released with the process / hipDeviceReset; free what we own explicitly
     T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, BX, BY, AY,
                  tval, S, Wm, Bm, Qslab, Q, Qf, Qinv, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
-                 bvec, dyv, pvec, uvec, bpart, eigX, tmpsc, tC, Stmp, own_send, Vt};
+                 bvec, dyv, pvec, uvec, bpart, eigX, tmpsc, tC, Stmp, own_send, Vt, Pres, pres, dres};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
     (void)hipFree(ksamp);
     (void)hipFree(rsums);
     if (stat_dev) (void)hipFree(stat_dev);
     if (stat_host) (void)hipHostFree(stat_host);
+    for (char* r : ring_host)
+      if (r) (void)hipHostFree(r);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_s, ev_r, ev_qa, ev_q})
+    for (hipEvent_t e : {ev_s, ev_r, ev_qa, ev_q, ring_ev[0], ring_ev[1]})
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
       if (g) (void)hipGraphExecDestroy(g);
@@ -512,6 +522,8 @@ struct Solver final : HandleBase {
     rhs = dmalloc<T>(nx); tvec = dmalloc<T>(nx); tmpv = dmalloc<T>(nx);
     pslab = dmalloc<T>((size_t)std::max(nc(), 1) * n_y);
     y = dmalloc<T>(n_y); bvec = dmalloc<T>(n_y); dyv = dmalloc<T>(n_y); pvec = dmalloc<T>(n_y);
+    Pres = dmalloc<T>(std::max<int64_t>(nblk_el, 1)); pres = dmalloc<T>(std::max<int64_t>(n_y, 1));
+    dres = dmalloc<T>(std::max<int64_t>(nx, 1));
     uvec = dmalloc<T>(n_y);
     // sc and the status words share one allocation (one D2H copy per iteration, pinned host
     // mirror) -- see stat_alloc()
@@ -530,7 +542,8 @@ struct Solver final : HandleBase {
     rsums = dmalloc<int>(nRS);
     if (fast_schur) Vt = dmalloc<T>(std::max<int64_t>(nV, 1));
     // info layout: [X: nb][Y: nb][S: nc single + nc2 second blocks][Q: 1]
-    info_count = 2 * nb() + nc() + nc2 + 1;
+    info_count = 2 * nb() + nc() + nc2 + 1 + 1;   // + the halt word (last; not zeroed)
+    info_H = info_count - 1;
     info_Y0 = nb();
     info_S0 = 2 * nb();
     info_Q0 = 2 * nb() + nc() + nc2;
@@ -924,6 +937,10 @@ struct Solver final : HandleBase {
             int64_t n) {
     if (n > 0) vec_lin<T><<<cdiv(n, 256), 256, 0, stream>>>(out, a_, ca, b_, cb, c_, cc, n);
   }
+  void copy_guarded(T* dst, const T* src, int64_t n) {
+    if (n > 0)
+      vec_copy_guard<T><<<std::min<unsigned>(cdiv(n, 256), 2048), 256, 0, stream>>>(dst, src, n, info + info_H);
+  }
   void fill(T* out, double v, int64_t n) {
     if (n > 0) vec_fill<T><<<cdiv(n, 256), 256, 0, stream>>>(out, v, n);
   }
@@ -934,20 +951,32 @@ struct Solver final : HandleBase {
       blk_sym2<T><<<dim3(nb(), 32), 128, 0, stream>>>(d_blk, out, Zm, mode);
     }
   }
+  static T limbs(const double* l) {
+    T v = T(l[0]);
+    for (int i = 1; i < Num<T>::W && i < 4; ++i) v += T(l[i]);
+    return v;
+  }
   ScalarParams<T> sparams(const clrsdp_params* prm, int pd_feas) {
-    ScalarParams<T> p;
-    auto lim = [](const double* l) {
-      T v = T(l[0]);
-      for (int i = 1; i < Num<T>::W && i < 4; ++i) v += T(l[i]);
-      return v;
-    };
-    p.beta_inf = lim(prm->beta_infeasible);
-    p.beta_feas = lim(prm->beta_feasible);
-    p.gamma = lim(prm->gamma);
-    p.b0 = lim(prm->b0);
+    ScalarParams<T> p{};
+    p.beta_inf = limbs(prm->beta_infeasible);
+    p.beta_feas = limbs(prm->beta_feasible);
+    p.gamma = limbs(prm->gamma);
+    p.b0 = limbs(prm->b0);
+    p.gap_thr = gap_thr;
+    p.p_thr = p_thr;
+    p.d_thr = d_thr;
+    p.need_p = need_p;
+    p.need_d = need_d;
     p.dim = dimtot;
     p.pd_feas = pd_feas;
     return p;
+  }
+  void set_control(const clrsdp_control* c) override {
+    gap_thr = limbs(c->duality_gap_threshold);
+    p_thr = limbs(c->primal_error_threshold);
+    d_thr = limbs(c->dual_error_threshold);
+    need_p = c->need_primal_feasible != 0;
+    need_d = c->need_dual_feasible != 0;
   }
   bool zero_cy = false, zero_info = false;
   // ---- scalar slots + status words: one device block, one pinned host mirror
@@ -970,8 +999,9 @@ struct Solver final : HandleBase {
   void scalars(const clrsdp_params* prm, int pd_feas, int which) {
     ScalarParams<T> p = prm ? sparams(prm, pd_feas) : ScalarParams<T>{};
     p.zero_cy = zero_cy ? 1 : 0;
-    p.zero_n = zero_info ? info_count : 0;  // status words of this iteration
+    p.zero_n = zero_info ? info_count - 1 : 0;  // status words of this iteration (not the halt word)
     p.zero_ptr = info;
+    p.halt_ptr = zero_info ? info + info_H : nullptr;  // which == 0 at the start of a loop body
     zero_info = false;
     size_t q = 0;
     while (q < pend.size() || q == 0) {  // at most 6 folded reductions per launch
@@ -1276,7 +1306,7 @@ struct Solver final : HandleBase {
     }
     scalars(prm, pd_feas, 2);
   }
-  void objectives(const clrsdp_params* prm, int pd_feas) {
+  void objectives(const clrsdp_params* prm, int pd_feas, int which = 3) {
     zero_cy = !hasC;
     if (world == 1) {
       if (nx > 0) vec_reduce<T><<<1, 1024, 0, stream>>>(cvec, x, nx, 0, sc + SC_DOT_CX);
@@ -1292,7 +1322,7 @@ struct Solver final : HandleBase {
       reduce_ranks(2, 1, 0, SC_DOT_CY);
     }
     vec_reduce<T><<<1, 1024, 0, stream>>>(bvec, y, n_y, 0, sc + SC_DOT_BY);
-    scalars(prm, pd_feas, 3);
+    scalars(prm, pd_feas, which);
     zero_cy = false;
   }
   void st_update(const clrsdp_params* prm, int pd_feas) {
@@ -1308,7 +1338,7 @@ struct Solver final : HandleBase {
     if (small) {
       const ScalarParams<T> p = sparams(prm, pd_feas);
       update_small<T><<<1, 1024, 0, stream>>>(x, dx, nx, y, dyv, n_y, cvec, bvec, sc, info,
-                                              info_count, p.b0);
+                                              info_count, p);
       return;
     }
     objectives(prm, pd_feas);
@@ -1332,8 +1362,8 @@ struct Solver final : HandleBase {
   }
 
   // both parse the host mirror filled by stat_fetch()
-  int check_info() {
-    const int* h = reinterpret_cast<const int*>(stat_host + stat_info_off);
+  int check_info(const char* blk = nullptr) {
+    const int* h = reinterpret_cast<const int*>((blk ? blk : stat_host) + stat_info_off);
     for (int i = 0; i < nb(); ++i)
       if (h[i]) { err = "X block not positive definite (spd_inv! failed)"; return CLRSDP_E_NOT_PD_X; }
     for (int i = 0; i < nc() + nc2; ++i)
@@ -1344,8 +1374,8 @@ struct Solver final : HandleBase {
     return CLRSDP_OK;
   }
 
-  void read_stats(clrsdp_iter_stats* st) {
-    const T* h = reinterpret_cast<const T*>(stat_host);
+  void read_stats(clrsdp_iter_stats* st, const char* blk = nullptr) {
+    const T* h = reinterpret_cast<const T*>(blk ? blk : stat_host);
     auto f = [&](int i) { return Num<T>::hi(h[i]); };
     st->mu = f(SC_MU);
     st->P_err = f(SC_ERR_PMAT);
@@ -1362,7 +1392,7 @@ struct Solver final : HandleBase {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
     std::memset(st, 0, sizeof(*st));
     st_residuals(false);
-    objectives(prm, 0);
+    objectives(prm, 0, 4);   // + gap / pd_feas / terminate of the initial point (device control)
     stat_fetch();
     read_stats(st);
     return CLRSDP_OK;
@@ -1374,6 +1404,10 @@ struct Solver final : HandleBase {
     auto mark = [&](int s) {
       if (timing) HIPCHK(hipEventRecord(ev[s], stream));
     };
+    // pipelined loop: P, p, d of every body that runs are copied aside (guarded by the halt
+    // word), so a skipped body leaves the residuals of the last iteration that ran, which the
+    // reference returns (MPMP.jl:1014-1024)
+    const bool keep_res = pd_feas < 0;
     for (int s = 0; s <= CLRSDP_STAGE_SCHUR; ++s) {
       mark(s);
       stage(s, prm, pd_feas);
@@ -1384,6 +1418,10 @@ struct Solver final : HandleBase {
     HIPCHK(hipStreamWaitEvent(aux, ev_s, 0));
     stream = aux;
     residuals_local(true);
+    if (keep_res) {
+      copy_guarded(Pres, P, nblk_el);
+      copy_guarded(dres, dvec, nx);
+    }
     HIPCHK(hipEventRecord(ev_r, aux));
     stream = main_s;
     mark(CLRSDP_STAGE_FACTOR);
@@ -1399,6 +1437,7 @@ struct Solver final : HandleBase {
     mark(CLRSDP_STAGE_RESIDUALS);
     HIPCHK(hipStreamWaitEvent(main_s, ev_r, 0));
     residuals_finish();
+    if (keep_res) copy_guarded(pres, pvec, n_y);
     HIPCHK(hipGetLastError());
     for (int s = CLRSDP_STAGE_PREDICTOR; s < CLRSDP_NUM_STAGES; ++s) {
       mark(s);
@@ -1414,11 +1453,14 @@ struct Solver final : HandleBase {
   // One hipGraph per pd_feas value replays the whole loop body with a single launch (one
   // process per GPU with no exchange, and no per-stage timing).  The scalar parameters are
   // baked into the graph, so a change of them re-captures.
-  hipGraphExec_t gexec[2] = {nullptr, nullptr};
-  clrsdp_params gprm[2];
+  // pd_feas 0, 1 and decided on the device (two instances of that one, used alternately, so a
+  // launch never waits for the previous launch of the same executable graph)
+  hipGraphExec_t gexec[4] = {nullptr, nullptr, nullptr, nullptr};
+  clrsdp_params gprm[4];
+  unsigned graph_launches = 0;
   bool use_graph = std::getenv("CLRSDP_NO_GRAPH") == nullptr;
   void launch_graph(const clrsdp_params* prm, int pd_feas) {
-    const int g = pd_feas ? 1 : 0;
+    const int g = pd_feas < 0 ? 2 + (graph_launches++ & 1) : (pd_feas ? 1 : 0);
     if (!gexec[g] || std::memcmp(&gprm[g], prm, sizeof(*prm)) != 0) {
       if (gexec[g]) HIPCHK(hipGraphExecDestroy(gexec[g]));
       gexec[g] = nullptr;
@@ -1441,8 +1483,10 @@ struct Solver final : HandleBase {
 
   int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
+    if (inflight) { err = "iterate with loop bodies in flight (call iterate_wait)"; return CLRSDP_E_STATE; }
     if (use_graph && world == 1 && !timing) launch_graph(prm, pd_feas);
     else enqueue_iteration(prm, pd_feas);
+    res_from_copy = false;
     std::memset(st, 0, sizeof(*st));
     stat_fetch();
     read_stats(st);
@@ -1457,6 +1501,48 @@ struct Solver final : HandleBase {
     return rc;
   }
   void set_timing(int on) override { timing = on; }
+
+  // ---- pipelined loop: the host enqueues loop body k+1 before it reads the log row of body k.
+  // pd_feas and terminate() are evaluated on the device at the end of each update (and by
+  // initial_residuals); a body enqueued after the device decided to terminate changes no
+  // state (the halt word guards every update like a failed factorisation) and reports ran = 0.
+  char* ring_host[2] = {nullptr, nullptr};
+  hipEvent_t ring_ev[2] = {nullptr, nullptr};
+  int ring_head = 0, inflight = 0;
+  int iterate_async(const clrsdp_params* prm) override {
+    if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
+    if (inflight >= 2) { err = "two loop bodies already in flight (call iterate_wait)"; return CLRSDP_E_STATE; }
+    if (!ring_host[0]) {
+      for (int i = 0; i < 2; ++i) {
+        HIPCHK(hipHostMalloc((void**)&ring_host[i], stat_bytes, hipHostMallocDefault));
+        HIPCHK(hipEventCreateWithFlags(&ring_ev[i], hipEventDisableTiming));
+      }
+    }
+    if (use_graph && world == 1 && !timing) launch_graph(prm, -1);
+    else enqueue_iteration(prm, -1);
+    const int slot = (ring_head + inflight) % 2;
+    HIPCHK(hipMemcpyAsync(ring_host[slot], stat_dev, stat_bytes, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipEventRecord(ring_ev[slot], stream));
+    ++inflight;
+    return CLRSDP_OK;
+  }
+  int iterate_wait(clrsdp_iter_stats* st, int* ran) override {
+    if (!inflight) { err = "no loop body in flight"; return CLRSDP_E_STATE; }
+    const int slot = ring_head;
+    ring_head = (ring_head + 1) % 2;
+    --inflight;
+    HIPCHK(hipEventSynchronize(ring_ev[slot]));
+    std::memset(st, 0, sizeof(*st));
+    read_stats(st, ring_host[slot]);
+    const int* h = reinterpret_cast<const int*>(ring_host[slot] + stat_info_off);
+    const bool halted = h[info_H] != 0;
+    if (ran) *ran = halted ? 0 : 1;
+    res_from_copy = true;
+    if (halted) return CLRSDP_OK;   // skipped body: its factorisations may fail, nothing applied
+    const int rc = check_info(ring_host[slot]);
+    st->status = rc;
+    return rc;
+  }
 
   int run_stage(int s, const clrsdp_params* prm, int pd_feas) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
@@ -1478,9 +1564,9 @@ struct Solver final : HandleBase {
       case CLRSDP_BUF_S: src = S; n = nS; break;
       case CLRSDP_BUF_AY: src = AY; n = nAY; break;
       case CLRSDP_BUF_Q: src = Q; n = n_y * n_y; break;
-      case CLRSDP_BUF_P: src = P; n = nblk_el; break;
-      case CLRSDP_BUF_PVEC: src = pvec; n = n_y; break;
-      case CLRSDP_BUF_DVEC: src = dvec; n = nx; break;
+      case CLRSDP_BUF_P: src = res_from_copy ? Pres : P; n = nblk_el; break;
+      case CLRSDP_BUF_PVEC: src = res_from_copy ? pres : pvec; n = n_y; break;
+      case CLRSDP_BUF_DVEC: src = res_from_copy ? dres : dvec; n = nx; break;
       case CLRSDP_BUF_DX: src = dx; n = nx; break;
       case CLRSDP_BUF_DXMAT: src = dX; n = nblk_el; break;
       case CLRSDP_BUF_DY: src = dyv; n = n_y; break;
@@ -1578,7 +1664,28 @@ int32_t clrsdp_initial_residuals(clrsdp_handle* h, const clrsdp_params* prm, clr
 int32_t clrsdp_iterate(clrsdp_handle* h, const clrsdp_params* prm, int32_t pd_feas,
                        clrsdp_iter_stats* st) {
   if (!h || !prm || !st) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  if (pd_feas != 0 && pd_feas != 1) { g_last_error = "pd_feas must be 0 or 1"; return CLRSDP_E_ARG; }
   GUARD(h, { return h->impl->iterate(prm, pd_feas, st); })
+}
+
+int32_t clrsdp_set_control(clrsdp_handle* h, const clrsdp_control* ctl) {
+  if (!h || !ctl) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->set_control(ctl); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_iterate_async(clrsdp_handle* h, const clrsdp_params* prm) {
+  if (!h || !prm) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, { return h->impl->iterate_async(prm); })
+}
+
+int32_t clrsdp_iterate_wait(clrsdp_handle* h, clrsdp_iter_stats* st, int32_t* ran) {
+  if (!h || !st) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, {
+    int r = 0;
+    const int rc = h->impl->iterate_wait(st, &r);
+    if (ran) *ran = r;
+    return rc;
+  })
 }
 
 int32_t clrsdp_run_stage(clrsdp_handle* h, int32_t stage, const clrsdp_params* prm, int32_t pd_feas) {

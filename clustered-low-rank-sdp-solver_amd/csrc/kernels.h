@@ -1248,6 +1248,17 @@ __global__ void rect_fill(const RectDesc* __restrict__ rd, double v) {
 }
 
 // out[0..n) = v
+// dst = src unless *halt (the loop body was skipped by device-side termination): keeps P, p, d
+// of the last loop body that ran for the pipelined loop
+template <class T>
+__global__ void vec_copy_guard(T* __restrict__ dst, const T* __restrict__ src, long long n,
+                               const int* __restrict__ halt) {
+  if (*halt) return;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x)
+    dst[e] = src[e];
+}
+
 template <class T>
 __global__ void vec_fill(T* out, double v, long long n) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1457,7 +1468,10 @@ __global__ void extract_AY(const AYDesc* __restrict__ ad, const T* BY, T* AY) {
 // ------------------------------------------------------------------------------------------
 enum { SC_MU = 0, SC_MU_P, SC_R, SC_BETA, SC_BETA_C, SC_MU_C, SC_ALPHA_P, SC_ALPHA_D, SC_MINEIG_X,
        SC_MINEIG_Y, SC_POBJ, SC_DOBJ, SC_ERR_PMAT, SC_ERR_PVEC, SC_ERR_DVEC, SC_DOT_XY, SC_DOT_XDY,
-       SC_DOT_CX, SC_DOT_BY, SC_DOT_CY, SC_TMP0, SC_TMP1, SC_TMP2, SC_TMP3, SC_COUNT };
+       SC_DOT_CX, SC_DOT_BY, SC_DOT_CY, SC_TMP0, SC_TMP1, SC_TMP2, SC_TMP3,
+       // loop control decided on the device (pipelined iterate): check_pd_feasibility and
+       // terminate of the state after the last update (MPMP.jl:942-945, 1147-1185)
+       SC_PDFEAS, SC_HALT, SC_GAP, SC_COUNT };
 
 // A fixed-order reduction folded into scalar_kernel: sc[dst] = op over cnt values spaced
 // `stride` apart (op 0 sum, 2 max, 3 min, 4 max |.|).  Used for the rank-ordered reductions of
@@ -1469,14 +1483,42 @@ template <class T> struct FoldRed {
 };
 template <class T> struct ScalarParams {
   T beta_inf, beta_feas, gamma, b0;
+  T gap_thr, p_thr, d_thr;  // terminate / check_pd_feasibility thresholds (device loop control)
   double dim;
-  int pd_feas;
+  int pd_feas;  // 0/1 from the host; -1: read sc[SC_PDFEAS] (decided at the end of the last update)
+  int need_p, need_d;
   int nred;
   int zero_cy;  // which == 3 without C: <C,Y> = 0
   int zero_n;   // zero the status words zero_ptr[0..zero_n) (start of an iteration)
   int* zero_ptr;
+  int* halt_ptr;  // which == 0: status word "skip this loop body" (device-decided termination)
   FoldRed<T> red[6];
 };
+
+template <class T>
+__device__ inline bool pd_feasible(const T* sc, const ScalarParams<T>& p) {
+  return p.pd_feas < 0 ? sc[SC_PDFEAS] > T(0.5) : p.pd_feas != 0;
+}
+
+// gap, pd_feas and terminate() of the current objectives and errors (MPMP.jl:942-945 and
+// 1067-1078, 1147-1185); excl_b0: the initial gap of MPMP.jl:725 (compute_duality_gap has no b0)
+template <class T>
+__device__ inline void control_update(T* sc, const ScalarParams<T>& p, bool excl_b0) {
+  const T po = excl_b0 ? sc[SC_POBJ] - p.b0 : sc[SC_POBJ];
+  const T dob = excl_b0 ? sc[SC_DOBJ] - p.b0 : sc[SC_DOBJ];
+  const T den0 = Num<T>::abs_(po + dob);
+  const T den = den0 > T(1.0) ? den0 : T(1.0);
+  const T gap = Num<T>::abs_(po - dob) / den;
+  const T perr = sc[SC_ERR_PMAT] > sc[SC_ERR_PVEC] ? sc[SC_ERR_PMAT] : sc[SC_ERR_PVEC];
+  const T derr = sc[SC_ERR_DVEC];
+  const bool pf = perr < p.p_thr, df = derr < p.d_thr, go = gap < p.gap_thr;
+  // sticky once set (a skipped body must not un-terminate the loop); reset by excl_b0 (initial)
+  const bool halt = (p.need_p && pf) || (p.need_d && df) || (pf && df && go) ||
+                    (!excl_b0 && sc[SC_HALT] > T(0.5));
+  sc[SC_GAP] = gap;
+  sc[SC_PDFEAS] = T((pf && df) ? 1.0 : 0.0);
+  sc[SC_HALT] = T(halt ? 1.0 : 0.0);
+}
 
 // one wave: lane l folds elements l, l+64, ... in order, then a fixed xor butterfly
 template <class T>
@@ -1516,13 +1558,15 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
   if (lane != 0) return;
   const T dim = T(p.dim);
   if (which == 0) {  // mu, mu_p
+    const bool pdf = pd_feasible(sc, p);
+    if (p.halt_ptr) *p.halt_ptr = (p.pd_feas < 0 && sc[SC_HALT] > T(0.5)) ? 1 : 0;
     sc[SC_MU] = sc[SC_DOT_XY] / dim;
-    sc[SC_MU_P] = p.pd_feas ? T(0.0) : p.beta_inf * sc[SC_MU];
+    sc[SC_MU_P] = pdf ? T(0.0) : p.beta_inf * sc[SC_MU];
   } else if (which == 1) {  // r, beta, beta_c, mu_c
     const T r = sc[SC_DOT_XDY] / (sc[SC_MU] * dim);
     const T beta = (r < T(1.0)) ? r * r : r;
     T bc;
-    if (p.pd_feas) {
+    if (pd_feasible(sc, p)) {
       bc = (p.beta_feas > beta) ? p.beta_feas : beta;
       if (bc > T(1.0)) bc = T(1.0);
     } else {
@@ -1536,7 +1580,7 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     const T g = p.gamma;
     T ap = (sc[SC_MINEIG_X] > -g) ? T(1.0) : -g / sc[SC_MINEIG_X];
     T ad = (sc[SC_MINEIG_Y] > -g) ? T(1.0) : -g / sc[SC_MINEIG_Y];
-    if (p.pd_feas) {
+    if (pd_feasible(sc, p)) {
       const T mn = (ad < ap) ? ad : ap;
       ap = mn;
       ad = mn;
@@ -1547,6 +1591,12 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     if (p.zero_cy) sc[SC_DOT_CY] = T(0.0);
     sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;
     sc[SC_DOBJ] = sc[SC_DOT_CY] + sc[SC_DOT_BY] + p.b0;
+    control_update(sc, p, false);
+  } else if (which == 4) {  // objectives + control of the initial point (MPMP.jl:723-736)
+    if (p.zero_cy) sc[SC_DOT_CY] = T(0.0);
+    sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;
+    sc[SC_DOBJ] = sc[SC_DOT_CY] + sc[SC_DOT_BY] + p.b0;
+    control_update(sc, p, true);
   }
 }
 
@@ -1556,7 +1606,8 @@ template <class T>
 __global__ __launch_bounds__(1024) void update_small(T* x, const T* dx, long long nx, T* y,
                                                      const T* dy, long long ny, const T* c,
                                                      const T* b, T* sc, const int* info, int ninfo,
-                                                     T b0) {
+                                                     ScalarParams<T> p) {
+  const T b0 = p.b0;
   __shared__ T red[1024];
   __shared__ int any;
   const int tid = threadIdx.x;
@@ -1599,6 +1650,7 @@ __global__ __launch_bounds__(1024) void update_small(T* x, const T* dx, long lon
     sc[SC_DOT_BY] = red[0];
     sc[SC_POBJ] = cx + b0;
     sc[SC_DOBJ] = red[0] + b0;
+    control_update(sc, p, false);
   }
 }
 

@@ -47,6 +47,20 @@ def make_params(beta_infeasible, beta_feasible, gamma, b0) -> _lib.Params:
     return p
 
 
+def make_control(duality_gap_threshold, primal_error_threshold, dual_error_threshold,
+                 need_primal_feasible=False, need_dual_feasible=False) -> _lib.Control:
+    c = _lib.Control()
+    for name, v in (("duality_gap_threshold", duality_gap_threshold),
+                    ("primal_error_threshold", primal_error_threshold),
+                    ("dual_error_threshold", dual_error_threshold)):
+        arr = getattr(c, name)
+        for i, x in enumerate(limbs(v)):
+            arr[i] = x
+    c.need_primal_feasible = 1 if need_primal_feasible else 0
+    c.need_dual_feasible = 1 if need_dual_feasible else 0
+    return c
+
+
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(_lib.P_f64)
 
@@ -149,6 +163,27 @@ class DeviceSolver:
         self.check(self.L.clrsdp_get_buffer(self.h, buf, _ptr(out), C.byref(cnt)))
         return self._from_planes(out, n, exact)
 
+    def global_P_d(self):
+        """P (blocks) and d (vector) in the global layout of get_state: the device buffers hold
+        the owned clusters only (in owned order); the other clusters' entries are zero, as in
+        get_state, and live on the ranks that own them."""
+        bi = self.bi
+        Pl, dl = self.buffer(_lib.BUF_P), self.buffer(_lib.BUF_DVEC)
+        if len(self.owned) == bi.J:
+            return flat_to_blocks(Pl, bi), dl
+        P = [[np.zeros((n, n)) for n in bj] for bj in bi.Y_blocksizes]
+        d = np.zeros(self.n_x)
+        xoff = np.concatenate([[0], np.cumsum(bi.dim_S)])
+        po = lo = 0
+        for j in self.owned:
+            for l, n in enumerate(bi.Y_blocksizes[j]):
+                P[j][l] = np.asarray(Pl[po:po + n * n]).reshape(n, n, order="F")
+                po += n * n
+            D = bi.dim_S[j]
+            d[xoff[j]:xoff[j] + D] = dl[lo:lo + D]
+            lo += D
+        return P, d
+
     def scalar(self, name: str, exact=False):
         return self.buffer(_lib.BUF_SCALARS, exact)[_lib.SC[name]]
 
@@ -162,6 +197,21 @@ class DeviceSolver:
         st = _lib.IterStats()
         self.check(self.L.clrsdp_iterate(self.h, C.byref(prm), 1 if pd_feas else 0, C.byref(st)))
         return st
+
+    def set_control(self, ctl: _lib.Control):
+        self.check(self.L.clrsdp_set_control(self.h, C.byref(ctl)))
+
+    def iterate_async(self, prm: _lib.Params):
+        """Enqueue one loop body (pd_feas / termination decided on the device); no wait."""
+        self.check(self.L.clrsdp_iterate_async(self.h, C.byref(prm)))
+
+    def iterate_wait(self):
+        """Stats of the oldest loop body in flight and whether it ran (0: the device had
+        terminated before it)."""
+        st = _lib.IterStats()
+        ran = C.c_int32(0)
+        self.check(self.L.clrsdp_iterate_wait(self.h, C.byref(st), C.byref(ran)))
+        return st, bool(ran.value)
 
     def run_stage(self, stage: int, prm: _lib.Params, pd_feas: bool):
         self.check(self.L.clrsdp_run_stage(self.h, stage, C.byref(prm), 1 if pd_feas else 0))
@@ -236,11 +286,17 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
                   omega_d=None, duality_gap_threshold=None, primal_error_threshold=None,
                   dual_error_threshold=None, need_primal_feasible=False, need_dual_feasible=False,
                   testing=True, initial_solutions=(), precision_words=1, device=0, verbose=True,
-                  solver: Optional[DeviceSolver] = None, return_info=False, record_exact=False):
+                  solver: Optional[DeviceSolver] = None, return_info=False, record_exact=False,
+                  pipelined: Optional[bool] = None):
     """Solve the clustered low-rank SDP on the GPU; same signature/semantics as MPMP.jl:595-614.
 
     Returns ``(x, X, y, Y, P, p, d, duality_gap, primal_objective, dual_objective, time)``
     (MPMP.jl:1014-1024); with ``return_info`` a :class:`RunInfo` is appended.
+
+    ``pipelined`` (default: on when the clusters are sharded over ranks): the host stays one loop body behind
+    the device (clrsdp_iterate_async / _wait) and pd_feas / terminate() are evaluated on the
+    device with the same thresholds, so no host round trip separates two loop bodies.  The
+    iterates, the log and the returned values are the same as the synchronous loop's.
     """
     kw = dict(beta_infeasible=beta_infeasible, beta_feasible=beta_feasible, gamma=gamma,
               omega_p=omega_p, omega_d=omega_d, duality_gap_threshold=duality_gap_threshold,
@@ -261,6 +317,14 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
         x, X, y, Y = initial_point(bi, float(prm_v["omega_p"]), float(prm_v["omega_d"]))
     dev.set_state(x, X, y, Y)
     b0f = float(b0)
+    if pipelined is None:
+        # one GPU: the hipGraph replay leaves only a short host round trip between bodies and
+        # the synchronous loop measured faster; sharded: enqueueing (exchange callbacks, no
+        # graph) is host-heavy, so the host runs one body ahead
+        pipelined = dev.world > 1 and not record_exact
+    dev.set_control(make_control(prm_v["duality_gap_threshold"], prm_v["primal_error_threshold"],
+                                 prm_v["dual_error_threshold"], need_primal_feasible,
+                                 need_dual_feasible))
     out(HEADER)
     st = dev.initial_residuals(prm)
     p_obj, d_obj = st.p_obj, st.d_obj
@@ -276,21 +340,11 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     t_after2 = None
     status = "maxiterations"
     exact = []
-    while True:
-        if _terminate(dual_gap, perr, derr, gthr, pthr, dthr, need_primal_feasible,
-                      need_dual_feasible, out):
-            status = "terminated"
-            break
-        if not it < maxiterations:
-            break
-        if it == 3:
-            t_after2 = time.time()
-        st = dev.iterate(prm, pd_feas)
+
+    def record(st):
+        nonlocal p_obj, d_obj, dual_gap, perr, derr, pd_feas, it
         if it > 2:
-            phase += np.array(st.phase_ms[:])
-        if record_exact:
-            sc = dev.buffer(_lib.BUF_SCALARS, exact=True)
-            exact.append({k: sc[v] for k, v in _lib.SC.items()})
+            phase[:] += np.array(st.phase_ms[:])
         row = (it, time.time() - t_start, st.mu, p_obj, d_obj, dual_gap, st.P_err, st.p_err,
                st.d_err, st.alpha_p, st.alpha_d, st.beta_c)
         log.append(row)
@@ -300,13 +354,65 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
         perr = max(st.p_err, st.P_err)                                         # MPMP.jl:943
         derr = st.d_err
         it += 1
-        pd_feas = perr < pthr and derr < dthr
+        pd_feas = perr < pthr and derr < dthr                                  # MPMP.jl:949-953
+
+    def term():
+        return _terminate(dual_gap, perr, derr, gthr, pthr, dthr, need_primal_feasible,
+                          need_dual_feasible, out)
+
+    if pipelined:
+        # the host one loop body behind: body it+1 is enqueued before the log row of body it is
+        # read; the device decides pd_feas and terminate() itself (same thresholds) and a body
+        # enqueued after termination applies nothing (ran = False)
+        inflight = 0
+        halted = False
+        if term():
+            status = "terminated"
+        elif it < maxiterations:
+            dev.iterate_async(prm)
+            inflight = 1
+        try:
+            while inflight:
+                if it + 1 < maxiterations:
+                    dev.iterate_async(prm)
+                    inflight += 1
+                if it == 3:
+                    t_after2 = time.time()
+                st, ran = dev.iterate_wait()
+                inflight -= 1
+                if not ran:
+                    halted = True
+                    break
+                record(st)
+        finally:
+            while inflight:   # drain skipped bodies (or the one behind a failure)
+                try:
+                    dev.iterate_wait()
+                except Exception:
+                    pass
+                inflight -= 1
+        if it > 1 or halted:
+            # the reference evaluates terminate() (which prints the reason) before iter < maxit
+            if term() or halted:
+                status = "terminated"
+    while not pipelined:
+        if term():
+            status = "terminated"
+            break
+        if not it < maxiterations:
+            break
+        if it == 3:
+            t_after2 = time.time()
+        st = dev.iterate(prm, pd_feas)
+        if record_exact:
+            sc = dev.buffer(_lib.BUF_SCALARS, exact=True)
+            exact.append({k: sc[v] for k, v in _lib.SC.items()})
+        record(st)
     t_total = time.time() - t_start
     out(HEADER)
     xf, Xf, yf, Yf = dev.get_state()
-    P = flat_to_blocks(dev.buffer(_lib.BUF_P), bi)
+    P, d = dev.global_P_d()
     p = dev.buffer(_lib.BUF_PVEC)
-    d = dev.buffer(_lib.BUF_DVEC)
     gap_nob0 = abs((p_obj - b0f) - (d_obj - b0f)) / max(1.0, abs((p_obj - b0f) + (d_obj - b0f)))
     res = (xf, Xf, yf, Yf, P, p, d, gap_nob0, p_obj, d_obj, t_total)
     if return_info:

@@ -123,6 +123,16 @@ typedef struct {
   double b0[4];
 } clrsdp_params;
 
+/* Loop-control thresholds of terminate() and check_pd_feasibility() (MPMP.jl:606-611,
+ * 1147-1185), up to 4 limbs each; used by the pipelined loop (clrsdp_iterate_async). */
+typedef struct {
+  double duality_gap_threshold[4];
+  double primal_error_threshold[4];
+  double dual_error_threshold[4];
+  int32_t need_primal_feasible;
+  int32_t need_dual_feasible;
+} clrsdp_control;
+
 /* What one loop body produces for the host's log row and termination test (MPMP.jl:923-953).
  * All values are the leading limb. */
 typedef struct {
@@ -183,6 +193,17 @@ int32_t clrsdp_initial_residuals(clrsdp_handle* h, const clrsdp_params* prm,
  * check_pd_feasibility result from the previous iteration (MPMP.jl:949-953). */
 int32_t clrsdp_iterate(clrsdp_handle* h, const clrsdp_params* prm, int32_t pd_feas,
                        clrsdp_iter_stats* st);
+
+/* Pipelined loop (replaces the same loop, MPMP.jl:743-954, with the host one body behind):
+ * clrsdp_set_control sets the thresholds; clrsdp_iterate_async enqueues one loop body whose
+ * pd_feas and termination are decided on the device from the previous body's results
+ * (after clrsdp_initial_residuals for the first) and returns at once; clrsdp_iterate_wait
+ * waits for the oldest body in flight and returns its log row.  At most two bodies are in
+ * flight.  A body enqueued after the device decided to terminate applies nothing and returns
+ * *ran = 0; P, p, d (clrsdp_get_buffer) are then those of the last body that ran. */
+int32_t clrsdp_set_control(clrsdp_handle* h, const clrsdp_control* ctl);
+int32_t clrsdp_iterate_async(clrsdp_handle* h, const clrsdp_params* prm);
+int32_t clrsdp_iterate_wait(clrsdp_handle* h, clrsdp_iter_stats* st, int32_t* ran);
 
 /* Run one stage (CLRSDP_STAGE_*) only; stages must be run in order within an iteration. */
 int32_t clrsdp_run_stage(clrsdp_handle* h, int32_t stage, const clrsdp_params* prm,

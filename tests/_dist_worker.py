@@ -23,6 +23,18 @@ def main():
     owned = pk.partition_clusters(bi, world)[rank]
     dev = pk.DeviceSolver(cons, b, bi, device=0, rank=rank, world=world, owned=owned)
     ex.attach(dev)
+    if len(sys.argv) > 3 and sys.argv[3] == "solve":
+        # the whole solverank1sdp loop, sharded (pipelined host loop by default at world > 1)
+        res = pk.solverank1sdp(cons, b, bi, solver=dev, omega_p=10.0, omega_d=10.0,
+                               duality_gap_threshold=1e-6, primal_error_threshold=1e-6,
+                               dual_error_threshold=1e-6, verbose=False, return_info=True)
+        info = res[-1]
+        json.dump({"rank": rank, "log": [list(r[2:]) for r in info.log], "status": info.status,
+                   "y": list(map(float, res[2])), "p_obj": res[8], "d_obj": res[9]},
+                  open(f"{out}.{rank}.json", "w"))
+        dev.close()
+        ex.close()
+        return
     P = pk.make_params("0.3", "0.1", "0.7", 0)
     dev.set_state(*pk.initial_point(bi, 10.0, 10.0))
     log = []

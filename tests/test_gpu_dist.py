@@ -52,3 +52,29 @@ def test_two_ranks_match_single_rank(pk):
         for j in rr["owned"]:
             a, c = bi.x_indices[j], bi.x_indices[j + 1]
             np.testing.assert_allclose(rr["x"][a:c], x[a:c], rtol=1e-10, atol=1e-12)
+
+
+def test_two_ranks_full_solve_pipelined(pk):
+    """solverank1sdp sharded over two ranks (pipelined host loop, device-side termination) ends
+    with the single-rank synchronous run's iteration count, log and objectives."""
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "s")
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={_port()}",
+               os.path.join(HERE, "_dist_worker.py"), out, "0", "solve"]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        res = [json.load(open(f"{out}.{k}.json")) for k in range(2)]
+    cons, b = pk.synth(seed=12, J=5, delta=16, rank=1, n_y=9, m=1)
+    bi = pk.get_block_info(cons)
+    ref = pk.solverank1sdp(cons, b, bi, omega_p=10.0, omega_d=10.0, duality_gap_threshold=1e-6,
+                           primal_error_threshold=1e-6, dual_error_threshold=1e-6,
+                           verbose=False, return_info=True, pipelined=False)
+    info = ref[-1]
+    assert info.status == "terminated"
+    for rr in res:
+        assert rr["status"] == "terminated" and len(rr["log"]) == len(info.log)
+        np.testing.assert_allclose(np.array(rr["log"]), np.array([r[2:] for r in info.log]),
+                                   rtol=1e-9, atol=1e-12)
+        assert abs(rr["d_obj"] - ref[9]) < 1e-9 and abs(rr["p_obj"] - ref[8]) < 1e-9

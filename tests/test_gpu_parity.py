@@ -319,3 +319,27 @@ def test_sphere_packing_bound_qd(pk):
     bound = -res[9]
     assert S.NACL_DENSITY < bound < 0.82
     assert abs(bound - 0.8150074605) < 3e-6
+
+
+@pytest.mark.parametrize("words,maxit", [(1, 100), (1, 5), (2, 100)])
+def test_pipelined_loop_equals_synchronous(pk, words, maxit):
+    """The pipelined host loop (device-side pd_feas / terminate, host one body behind) gives
+    the same log, iterates, residuals and objectives as the synchronous loop, bit for bit,
+    whether it stops by termination (the speculative body is skipped) or by maxiterations."""
+    cons, b = pk.synth(J=3, delta=5, rank=1, n_y=4, seed=7, m=2, L=2)
+    bi = pk.get_block_info(cons)
+    # thresholds well above the fp64 Cholesky breakdown near optimality (DESIGN.md §1)
+    kw = dict(omega_p=10.0, omega_d=10.0, duality_gap_threshold=1e-6, primal_error_threshold=1e-6,
+              dual_error_threshold=1e-6, maxiterations=maxit, precision_words=words,
+              verbose=False, return_info=True)
+    a = pk.solverank1sdp(cons, b, bi, pipelined=False, **kw)
+    p = pk.solverank1sdp(cons, b, bi, pipelined=True, **kw)
+    assert a[-1].status == p[-1].status and a[-1].iterations == p[-1].iterations
+    if maxit == 100:
+        assert a[-1].status == "terminated"
+    assert [r[2:] for r in a[-1].log] == [r[2:] for r in p[-1].log]
+    assert np.array_equal(a[0], p[0]) and np.array_equal(a[2], p[2])
+    for i in (1, 3, 4):   # X, Y, P blocks
+        assert all(np.array_equal(u, v) for bu, bv in zip(a[i], p[i]) for u, v in zip(bu, bv))
+    assert np.array_equal(a[5], p[5]) and np.array_equal(a[6], p[6])
+    assert a[7:10] == p[7:10]
