@@ -147,7 +147,7 @@ def main():
     dist = None
     if world > 1:
         from clrsdp_amd import dist as cdist
-        dist = cdist.TorchExchange(local_rank)
+        dist = cdist.make_exchange(local_rank)
     dev = pk.DeviceSolver(cons, b, bi, precision_words=args.precision, device=local_rank,
                           rank=rank, world=world, owned=owned, timing=False)
     if dist is not None:
@@ -253,7 +253,8 @@ def main():
                      "schur_ms_per_iteration": sch_s * 1e3,
                      "schur_alg_gbs": by / sch_s / 1e9},
         "phase_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.STAGE_NAMES, phase)},
-        "graph_replay": world == 1,
+        "graph_replay": world == 1 or getattr(dist, "backend", "") == "rccl",
+        "exchange": "none (1 GPU)" if dist is None else dist.backend,
         "host_loop": "pipelined (host one loop body behind, device-side pd_feas/terminate)"
                      if pipelined else "synchronous (one hipGraph replay per loop body)",
     }

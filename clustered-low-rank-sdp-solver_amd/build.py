@@ -15,7 +15,7 @@ DEPS = [SRC, os.path.join(HERE, "csrc", "kernels.h"), os.path.join(HERE, "csrc",
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                # keep MFMA accumulators in the unified VGPR file (otherwise hipcc shuttles them
                # through AGPRs every k-step: 46.7 vs 72.4 TF/s fp64, profiles/r01_f64_mfma_probe.log)
-               "-mllvm", "-amdgpu-mfma-vgpr-form"]
+               "-mllvm", "-amdgpu-mfma-vgpr-form", "-ldl"]
 
 
 def build(force: bool = False, verbose: bool = True) -> str:

@@ -7,7 +7,9 @@
 // world_size > 1 each rank owns a subset of clusters and the few cross-cluster quantities (Q,
 // the n_y-vectors p and sum_j B_j^T S_j^-1 r_j, and ~10 scalars) are all-gathered through the
 // registered exchange and reduced in rank order, so every rank computes identical y, dy, alpha.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -50,6 +52,52 @@ X* dmalloc(size_t n) {
   HIPCHK(hipMemset(p, 0, n * sizeof(X)));
   return reinterpret_cast<X*>(p);
 }
+
+// ---------------- RCCL, loaded at run time (the library itself has no link dependency on it,
+// so a single-GPU or CPU-side user never needs librccl).  Only the five entry points the
+// exchange uses are resolved.
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl& rccl() {
+  static Rccl api;
+  static bool tried = false;
+  static std::string why;
+  if (!tried) {
+    tried = true;
+    void* so = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((so = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+    if (!so) {
+      why = std::string("cannot load librccl: ") + dlerror();
+    } else {
+      api.get_unique_id = reinterpret_cast<decltype(api.get_unique_id)>(dlsym(so, "ncclGetUniqueId"));
+      api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(dlsym(so, "ncclCommInitRank"));
+      api.all_gather = reinterpret_cast<decltype(api.all_gather)>(dlsym(so, "ncclAllGather"));
+      api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(so, "ncclCommDestroy"));
+      api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(so, "ncclGetErrorString"));
+      if (!api.get_unique_id || !api.comm_init_rank || !api.all_gather || !api.comm_destroy ||
+          !api.error_string) {
+        api = Rccl{};
+        why = "librccl lacks an nccl* entry point";
+      }
+    }
+  }
+  if (!api.all_gather) throw ClrsdpError{CLRSDP_E_EXCHANGE, why};
+  return api;
+}
+
+#define RCCLCHK(x)                                                                       \
+  do {                                                                                   \
+    ncclResult_t r_ = (x);                                                               \
+    if (r_ != ncclSuccess)                                                               \
+      throw ClrsdpError{CLRSDP_E_EXCHANGE, std::string(#x) + ": " + rccl().error_string(r_)}; \
+  } while (0)
 
 template <class X>
 X* upload_vec(const std::vector<X>& v) {
@@ -288,6 +336,7 @@ struct HandleBase {
   virtual void get_buffer(int buf, double* host, int64_t* count) = 0;
   virtual int64_t exchange_bytes() const = 0;
   virtual void set_exchange(clrsdp_exchange_fn fn, void* ctx, void* send, void* recv) = 0;
+  virtual void comm_init(const uint8_t* id) = 0;
   virtual void set_stream(void* s) = 0;
   virtual void* get_stream() const = 0;
   virtual void synchronize() = 0;
@@ -329,6 +378,9 @@ struct Solver final : HandleBase {
   int64_t xcap = 0;  // exchange capacity in T values
   clrsdp_exchange_fn xfn = nullptr;
   void* xctx = nullptr;
+  ncclComm_t comm = nullptr;    // native RCCL communicator (clrsdp_comm_init)
+  T* comm_recv = nullptr;       // world * xcap values, rank r's partials at r * cnt
+  int device = 0;
   bool uploaded = false;
   int info_count = 0, info_S0 = 0, info_Q0 = 0, info_Y0 = 0, info_H = 0;
   // pipelined loop (iterate_async / iterate_wait): device-side loop control and results copy
@@ -387,6 +439,7 @@ struct Solver final : HandleBase {
     rank = cfg->rank;
     world = std::max(1, (int)cfg->world_size);
     timing = cfg->timing;
+    device = cfg->device;
     HIPCHK(hipSetDevice(cfg->device));
     J = desc->J;
     n_y = desc->n_y;
@@ -488,6 +541,11 @@ struct Solver final : HandleBase {
                  bvec, dyv, pvec, uvec, bpart, eigX, tmpsc, tC, Stmp, own_send, Vt, Pres, pres, dres};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
+    if (comm) {
+      (void)hipStreamSynchronize(stream);
+      (void)rccl().comm_destroy(comm);
+    }
+    if (comm_recv) (void)hipFree(comm_recv);
     (void)hipFree(ksamp);
     (void)hipFree(rsums);
     if (stat_dev) (void)hipFree(stat_dev);
@@ -905,6 +963,11 @@ struct Solver final : HandleBase {
   // Partials are written to xsend[0..cnt); after the exchange rank r's copy is at
   // xrecv[r*cnt..].  world == 1: xrecv == xsend, nothing to do.
   void exchange(int tag, int64_t cnt) {
+    if (comm) {  // native: one all-gather on the library stream (graph-capturable)
+      RCCLCHK(rccl().all_gather(xsend, xrecv, (size_t)(cnt * (int64_t)sizeof(T)), ncclUint8, comm,
+                                stream));
+      return;
+    }
     if (world == 1) return;
     if (!xfn) throw ClrsdpError{CLRSDP_E_EXCHANGE, "world_size > 1 but no exchange registered"};
     const int rc = xfn(xctx, tag, cnt * (int64_t)sizeof(T), (void*)stream);
@@ -1484,7 +1547,7 @@ struct Solver final : HandleBase {
   int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
     if (inflight) { err = "iterate with loop bodies in flight (call iterate_wait)"; return CLRSDP_E_STATE; }
-    if (use_graph && world == 1 && !timing) launch_graph(prm, pd_feas);
+    if (use_graph && (world == 1 || comm) && !timing) launch_graph(prm, pd_feas);
     else enqueue_iteration(prm, pd_feas);
     res_from_copy = false;
     std::memset(st, 0, sizeof(*st));
@@ -1518,7 +1581,7 @@ struct Solver final : HandleBase {
         HIPCHK(hipEventCreateWithFlags(&ring_ev[i], hipEventDisableTiming));
       }
     }
-    if (use_graph && world == 1 && !timing) launch_graph(prm, -1);
+    if (use_graph && (world == 1 || comm) && !timing) launch_graph(prm, -1);
     else enqueue_iteration(prm, -1);
     const int slot = (ring_head + inflight) % 2;
     HIPCHK(hipMemcpyAsync(ring_host[slot], stat_dev, stat_bytes, hipMemcpyDeviceToHost, stream));
@@ -1582,6 +1645,7 @@ struct Solver final : HandleBase {
 
   int64_t exchange_bytes() const override { return xcap * (int64_t)sizeof(T); }
   void set_exchange(clrsdp_exchange_fn fn, void* ctx, void* send, void* recv) override {
+    if (comm) throw ClrsdpError{CLRSDP_E_STATE, "the handle exchanges over its own RCCL communicator"};
     xfn = fn;
     xctx = ctx;
     if (send && recv) {
@@ -1590,6 +1654,32 @@ struct Solver final : HandleBase {
     } else {
       xsend = xrecv = own_send;
     }
+  }
+  void comm_init(const uint8_t* id) override {
+    if (comm) throw ClrsdpError{CLRSDP_E_STATE, "RCCL communicator already initialised"};
+    if (inflight) throw ClrsdpError{CLRSDP_E_STATE, "loop bodies in flight"};
+    ncclUniqueId uid;
+    static_assert(sizeof(uid) == CLRSDP_COMM_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(&uid, id, sizeof(uid));
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamSynchronize(stream));
+    if (world > 1 && !comm_recv) comm_recv = dmalloc<T>((size_t)world * xcap);
+    ncclComm_t c = nullptr;
+    RCCLCHK(rccl().comm_init_rank(&c, world, uid, rank));  // on failure the handle keeps no comm
+    comm = c;
+    xsend = own_send;
+    xrecv = world > 1 ? comm_recv : own_send;
+    // one eager all-gather of the full capacity: RCCL connects its channels on first use, which
+    // must not happen inside a graph capture
+    RCCLCHK(rccl().all_gather(xsend, xrecv, (size_t)(xcap * (int64_t)sizeof(T)), ncclUint8, comm,
+                              stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    // graphs captured before carry no all-gathers
+    for (hipGraphExec_t& g : gexec)
+      if (g) {
+        HIPCHK(hipGraphExecDestroy(g));
+        g = nullptr;
+      }
   }
   void set_stream(void* s) override { stream = s ? reinterpret_cast<hipStream_t>(s) : own_stream; }
   void* get_stream() const override { return (void*)stream; }
@@ -1708,6 +1798,24 @@ int32_t clrsdp_set_exchange(clrsdp_handle* h, clrsdp_exchange_fn fn, void* ctx, 
                             void* recv_dev) {
   if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
   GUARD(h, { h->impl->set_exchange(fn, ctx, send_dev, recv_dev); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_comm_unique_id(uint8_t* id) {
+  if (!id) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  try {
+    ncclUniqueId uid;
+    RCCLCHK(rccl().get_unique_id(&uid));
+    std::memcpy(id, &uid, sizeof(uid));
+    return CLRSDP_OK;
+  } catch (const ClrsdpError& e) {
+    g_last_error = e.msg;
+    return e.code;
+  }
+}
+
+int32_t clrsdp_comm_init(clrsdp_handle* h, const uint8_t* id) {
+  if (!h || !id) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->comm_init(id); return CLRSDP_OK; })
 }
 
 int32_t clrsdp_set_stream(clrsdp_handle* h, void* stream) {

@@ -1,7 +1,9 @@
-"""Multi-GPU plumbing: one process per GPU, the library's cross-rank exchange over
-torch.distributed (backend "nccl" = RCCL over xGMI on ROCm; "gloo" for CPU-side tests).
+"""Multi-GPU plumbing: one process per GPU.  Default (RcclExchange): the library's own RCCL
+communicator over xGMI, set up through torch.distributed's gloo control plane.  Alternative
+(TorchExchange): the library calls back into torch.distributed (backend "nccl" = RCCL on ROCm;
+"gloo" for tests that put several ranks on one GPU).
 
-The library (include/clrsdp.h) calls the registered exchange in the middle of a stage with its
+With the callback path the library (include/clrsdp.h) calls the registered exchange in the middle of a stage with its
 work enqueued on its own stream; the collective is issued on that same stream (wrapped as a
 torch ExternalStream), so an RCCL all-gather is ordered after the partials were written and
 before their rank-ordered reduction, with no host synchronisation.  Payloads are the few cross-cluster quantities of one iteration (Q:
@@ -82,3 +84,83 @@ class TorchExchange:
     def close(self):
         if self.dist.is_initialized():
             self.dist.destroy_process_group()
+
+
+class RcclExchange:
+    """The default multi-GPU path: the library's own RCCL communicator (clrsdp_comm_init).
+
+    torch.distributed (gloo, host side) is only the control plane: it broadcasts rank 0's RCCL
+    unique id and provides the benchmark's barrier and max-over-ranks.  Every exchange of the
+    loop body is an ncclAllGather the library issues on its stream, so the loop body is captured
+    and replayed as one hipGraph at any world size, with no Python in the data path."""
+
+    def __init__(self, local_rank: int):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.backend = "rccl"
+        if not dist.is_initialized():
+            dist.init_process_group("gloo")
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.local_rank = local_rank
+
+    def attach(self, dev):
+        from .solver import comm_unique_id
+        torch, dist = self.torch, self.dist
+        # every rank loads RCCL first, so that no rank waits in the communicator set-up for a
+        # rank that cannot join it
+        try:
+            uid = comm_unique_id()
+            ok = 1
+        except Exception as e:
+            print(f"[clrsdp rank {self.rank}] RCCL unavailable: {e!r}", flush=True)
+            uid, ok = bytes(128), 0
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) != 1:
+            raise RuntimeError("RCCL could not be loaded on every rank")
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        try:
+            dev.comm_init(bytes(t.tolist()))
+            ok = 1
+        except Exception as e:   # e.g. "invalid usage": several ranks on one GPU
+            print(f"[clrsdp rank {self.rank}] RCCL communicator failed: {e}", flush=True)
+            ok = 0
+        flag = torch.tensor([ok, ok], dtype=torch.int32)
+        dist.all_reduce(flag[:1], op=dist.ReduceOp.MIN)
+        dist.all_reduce(flag[1:], op=dist.ReduceOp.MAX)
+        if int(flag[0]) == 1:
+            return
+        if int(flag[1]) == 1:
+            raise RuntimeError("the RCCL communicator was created on some ranks only")
+        # every rank failed alike: host-staged exchange over the gloo control plane (correct,
+        # slow); loud, so a benchmark line is never mistaken for the native path
+        print(f"[clrsdp rank {self.rank}] falling back to the host-staged gloo exchange",
+              flush=True)
+        self.backend = "gloo (RCCL communicator failed)"
+        self._fallback = TorchExchange(self.local_rank, backend="gloo")
+        self._fallback.attach(dev)
+
+    def barrier(self):
+        self.dist.barrier()
+
+    def max_over_ranks(self, v: float) -> float:
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist.is_initialized():
+            self.dist.destroy_process_group()
+
+
+def make_exchange(local_rank: int):
+    """CLRSDP_EXCHANGE_BACKEND: "rccl" (default; native communicator, graph replay), "nccl"
+    (torch.distributed's RCCL group called back from the library, no graph) or "gloo"
+    (host-staged, for tests that put several ranks on one GPU)."""
+    backend = os.environ.get("CLRSDP_EXCHANGE_BACKEND", "rccl")
+    if backend == "rccl":
+        return RcclExchange(local_rank)
+    return TorchExchange(local_rank, backend)

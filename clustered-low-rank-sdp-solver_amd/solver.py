@@ -235,10 +235,25 @@ class DeviceSolver:
         self.check(self.L.clrsdp_exchange_bytes(self.h, C.byref(b)))
         return b.value
 
+    def comm_init(self, uid: bytes):
+        """Attach the native RCCL communicator (clrsdp_comm_init): every rank passes the id rank 0
+        got from :func:`comm_unique_id`; the exchanges are then all-gathers issued by the
+        library on its stream, captured into the replayed loop-body graph."""
+        if len(uid) != _lib.COMM_ID_BYTES:
+            raise ValueError("RCCL unique id must be %d bytes" % _lib.COMM_ID_BYTES)
+        self.check(self.L.clrsdp_comm_init(self.h, bytes(uid)))
+
     def set_exchange(self, fn, send_ptr: int, recv_ptr: int):
         self._xfn = _lib.EXCHANGE_FN(fn)
         self.check(self.L.clrsdp_set_exchange(self.h, self._xfn, None, C.c_void_p(send_ptr),
                                               C.c_void_p(recv_ptr)))
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (clrsdp_comm_unique_id), to be created on rank 0 only."""
+    buf = C.create_string_buffer(_lib.COMM_ID_BYTES)
+    _lib.check(_lib.lib().clrsdp_comm_unique_id(buf))
+    return buf.raw
 
 
 def initial_point(bi: BlockInfo, omega_p, omega_d):

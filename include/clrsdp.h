@@ -219,13 +219,28 @@ int32_t clrsdp_exchange_bytes(const clrsdp_handle* h, int64_t* bytes);
 int32_t clrsdp_set_exchange(clrsdp_handle* h, clrsdp_exchange_fn fn, void* ctx, void* send_dev,
                             void* recv_dev);
 
+/* Native RCCL exchange (the per-cluster partials all-gathered over xGMI, SURVEY.md §8e;
+ * replaces the reference's shared-memory reductions across cluster threads, e.g. the Q sum
+ * MPMP.jl:1486-1494 and the dy partials 1758-1761).  Rank 0 calls clrsdp_comm_unique_id and
+ * hands the CLRSDP_COMM_ID_BYTES bytes to every rank (any host channel); every rank then calls
+ * clrsdp_comm_init with them.  The handle creates an RCCL communicator of world_size ranks on
+ * its device (RCCL is loaded at run time) and from then on issues every exchange itself as an
+ * ncclAllGather on its stream; the exchange callback is no longer used, and the loop body is
+ * replayed as a hipGraph at any world size (the all-gathers are captured with it).  With
+ * world_size 1 the all-gathers are still issued (in place, one rank), which exercises the
+ * path. */
+#define CLRSDP_COMM_ID_BYTES 128
+int32_t clrsdp_comm_unique_id(uint8_t* id);
+int32_t clrsdp_comm_init(clrsdp_handle* h, const uint8_t* id);
+
 /* Run all work on `stream` (a hipStream_t; NULL = the handle's own stream). */
 int32_t clrsdp_set_stream(clrsdp_handle* h, void* stream);
 void* clrsdp_get_stream(const clrsdp_handle* h);
 int32_t clrsdp_synchronize(clrsdp_handle* h);
 
 /* Turn the per-stage HIP-event timing (clrsdp_iter_stats.phase_ms) on or off.  With timing
- * off and world_size 1, clrsdp_iterate replays a captured hipGraph of the loop body. */
+ * off and world_size 1 (or a native RCCL communicator), clrsdp_iterate replays a captured
+ * hipGraph of the loop body. */
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on);
 
 int32_t clrsdp_destroy(clrsdp_handle* h);

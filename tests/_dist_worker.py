@@ -1,5 +1,6 @@
 """Worker for tests/test_gpu_dist.py: one rank of a sharded run on a (shared) GPU, exchanging
-through torch.distributed gloo (host-staged), printing its iteration log as JSON."""
+through torch.distributed gloo (host-staged) or, with argv[4] = "rccl", the library's own RCCL
+communicator, printing its iteration log as JSON."""
 import json
 import os
 import sys
@@ -17,7 +18,8 @@ def main():
     from clrsdp_amd import dist as cdist
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
-    ex = cdist.TorchExchange(0, backend="gloo")
+    backend = sys.argv[4] if len(sys.argv) > 4 else "gloo"
+    ex = cdist.RcclExchange(0) if backend == "rccl" else cdist.TorchExchange(0, backend="gloo")
     cons, b = pk.synth(seed=12, J=5, delta=16, rank=1, n_y=9, m=1)
     bi = pk.get_block_info(cons)
     owned = pk.partition_clusters(bi, world)[rank]

@@ -22,14 +22,18 @@ def _port():
     return p
 
 
-def test_two_ranks_match_single_rank(pk):
+@pytest.mark.parametrize("backend", ["gloo", "rccl"])
+def test_two_ranks_match_single_rank(pk, backend):
+    """backend "rccl": the native communicator cannot put two ranks on the box's one GPU (RCCL
+    refuses with "invalid usage" on every rank), so this also covers the agreed fallback to the
+    host-staged exchange; on a multi-GPU node the same worker runs the native all-gathers."""
     iters = 4
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "r")
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                "--master-addr=127.0.0.1", f"--master-port={_port()}",
-               os.path.join(HERE, "_dist_worker.py"), out, str(iters)]
+               os.path.join(HERE, "_dist_worker.py"), out, str(iters), "iter", backend]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         res = [json.load(open(f"{out}.{k}.json")) for k in range(2)]
@@ -78,3 +82,35 @@ def test_two_ranks_full_solve_pipelined(pk):
         np.testing.assert_allclose(np.array(rr["log"]), np.array([r[2:] for r in info.log]),
                                    rtol=1e-9, atol=1e-12)
         assert abs(rr["d_obj"] - ref[9]) < 1e-9 and abs(rr["p_obj"] - ref[8]) < 1e-9
+
+
+def test_native_rccl_one_rank_graph_equals_plain(pk):
+    """The native RCCL path (clrsdp_comm_init) at world size 1: the all-gathers are issued in
+    place and captured into the loop-body graph; the iterates equal a handle without a
+    communicator bit for bit, through the synchronous and the pipelined loop."""
+    cons, b = pk.synth(seed=5, J=4, delta=12, rank=1, n_y=7, m=1)
+    bi = pk.get_block_info(cons)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    from clrsdp_amd.solver import comm_unique_id, make_control
+    runs = []
+    for native in (False, True):
+        dev = pk.DeviceSolver(cons, b, bi)
+        if native:
+            dev.comm_init(comm_unique_id())
+        dev.set_control(make_control("1e-15", "1e-30", "1e-30"))
+        dev.set_state(*pk.initial_point(bi, 10.0, 10.0))
+        dev.initial_residuals(P)
+        log = []
+        for _ in range(3):
+            st = dev.iterate(P, False)
+            log.append((st.mu, st.alpha_p, st.alpha_d, st.p_obj, st.d_obj))
+        for _ in range(3):
+            dev.iterate_async(P)
+            st, ran = dev.iterate_wait()
+            assert ran
+            log.append((st.mu, st.alpha_p, st.alpha_d, st.p_obj, st.d_obj))
+        x, X, y, Y = dev.get_state()
+        runs.append((log, x, y))
+        dev.close()
+    assert runs[0][0] == runs[1][0]
+    assert np.array_equal(runs[0][1], runs[1][1]) and np.array_equal(runs[0][2], runs[1][2])
