@@ -583,46 +583,109 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     }
   }
   __syncthreads();
-  if (tid < 64) {
-    T lo = T(0.0), hi = T(0.0);
-    if (tid == 0) {
-      for (int i = 0; i < n; ++i) {
-        T r = T(0.0);
-        if (i > 0) r += Num<T>::sqrt_(e2[i - 1]);
-        if (i + 1 < n) r += Num<T>::sqrt_(e2[i]);
-        const T a = dg[i] - r, b = dg[i] + r;
-        if (i == 0 || a < lo) lo = a;
-        if (i == 0 || b > hi) hi = b;
-      }
-      red[0] = lo;
-      red[1] = hi;
+  (void)red;
+  if (n == 1) {
+    if (tid == 0) out[blockIdx.x] = dg[0];
+    return;
+  }
+  // ---- multisection with all 512 threads (9 bits per round), in two phases:
+  //  (1) fp64 on the leading limbs of the tridiagonal: Gershgorin bracket, 7 rounds;
+  //  (2) multi-word, started from the fp64 eigenvalue +- delta, where delta bounds the effect of
+  //      the rounding to fp64 (Weyl: |dlambda| <= ||dT|| <= ~3 eps64 ||T||) and of the fp64 Sturm
+  //      counts (exact for a matrix perturbed by a few eps64 relative), with a wide margin.  The
+  //      bracket is checked with two multi-word counts (no eigenvalue below it, one below its top)
+  //      and replaced by the Gershgorin bracket if the check fails.  About half the multi-word
+  //      rounds of a multisection from the Gershgorin bracket.
+  // The matrix image in LDS is no longer needed: it holds the fp64 copy and the round masks.
+  double* dgh = reinterpret_cast<double*>(A);
+  double* e2h = dgh + n;
+  double* bnd = e2h + n;  // [0,1] Gershgorin bracket, [2,3] multi-word start bracket, [4] ok
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(bnd + 6);
+  for (int i = tid; i < n; i += NT) {
+    dgh[i] = Num<T>::hi(dg[i]);
+    e2h[i] = Num<T>::hi(e2[i]);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double glo = 0.0, ghi = 0.0;
+    for (int i = 0; i < n; ++i) {
+      double r = 0.0;
+      if (i > 0) r += sqrt(e2h[i - 1]);
+      if (i + 1 < n) r += sqrt(e2h[i]);
+      const double a = dgh[i] - r, b = dgh[i] + r;
+      if (i == 0 || a < glo) glo = a;
+      if (i == 0 || b > ghi) ghi = b;
     }
-    __builtin_amdgcn_wave_barrier();
-    __threadfence_block();
-    lo = red[0];
-    hi = red[1];
-    const T span = hi - lo;
-    lo = lo - span * T(1e-3) - T(1e-300);
-    hi = hi + span * T(1e-3) + T(1e-300);
-    const int rounds = Num<T>::BITS / 6 + 3;
+    // the leading limbs and the fp64 sqrt differ from the exact bounds by ~eps64 relative
+    const double span = ghi - glo, mag = fmax(fabs(glo), fabs(ghi));
+    bnd[0] = glo - span * 1e-3 - mag * 1e-12 - 1e-300;
+    bnd[1] = ghi + span * 1e-3 + mag * 1e-12 + 1e-300;
+  }
+  __syncthreads();
+  const int w = tid >> 6, lane = tid & 63;
+  // one 512-way round: the first of the 512 interior points with a count >= 1 (every thread
+  // gets the same answer); returns its index, or -1 if none
+  auto first_hit = [&](bool hit) -> int {
+    const unsigned long long mk = __ballot(hit);
+    if (lane == 0) masks[w] = mk;
+    __syncthreads();
+    int f = -1;
+    for (int q = 0; q < NW && f < 0; ++q)
+      if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
+    __syncthreads();
+    return f;
+  };
+  {
+    double lo = bnd[0], hi = bnd[1];
+    for (int it = 0; it < 7; ++it) {
+      const double width = hi - lo;
+      const double sigma = lo + width * ((double)(tid + 1) / 513.0);
+      const int f = first_hit(sturm_count_fast(dgh, e2h, n, sigma) >= 1);
+      if (f < 0) {
+        lo = lo + width * (512.0 / 513.0);
+      } else {
+        hi = lo + width * ((double)(f + 1) / 513.0);
+        if (f > 0) lo = lo + width * ((double)f / 513.0);
+      }
+    }
+    if (tid == 0) {
+      const double c = 0.5 * (lo + hi);
+      const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
+      const double delta = 64.0 * (double)n * 2.3e-16 * mag + (hi - lo) + 1e-300;
+      bnd[2] = c - delta;
+      bnd[3] = c + delta;
+    }
+  }
+  __syncthreads();
+  T lo = T(bnd[2]), hi = T(bnd[3]);
+  // check the start bracket at full width: count(lo) == 0 and count(hi) >= 1
+  {
+    int c = 0;
+    if (tid == 0) c = sturm_count(dg, e2, n, lo) == 0;
+    if (tid == 64) c = sturm_count(dg, e2, n, hi) >= 1;
+    if (tid == 0 || tid == 64) masks[tid >> 6] = (unsigned long long)c;
+    __syncthreads();
+    const bool ok = masks[0] && masks[1];
+    __syncthreads();
+    if (!ok) {
+      lo = T(bnd[0]);
+      hi = T(bnd[1]);
+    }
+    // rounds to shrink the bracket to ~2^-BITS of the spectrum's magnitude
+    const int rounds = ok ? (Num<T>::BITS - 25) / 9 + 2 : Num<T>::BITS / 9 + 3;
     for (int it = 0; it < rounds; ++it) {
       const T width = hi - lo;
-      const T sigma = lo + width * T((double)(tid + 1) / 65.0);
-      const int c = sturm_count(dg, e2, n, sigma);
-      const unsigned long long mask = __ballot(c >= 1);
-      T nlo = lo, nhi = hi;
-      if (mask == 0ull) {
-        nlo = lo + width * T(64.0 / 65.0);
+      const T sigma = lo + width * T((double)(tid + 1) / 513.0);
+      const int f = first_hit(sturm_count(dg, e2, n, sigma) >= 1);
+      if (f < 0) {
+        lo = lo + width * T(512.0 / 513.0);
       } else {
-        const int f = __ffsll((long long)mask) - 1;
-        nhi = lo + width * T((double)(f + 1) / 65.0);
-        if (f > 0) nlo = lo + width * T((double)f / 65.0);
+        hi = lo + width * T((double)(f + 1) / 513.0);
+        if (f > 0) lo = lo + width * T((double)f / 513.0);
       }
-      lo = nlo;
-      hi = nhi;
     }
-    if (tid == 0) out[blockIdx.x] = (lo + hi) * T(0.5);
   }
+  if (tid == 0) out[blockIdx.x] = (lo + hi) * T(0.5);
 }
 
 }  // namespace clrsdp
