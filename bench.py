@@ -216,6 +216,7 @@ def main():
         schur_ms = dist.max_over_ranks(schur_ms)
 
     if rank != 0:
+        dev.close()   # the RCCL communicator goes with the handle, before the control plane
         dist.close()
         return
     its = args.steps / dt
@@ -260,10 +261,10 @@ def main():
     }
     if world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(cons, b, bi, args.precision)
-    print(json.dumps(res))
+    print(json.dumps(res), flush=True)
+    dev.close()
     if dist is not None:
         dist.close()
-    dev.close()
 
 
 if __name__ == "__main__":
