@@ -36,6 +36,10 @@ CONFIGS = {
 DTYPES = {1: "f64", 2: "dd(f64x2)", 4: "qd(f64x4)"}
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X fp64 matrix spec; measured ceiling 72.4 (profiles/r01_f64_mfma_probe.log)
 HBM_PEAK_GBS = 8000.0
+# multi-word runs (dd, qd) compute on the fp64 VALU: measured multiply-add ceilings x 2 flops
+# (tools/micro/mw_peak.hip -> profiles/r01_mw_peak.log: dd 1.868 T/s, qd 0.349 T/s; fp64 FMA
+# 30.2 T/s, so a dd multiply-add costs 16.2 and a qd one 86.5 fp64 FMA slots)
+MW_VALU_PEAK_TFLOPS = {2: 3.736, 4: 0.698}
 
 
 def schur_flops_bytes(bi, word=8):
@@ -226,7 +230,8 @@ def main():
         by /= world
     sch_s = schur_ms / 1e3 / n_inst
     traffic, traffic_src = schur_pmc_traffic(args.config, args.precision, world)
-    achieved = fl / sch_s / 1e12
+    achieved = fl / sch_s / 1e12   # in flops of the word type (multi-word flops when w > 1)
+    peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]
     res = {
         "metric": "interior-point iterations/sec (solverank1sdp loop body, MPMP.jl:755-887)",
         "value": its,
@@ -246,9 +251,13 @@ def main():
                                f"{args.config}: sphere-packing shape, J={bi.J} clusters, blocks "
                                f"{bi.Y_blocksizes}, dim_S {bi.dim_S}, n_y={bi.n_y}",
                    "parallelism": f"clusters sharded over {world} GPU(s)" if world > 1 else "1 GPU"},
-        "roofline": {"bound": "mfma", "kernel": "Schur assembly (stage SCHUR)",
-                     "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
+        "roofline": {"bound": "mfma" if args.precision == 1 else "valu",
+                     "kernel": "Schur assembly (stage SCHUR)",
+                     "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "peak_source": "MI355X fp64 matrix spec" if args.precision == 1 else
+                                    "measured %s multiply-add ceiling x 2 (profiles/r01_mw_peak.log)"
+                                    % DTYPES[args.precision],
+                     "frac": achieved / peak, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "alg_bytes_per_iteration": by,
                      "schur_ms_per_iteration": sch_s * 1e3,
