@@ -20,7 +20,8 @@ def main():
     world = int(os.environ["WORLD_SIZE"])
     backend = sys.argv[4] if len(sys.argv) > 4 else "gloo"
     ex = cdist.RcclExchange(0) if backend == "rccl" else cdist.TorchExchange(0, backend="gloo")
-    cons, b = pk.synth(seed=12, J=5, delta=16, rank=1, n_y=9, m=1)
+    J = int(os.environ.get("CLRSDP_TEST_J", "5"))
+    cons, b = pk.synth(seed=12, J=J, delta=16, rank=1, n_y=9, m=1)
     bi = pk.get_block_info(cons)
     owned = pk.partition_clusters(bi, world)[rank]
     dev = pk.DeviceSolver(cons, b, bi, device=0, rank=rank, world=world, owned=owned)

@@ -22,22 +22,24 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("backend", ["gloo", "rccl"])
-def test_two_ranks_match_single_rank(pk, backend):
+@pytest.mark.parametrize("backend,J", [("gloo", 5), ("rccl", 5), ("gloo", 1)])
+def test_two_ranks_match_single_rank(pk, backend, J):
     """backend "rccl": the native communicator cannot put two ranks on the box's one GPU (RCCL
     refuses with "invalid usage" on every rank), so this also covers the agreed fallback to the
-    host-staged exchange; on a multi-GPU node the same worker runs the native all-gathers."""
+    host-staged exchange; on a multi-GPU node the same worker runs the native all-gathers.
+    J = 1: one rank owns no cluster (as config 5's 7 clusters on 8 GPUs) and only contributes
+    neutral partials."""
     iters = 4
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "r")
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CLRSDP_TEST_J=str(J))
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                "--master-addr=127.0.0.1", f"--master-port={_port()}",
                os.path.join(HERE, "_dist_worker.py"), out, str(iters), "iter", backend]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         res = [json.load(open(f"{out}.{k}.json")) for k in range(2)]
-    cons, b = pk.synth(seed=12, J=5, delta=16, rank=1, n_y=9, m=1)
+    cons, b = pk.synth(seed=12, J=J, delta=16, rank=1, n_y=9, m=1)
     bi = pk.get_block_info(cons)
     dev = pk.DeviceSolver(cons, b, bi)
     P = pk.make_params("0.3", "0.1", "0.7", 0)
