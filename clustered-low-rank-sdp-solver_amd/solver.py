@@ -96,6 +96,7 @@ class DeviceSolver:
             cfg.owned = own.ctypes.data_as(_lib.P_i32)
             cfg.n_owned = len(own)
         cfg.timing = 1 if timing else 0
+        self.timing = bool(timing)
         h = C.c_void_p()
         _lib.check(self.L.clrsdp_create(C.byref(desc), C.byref(cfg), C.byref(h)))
         self.h = h
@@ -222,6 +223,7 @@ class DeviceSolver:
     def set_timing(self, on: bool):
         """Per-stage HIP-event timing on/off (off + one rank: iterate replays a hipGraph)."""
         self.check(self.L.clrsdp_set_timing(self.h, 1 if on else 0))
+        self.timing = bool(on)
 
     def set_stream(self, stream_ptr: int):
         self.check(self.L.clrsdp_set_stream(self.h, C.c_void_p(stream_ptr)))
@@ -296,6 +298,39 @@ class RunInfo:
     exact: list = None   # per iteration, the device scalar slots at full precision (record_exact)
 
 
+def _stage_groups(ph):
+    """The reference's timing groups (MPMP.jl:888-898) from the device stages (seconds)."""
+    S = {n: ph[i] for i, n in enumerate(_lib.STAGE_NAMES)}
+    return {"Decomp": S["schur"] + S["factor"], "predict_dir": S["predictor"],
+            "correct_dir": S["corrector"], "alpha": S["step"], "Xinv": S["Xinv"],
+            "R": S["mu_R"] + S["corrector_R"], "res": S["residuals"], "update": S["update"]}
+
+
+def _first_iteration_times(ph):
+    g = _stage_groups(ph)
+    return ("decomp:%s. directions:%s. steplength:%s\nschur:%s factor (chol S, CinvB, Q, chol Q):%s\n"
+            "X inv:%s. R:%s. residuals p,P,d:%s" % (
+                g["Decomp"], g["predict_dir"] + g["correct_dir"], g["alpha"], ph[2], ph[3],
+                g["Xinv"], g["R"], g["res"]))
+
+
+def _time_spent(total, ph):
+    """MPMP.jl:973-1012.  Per-stage device times (sums over iterations 3, 4, ...) need the
+    handle's HIP-event timing (DeviceSolver(timing=True)); without it only the total is known."""
+    cols = ["total", "Decomp", "predict_dir", "correct_dir", "alpha", "Xinv", "R", "res"]
+    lines = ["\nTime spent: (The total time may include compile time. The first few iterations "
+             "are not included in the rest of the times)",
+             ("%11s " * len(cols)).rstrip() % tuple(cols)]
+    if ph is None:
+        lines.append("%11.5e %s" % (total, "(per-stage times need DeviceSolver(timing=True))"))
+        return "\n".join(lines) + "\n"
+    g = _stage_groups(ph)
+    lines.append(("%11.5e " * len(cols)).rstrip() % tuple([total] + [g[c] for c in cols[1:]]))
+    lines.append("\nTime inside decomp:\n%11s %11s\n%11.5e %11.5e" % (
+        "schur", "factor", ph[2], ph[3]))
+    return "\n".join(lines) + "\n"
+
+
 def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterations=500,
                   beta_infeasible=None, beta_feasible=None, gamma=None, omega_p=None,
                   omega_d=None, duality_gap_threshold=None, primal_error_threshold=None,
@@ -356,10 +391,14 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     status = "maxiterations"
     exact = []
 
+    timed = bool(getattr(dev, "timing", False))
+
     def record(st):
         nonlocal p_obj, d_obj, dual_gap, perr, derr, pd_feas, it
         if it > 2:
             phase[:] += np.array(st.phase_ms[:])
+        elif testing and timed:  # MPMP.jl:899-920: the times of the first iterations
+            out(_first_iteration_times(np.array(st.phase_ms[:]) / 1e3))
         row = (it, time.time() - t_start, st.mu, p_obj, d_obj, dual_gap, st.P_err, st.p_err,
                st.d_err, st.alpha_p, st.alpha_d, st.beta_c)
         log.append(row)
@@ -425,6 +464,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
         record(st)
     t_total = time.time() - t_start
     out(HEADER)
+    out(_time_spent(t_total, phase / 1e3 if timed else None))
     xf, Xf, yf, Yf = dev.get_state()
     P, d = dev.global_P_d()
     p = dev.buffer(_lib.BUF_PVEC)

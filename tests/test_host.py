@@ -169,3 +169,19 @@ def test_planar_limbs_exact_at_default_mpmath_precision(pk):
         assert float(to_planes(np.array([mpmath.pi], dtype=object), 4)[3]) != 0.0
     finally:
         mpmath.mp.prec = old
+
+
+def test_time_spent_report_groups_stages_like_the_reference(pk):
+    """solverank1sdp's closing report (MPMP.jl:973-1012): the device stages are summed into the
+    reference's groups (Decomp = Schur + factorisation, R = both R computations, ...)."""
+    from clrsdp_amd import _lib
+    from clrsdp_amd.solver import _stage_groups, _time_spent
+    ph = np.arange(1, _lib.NUM_STAGES + 1, dtype=float)
+    g = _stage_groups(ph)
+    S = dict(zip(_lib.STAGE_NAMES, ph))
+    assert g["Decomp"] == S["schur"] + S["factor"] and g["R"] == S["mu_R"] + S["corrector_R"]
+    assert g["alpha"] == S["step"] and g["predict_dir"] == S["predictor"]
+    assert sum(g.values()) == ph.sum()
+    txt = _time_spent(2.0, ph)
+    assert "Time spent" in txt and "Decomp" in txt and "Time inside decomp" in txt
+    assert "timing=True" in _time_spent(2.0, None)
