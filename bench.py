@@ -263,7 +263,8 @@ def main():
                      "schur_ms_per_iteration": sch_s * 1e3,
                      "schur_alg_gbs": by / sch_s / 1e9},
         "phase_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.STAGE_NAMES, phase)},
-        "graph_replay": world == 1 or getattr(dist, "backend", "") == "rccl",
+        "graph_replay": world == 1 or (getattr(dist, "backend", "") == "rccl"
+                                       and os.environ.get("CLRSDP_GRAPH_RCCL") is not None),
         "exchange": "none (1 GPU)" if dist is None else dist.backend,
         "host_loop": "pipelined (host one loop body behind, device-side pd_feas/terminate)"
                      if pipelined else "synchronous (one hipGraph replay per loop body)",

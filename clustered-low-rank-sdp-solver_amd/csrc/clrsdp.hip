@@ -1522,6 +1522,11 @@ struct Solver final : HandleBase {
   clrsdp_params gprm[4];
   unsigned graph_launches = 0;
   bool use_graph = std::getenv("CLRSDP_NO_GRAPH") == nullptr;
+  // multi-rank loop bodies with the native communicator are enqueued eagerly by default (the
+  // pipelined host loop hides the enqueue); CLRSDP_GRAPH_RCCL=1 captures the all-gathers into
+  // the replayed graph as well
+  bool graph_rccl = std::getenv("CLRSDP_GRAPH_RCCL") != nullptr;
+  bool graph_ok() const { return use_graph && !timing && (world == 1 || (comm && graph_rccl)); }
   void launch_graph(const clrsdp_params* prm, int pd_feas) {
     const int g = pd_feas < 0 ? 2 + (graph_launches++ & 1) : (pd_feas ? 1 : 0);
     if (!gexec[g] || std::memcmp(&gprm[g], prm, sizeof(*prm)) != 0) {
@@ -1547,7 +1552,7 @@ struct Solver final : HandleBase {
   int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
     if (inflight) { err = "iterate with loop bodies in flight (call iterate_wait)"; return CLRSDP_E_STATE; }
-    if (use_graph && (world == 1 || comm) && !timing) launch_graph(prm, pd_feas);
+    if (graph_ok()) launch_graph(prm, pd_feas);
     else enqueue_iteration(prm, pd_feas);
     res_from_copy = false;
     std::memset(st, 0, sizeof(*st));
@@ -1581,7 +1586,7 @@ struct Solver final : HandleBase {
         HIPCHK(hipEventCreateWithFlags(&ring_ev[i], hipEventDisableTiming));
       }
     }
-    if (use_graph && (world == 1 || comm) && !timing) launch_graph(prm, -1);
+    if (graph_ok()) launch_graph(prm, -1);
     else enqueue_iteration(prm, -1);
     const int slot = (ring_head + inflight) % 2;
     HIPCHK(hipMemcpyAsync(ring_host[slot], stat_dev, stat_bytes, hipMemcpyDeviceToHost, stream));

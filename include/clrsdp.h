@@ -225,10 +225,11 @@ int32_t clrsdp_set_exchange(clrsdp_handle* h, clrsdp_exchange_fn fn, void* ctx, 
  * hands the CLRSDP_COMM_ID_BYTES bytes to every rank (any host channel); every rank then calls
  * clrsdp_comm_init with them.  The handle creates an RCCL communicator of world_size ranks on
  * its device (RCCL is loaded at run time) and from then on issues every exchange itself as an
- * ncclAllGather on its stream; the exchange callback is no longer used, and the loop body is
- * replayed as a hipGraph at any world size (the all-gathers are captured with it).  With
- * world_size 1 the all-gathers are still issued (in place, one rank), which exercises the
- * path. */
+ * ncclAllGather on its stream; the exchange callback is no longer used.  With world_size > 1
+ * the loop body is enqueued eagerly (the pipelined loop hides the enqueue), or replayed as one
+ * hipGraph with the all-gathers captured in it when CLRSDP_GRAPH_RCCL is set.  With
+ * world_size 1 the all-gathers are still issued (in place, one rank) inside the graph, which
+ * exercises the capture path. */
 #define CLRSDP_COMM_ID_BYTES 128
 int32_t clrsdp_comm_unique_id(uint8_t* id);
 int32_t clrsdp_comm_init(clrsdp_handle* h, const uint8_t* id);

@@ -58,14 +58,14 @@ int main(int argc, char** argv) {
   for (int v = 0; v < 2; ++v) {
     float t1, t2, t3;
     if (v == 0) {
-      t1 = timeit([&] { gemm_f64_lds<false, true, 1, 32><<<(unsigned)gt.size(), 256>>>(dgd, dgt, 1.0, 0.0); });
+      t1 = timeit([&] { gemm_f64_lds<false, true, 1, 32><<<(unsigned)gt.size(), 512>>>(dgd, dgt, 1.0, 0.0); });
       t2 = timeit([&] { schur_pairs_f64<32><<<(unsigned)pt.size(), 256>>>(dpd, dpt); });
-      t3 = timeit([&] { gemm_f64_lds<false, true, 1, 32><<<(unsigned)gt.size(), 256>>>(dgd, dgt, 1.0, 0.0);
+      t3 = timeit([&] { gemm_f64_lds<false, true, 1, 32><<<(unsigned)gt.size(), 512>>>(dgd, dgt, 1.0, 0.0);
                         schur_pairs_f64<32><<<(unsigned)pt.size(), 256>>>(dpd, dpt); });
     } else {
-      t1 = timeit([&] { gemm_f64_lds<false, true, 1, 16><<<(unsigned)gt.size(), 256>>>(dgd, dgt, 1.0, 0.0); });
+      t1 = timeit([&] { gemm_f64_lds<false, true, 1, 16><<<(unsigned)gt.size(), 512>>>(dgd, dgt, 1.0, 0.0); });
       t2 = timeit([&] { schur_pairs_f64<16><<<(unsigned)pt.size(), 256>>>(dpd, dpt); });
-      t3 = timeit([&] { gemm_f64_lds<false, true, 1, 16><<<(unsigned)gt.size(), 256>>>(dgd, dgt, 1.0, 0.0);
+      t3 = timeit([&] { gemm_f64_lds<false, true, 1, 16><<<(unsigned)gt.size(), 512>>>(dgd, dgt, 1.0, 0.0);
                         schur_pairs_f64<16><<<(unsigned)pt.size(), 256>>>(dpd, dpt); });
     }
     printf("BK %d\n", v == 0 ? 32 : 16);
