@@ -412,18 +412,26 @@ __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restric
 //   op 0: sum a.*b    op 1: sum (a+da).*(b+db)    op 2: max |a|
 // ------------------------------------------------------------------------------------------
 template <class T>
-__global__ __launch_bounds__(256) void flat_reduce(const T* a, const T* b, const T* da,
-                                                   const T* db, long long n, int op,
+__global__ __launch_bounds__(256) void flat_reduce(const T* __restrict__ a, const T* __restrict__ b,
+                                                   const T* __restrict__ da,
+                                                   const T* __restrict__ db, long long n, int op,
                                                    T* __restrict__ partial) {
   __shared__ T red[256];
   const long long chunk = (n + gridDim.x - 1) / gridDim.x;
   const long long lo = (long long)blockIdx.x * chunk;
   const long long hi = lo + chunk < n ? lo + chunk : n;
   T acc = T(0.0);
-  for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-    if (op == 0) acc += a[e] * b[e];
-    else if (op == 1) acc += (a[e] + da[e]) * (b[e] + db[e]);
-    else {
+  // one loop per operation (uniform), unrolled so the loads of several elements are in flight;
+  // the per-thread accumulation order is unchanged
+  if (op == 0) {
+#pragma unroll 4
+    for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) acc += a[e] * b[e];
+  } else if (op == 1) {
+#pragma unroll 4
+    for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) acc += (a[e] + da[e]) * (b[e] + db[e]);
+  } else {
+#pragma unroll 4
+    for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) {
       const T v = Num<T>::abs_(a[e]);
       if (v > acc) acc = v;
     }
@@ -1603,9 +1611,12 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
 // x += alpha_p dx, y += alpha_d dy (guarded), then <c,x>, <b,y> and the objectives
 // (MPMP.jl:877-878, 940-941; one rank, C = 0).  One 1024-thread workgroup.
 template <class T>
-__global__ __launch_bounds__(1024) void update_small(T* x, const T* dx, long long nx, T* y,
-                                                     const T* dy, long long ny, const T* c,
-                                                     const T* b, T* sc, const int* info, int ninfo,
+__global__ __launch_bounds__(1024) void update_small(T* __restrict__ x, const T* __restrict__ dx,
+                                                     long long nx, T* __restrict__ y,
+                                                     const T* __restrict__ dy, long long ny,
+                                                     const T* __restrict__ c,
+                                                     const T* __restrict__ b, T* sc,
+                                                     const int* info, int ninfo,
                                                      ScalarParams<T> p) {
   const T b0 = p.b0;
   __shared__ T red[1024];
@@ -1619,6 +1630,9 @@ __global__ __launch_bounds__(1024) void update_small(T* x, const T* dx, long lon
   const bool upd = !any;
   const T ap = sc[SC_ALPHA_P], ad = sc[SC_ALPHA_D];
   T acc = T(0.0);
+  // (restrict + unroll: the loads of several elements are in flight together; the per-thread
+  // accumulation order is unchanged)
+#pragma unroll 8
   for (long long e = tid; e < nx; e += 1024) {
     T v = x[e];
     if (upd) { v = v + ap * dx[e]; x[e] = v; }
