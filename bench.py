@@ -116,8 +116,8 @@ def cpu_baseline(cons, b, bi, precision=1, budget_s=20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--precision", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
