@@ -1328,8 +1328,14 @@ struct Solver final : HandleBase {
   void st_corrector_r(const clrsdp_params* prm, int pd_feas) {
     blk_dot(X, Y, dX, dY, 1, SC_DOT_XDY, 5);
     scalars(prm, pd_feas, 1);
-    p_XY.launch(stream, -1.0, 0.0);
-    gemm_diag(p_dXdY, -1.0, 1.0, SC_MU_C);      // R = mu_c I - XY - dX dY
+    if constexpr (std::is_same<T, double>::value) {
+      // R still holds mu_p I - XY from MU_R (the predictor only reads it), so one GEMM:
+      // R = (mu_p I - XY) - dX dY + (mu_c - mu_p) I, without forming XY again
+      gemm_diag(p_dXdY, -1.0, 1.0, SC_DMU);
+    } else {  // multi-word: the reference's order of operations (MPMP.jl:1209-1214)
+      p_XY.launch(stream, -1.0, 0.0);
+      gemm_diag(p_dXdY, -1.0, 1.0, SC_MU_C);    // R = mu_c I - XY - dX dY
+    }
   }
   void st_step(const clrsdp_params* prm, int pd_feas) {
     if (reg_blk) {

@@ -1476,7 +1476,8 @@ __global__ void extract_AY(const AYDesc* __restrict__ ad, const T* BY, T* AY) {
 // ------------------------------------------------------------------------------------------
 enum { SC_MU = 0, SC_MU_P, SC_R, SC_BETA, SC_BETA_C, SC_MU_C, SC_ALPHA_P, SC_ALPHA_D, SC_MINEIG_X,
        SC_MINEIG_Y, SC_POBJ, SC_DOBJ, SC_ERR_PMAT, SC_ERR_PVEC, SC_ERR_DVEC, SC_DOT_XY, SC_DOT_XDY,
-       SC_DOT_CX, SC_DOT_BY, SC_DOT_CY, SC_TMP0, SC_TMP1, SC_TMP2, SC_TMP3,
+       SC_DOT_CX, SC_DOT_BY, SC_DOT_CY, SC_TMP0, SC_TMP1, SC_TMP2,
+       SC_DMU,  // mu_c - mu_p (the corrector's R from the predictor's, fp64)
        // loop control decided on the device (pipelined iterate): check_pd_feasibility and
        // terminate of the state after the last update (MPMP.jl:942-945, 1147-1185)
        SC_PDFEAS, SC_HALT, SC_GAP, SC_COUNT };
@@ -1584,6 +1585,7 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     sc[SC_BETA] = beta;
     sc[SC_BETA_C] = bc;
     sc[SC_MU_C] = bc * sc[SC_MU];
+    sc[SC_DMU] = sc[SC_MU_C] - sc[SC_MU_P];
   } else if (which == 2) {  // step lengths
     const T g = p.gamma;
     T ap = (sc[SC_MINEIG_X] > -g) ? T(1.0) : -g / sc[SC_MINEIG_X];
