@@ -169,16 +169,30 @@ def main():
 
     pipelined = args.loop == "pipelined" or (args.loop == "auto" and world > 1)
 
+    # Every RESTART bodies the iterate goes back to the snapshot taken after the warm-up (a
+    # device-side copy, stream-ordered): the instance stagnates near mu ~ 1e-12 after ~100
+    # iterations and the fp64 factorisations break down after ~250, so a long --steps window
+    # replays iterations 1..RESTART instead.  Every timed step is still one full loop body.
+    RESTART = 64
+    count = [0]
+
+    def maybe_restart():
+        count[0] += 1
+        if count[0] % RESTART == 0:
+            dev.restore_state()
+
     def run_bodies(n):
         """n loop bodies as solverank1sdp runs them: the host one body behind the device
         (clrsdp_iterate_async / _wait), every log row read back."""
         if not pipelined:
             for _ in range(n):
                 step()
+                maybe_restart()
             return
         inflight = 0
         for _ in range(n):
             dev.iterate_async(prm)
+            maybe_restart()
             inflight += 1
             if inflight == 2:
                 _, ran = dev.iterate_wait()
@@ -191,6 +205,7 @@ def main():
             if not ran:
                 raise RuntimeError("solver terminated inside the benchmark window")
 
+    dev.save_state()   # snapshot of the initial point (restart target of long windows)
     run_bodies(args.warmup)
 
     def barrier_sync():

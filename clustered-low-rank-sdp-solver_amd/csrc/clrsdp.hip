@@ -341,6 +341,8 @@ struct HandleBase {
   virtual void* get_stream() const = 0;
   virtual void synchronize() = 0;
   virtual void set_timing(int on) = 0;
+  virtual void save_state() = 0;
+  virtual void restore_state() = 0;
 };
 
 template <class T>
@@ -546,6 +548,7 @@ struct Solver final : HandleBase {
       (void)rccl().comm_destroy(comm);
     }
     if (comm_recv) (void)hipFree(comm_recv);
+    if (snap) (void)hipFree(snap);
     (void)hipFree(ksamp);
     (void)hipFree(rsums);
     if (stat_dev) (void)hipFree(stat_dev);
@@ -1275,6 +1278,16 @@ struct Solver final : HandleBase {
     if (anyMgt1) sym(Z, Z, 0);
     // rhs_x = -d - Tr(A_* Z)
     p_trU_Z.launch(stream, 1.0, 0.0);
+    direction_solves(tag);
+    // dX = P + sum_i dx_i A_i
+    weighted_A(dx, p_wA_dX, dX, 1.0);
+    // dY = sym(X^-1 (R - dX Y))
+    p_dXY.launch(stream, -1.0, 1.0);
+    p_dY.launch(stream, 1.0, 0.0);
+    sym(dY, dY, 0);
+  }
+  // rhs, the three-stage solve and dx as separate batched launches (any word type / rank count)
+  void direction_solves(int tag) {
     if (trivial_tuples) {
       dim3 g(cdiv(max_K, 4), n_pair);
       colsum_rhs<T><<<g, 256, 0, stream>>>(d_pair, TX, V, lam, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
@@ -1318,12 +1331,6 @@ struct Solver final : HandleBase {
       p_Wdy.launch(stream, 1.0, 1.0);
       t_dx.launch(stream, true);
     }
-    // dX = P + sum_i dx_i A_i
-    weighted_A(dx, p_wA_dX, dX, 1.0);
-    // dY = sym(X^-1 (R - dX Y))
-    p_dXY.launch(stream, -1.0, 1.0);
-    p_dY.launch(stream, 1.0, 0.0);
-    sym(dY, dY, 0);
   }
   void st_corrector_r(const clrsdp_params* prm, int pd_feas) {
     blk_dot(X, Y, dX, dY, 1, SC_DOT_XDY, 5);
@@ -1575,6 +1582,34 @@ struct Solver final : HandleBase {
     return rc;
   }
   void set_timing(int on) override { timing = on; }
+
+  // device-side snapshot of the iterate (x, X, y, Y) and the scalar slots, stream-ordered
+  T* snap = nullptr;
+  bool snapped = false;
+  void snap_copy(bool save) {
+    const int64_t B = nblk_el;
+    T* dst[5] = {snap, snap + nx, snap + nx + B, snap + nx + 2 * B, snap + nx + 2 * B + n_y};
+    T* src[5] = {x, X, Y, y, sc};
+    const int64_t cnt[5] = {nx, B, B, n_y, (int64_t)SC_COUNT};
+    for (int i = 0; i < 5; ++i)
+      if (cnt[i])
+        HIPCHK(hipMemcpyAsync(save ? dst[i] : src[i], save ? src[i] : dst[i], cnt[i] * sizeof(T),
+                              hipMemcpyDeviceToDevice, stream));
+  }
+  void save_state() override {
+    if (!snap) {
+      snap = dmalloc<T>((size_t)nx + 2 * (size_t)nblk_el + (size_t)n_y + SC_COUNT);
+      // dmalloc's hipMemset runs on the null stream, which a non-blocking handle stream does
+      // not order against: without this the zero fill can land after the first copy below
+      HIPCHK(hipDeviceSynchronize());
+    }
+    snap_copy(true);
+    snapped = true;
+  }
+  void restore_state() override {
+    if (!snapped) throw ClrsdpError{CLRSDP_E_STATE, "restore_state without save_state"};
+    snap_copy(false);
+  }
 
   // ---- pipelined loop: the host enqueues loop body k+1 before it reads the log row of body k.
   // pd_feas and terminate() are evaluated on the device at the end of each update (and by
@@ -1839,6 +1874,16 @@ void* clrsdp_get_stream(const clrsdp_handle* h) { return h ? h->impl->get_stream
 int32_t clrsdp_synchronize(clrsdp_handle* h) {
   if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
   GUARD(h, { h->impl->synchronize(); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_save_state(clrsdp_handle* h) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->save_state(); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_restore_state(clrsdp_handle* h) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->restore_state(); return CLRSDP_OK; })
 }
 
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on) {

@@ -225,6 +225,14 @@ class DeviceSolver:
         self.check(self.L.clrsdp_set_timing(self.h, 1 if on else 0))
         self.timing = bool(on)
 
+    def save_state(self):
+        """Device-side snapshot of x, X, y, Y and the scalar slots (clrsdp_save_state)."""
+        self.check(self.L.clrsdp_save_state(self.h))
+
+    def restore_state(self):
+        """Restore the last snapshot, stream-ordered after the work already enqueued."""
+        self.check(self.L.clrsdp_restore_state(self.h))
+
     def set_stream(self, stream_ptr: int):
         self.check(self.L.clrsdp_set_stream(self.h, C.c_void_p(stream_ptr)))
 

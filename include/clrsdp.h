@@ -234,6 +234,14 @@ int32_t clrsdp_set_exchange(clrsdp_handle* h, clrsdp_exchange_fn fn, void* ctx, 
 int32_t clrsdp_comm_unique_id(uint8_t* id);
 int32_t clrsdp_comm_init(clrsdp_handle* h, const uint8_t* id);
 
+/* Device-side snapshot of the iterate: clrsdp_save_state copies x, X, y, Y and the scalar
+ * slots into a buffer of the handle, clrsdp_restore_state copies them back; both are enqueued
+ * on the handle's stream (no host synchronisation), so a benchmark can replay a window of loop
+ * bodies indefinitely without converging into the fp64 breakdown regime.  (No reference
+ * counterpart; initial_solutions, MPMP.jl:613, restarts from the host.) */
+int32_t clrsdp_save_state(clrsdp_handle* h);
+int32_t clrsdp_restore_state(clrsdp_handle* h);
+
 /* Run all work on `stream` (a hipStream_t; NULL = the handle's own stream). */
 int32_t clrsdp_set_stream(clrsdp_handle* h, void* stream);
 void* clrsdp_get_stream(const clrsdp_handle* h);

@@ -343,3 +343,27 @@ def test_pipelined_loop_equals_synchronous(pk, words, maxit):
         assert all(np.array_equal(u, v) for bu, bv in zip(a[i], p[i]) for u, v in zip(bu, bv))
     assert np.array_equal(a[5], p[5]) and np.array_equal(a[6], p[6])
     assert a[7:10] == p[7:10]
+
+
+def test_save_restore_state_replays_bitwise(pk):
+    """clrsdp_save_state / clrsdp_restore_state: after a restore the same loop bodies give the
+    same log rows and iterates bit for bit (graph replay and eager enqueue alike)."""
+    cons, b = pk.synth(seed=4, J=3, delta=8, rank=1, n_y=5, m=1)
+    bi = pk.get_block_info(cons)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    dev = pk.DeviceSolver(cons, b, bi)
+    dev.set_state(*pk.initial_point(bi, 10.0, 10.0))
+    dev.initial_residuals(P)
+    for _ in range(3):
+        dev.iterate(P, False)
+    dev.save_state()
+    runs = []
+    for _ in range(2):
+        rows = [tuple(getattr(st, f) for f in ("mu", "alpha_p", "alpha_d", "p_obj", "d_obj", "P_err"))
+                for st in (dev.iterate(P, False) for _ in range(3))]
+        x, X, y, Y = dev.get_state()
+        runs.append((rows, x, y))
+        dev.restore_state()
+    dev.close()
+    assert runs[0][0] == runs[1][0]
+    assert np.array_equal(runs[0][1], runs[1][1]) and np.array_equal(runs[0][2], runs[1][2])
