@@ -262,12 +262,20 @@ struct MatPlan {  // potrf / eigmin
     if (eig_lds_bytes<T>(nmax) <= LDS_MAX) {
       const size_t lds = eig_lds_bytes<T>(nmax);
       static bool attr = false;
+      // CLRSDP_EIG_NEWTON=0 keeps the multi-word multisection from the fp64 bracket
+      static const bool newton = [] {
+        const char* e = std::getenv("CLRSDP_EIG_NEWTON");
+        return !(e && e[0] == '0');
+      }();
       if (!attr) {
-        HIPCHK(hipFuncSetAttribute((const void*)eigmin_lds<T>,
+        HIPCHK(hipFuncSetAttribute((const void*)eigmin_lds<T, true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX));
+        HIPCHK(hipFuncSetAttribute((const void*)eigmin_lds<T, false>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX));
         attr = true;
       }
-      eigmin_lds<T><<<(unsigned)h.size(), 512, lds, s>>>(d, out);
+      if (newton) eigmin_lds<T, true><<<(unsigned)h.size(), 512, lds, s>>>(d, out);
+      else eigmin_lds<T, false><<<(unsigned)h.size(), 512, lds, s>>>(d, out);
     } else {
       const size_t lds = sizeof(T) * (4 * (size_t)nmax + 256);
       eigmin_batched<T><<<(unsigned)h.size(), 256, lds, s>>>(d, out);

@@ -456,7 +456,7 @@ __device__ unsigned long long g_eig_stamps[8];
 #else
 #define EIG_STAMP(slot)
 #endif
-template <class T>
+template <class T, bool NEWTON = true>
 __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__ descs,
                                                   T* __restrict__ out) {
 #ifdef CLRSDP_EIG_STAMPS
@@ -657,6 +657,59 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     }
   }
   __syncthreads();
+  if constexpr (NEWTON && Num<T>::BITS > 120) {
+    // (2') quad-double: Newton on det(T - sigma I) from the fp64 centre (at dd the 11 parallel
+    // multisection rounds are as fast as the sequential Newton chain, so dd keeps them).  With the pivots of
+    // T - sigma I = L D L^T, q_i = (d_i - sigma) - e2_{i-1} / q_{i-1}, and s_i = dq_i/dsigma =
+    // -1 + e2_{i-1} s_{i-1} / q_{i-1}^2, the Newton step is 1 / sum_i s_i / q_i.  It converges
+    // quadratically from the fp64 estimate (3 steps for a simple eigenvalue, a 4th confirms).
+    // The result is accepted only if it converged AND two multi-word Sturm counts bracket it
+    // (no eigenvalue below sigma - delta, one at most sigma + delta, delta = 2^(12-BITS)
+    // magnitudes); otherwise the multisection below runs as before.
+    T* nres = Wv;  // free after the reduction: [0] = sigma
+    const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
+    if (tid == 0) {
+      T s = T(0.5 * (bnd[2] + bnd[3]));
+      const double tol = ldexp(mag, -(Num<T>::BITS + 2)) + 1e-300;
+      int conv = 0;
+      for (int it = 0; it < 4; ++it) {
+        T q = dg[0] - s;
+        if (q == T(0.0)) q = T(1e-300);
+        T r = T(1.0) / q, sd = T(-1.0), g = -r;
+        for (int i = 1; i < n; ++i) {
+          const T t = e2[i - 1] * r;
+          sd = (t * r) * sd - T(1.0);
+          q = (dg[i] - s) - t;
+          if (q == T(0.0)) q = T(1e-300);
+          r = T(1.0) / q;
+          g = g + sd * r;
+        }
+        const T step = T(1.0) / g;
+        s = s - step;
+        const double as = fabs(Num<T>::hi(step));
+        if (!(as == as)) break;  // NaN: leave conv = 0
+        if (as <= tol) { conv = 1; break; }
+      }
+      nres[0] = s;
+      masks[2] = (unsigned long long)conv;
+    }
+    __syncthreads();
+    const T s = nres[0];
+    const T dl = T(ldexp(mag, 12 - Num<T>::BITS) + 1e-300);
+    int c = 0;
+    if (tid == 0) c = masks[2] && sturm_count(dg, e2, n, s - dl) == 0;
+    if (tid == 64) c = sturm_count(dg, e2, n, s + dl) >= 1;
+    __syncthreads();
+    if (tid == 0 || tid == 64) masks[tid >> 6] = (unsigned long long)c;
+    __syncthreads();
+    const bool ok = masks[0] && masks[1];
+    __syncthreads();
+    if (ok) {
+      if (tid == 0) out[blockIdx.x] = s;
+      EIG_STAMP(6)
+      return;
+    }
+  }
   T lo = T(bnd[2]), hi = T(bnd[3]);
   // check the start bracket at full width: count(lo) == 0 and count(hi) >= 1
   {
@@ -686,6 +739,7 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     }
   }
   if (tid == 0) out[blockIdx.x] = (lo + hi) * T(0.5);
+  EIG_STAMP(6)
 }
 
 }  // namespace clrsdp
