@@ -537,7 +537,10 @@ struct Solver final : HandleBase {
     HIPCHK(hipStreamCreateWithFlags(&own_stream, hipStreamNonBlocking));
     stream = own_stream;
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
-    HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    // CLRSDP_ONE_STREAM=1: the side-stream work runs in order on the main stream (experiment:
+    // graph-boundary and join idle time against the lost overlap)
+    if (std::getenv("CLRSDP_ONE_STREAM")) aux = own_stream;
+    else HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
     for (hipEvent_t* e : {&ev_s, &ev_r, &ev_qa, &ev_q})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
@@ -568,7 +571,7 @@ struct Solver final : HandleBase {
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
       if (g) (void)hipGraphExecDestroy(g);
-    if (aux) (void)hipStreamDestroy(aux);
+    if (aux && aux != own_stream) (void)hipStreamDestroy(aux);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 
