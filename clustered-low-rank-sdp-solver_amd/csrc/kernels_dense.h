@@ -230,6 +230,46 @@ __device__ inline int sturm_count_fast(const double* dg, const double* e2, int n
   return cnt;
 }
 
+// The same count from the leading principal minors p_i = (d_i - sigma) p_{i-1} - e2_{i-1} p_{i-2}
+// (q_i = p_i / p_{i-1}, so q_i < 0 <=> the sign changes).  One dependent FMA per row instead of
+// a reciprocal and two Newton steps: e2_{i-1} p_{i-2} is formed a row ahead, off the chain.  The
+// pair (p_{i-1}, p_i) is rescaled by a power of two every 8 rows (exact, signs kept), so 8 rows of
+// growth must stay in range: every |d_i - sigma| + |e_i| is within twice the Gershgorin span.  A
+// zero minor becomes 2^-60 p_{i-1} (q_i = 2^-60 > 0: not counted, and the next q strongly
+// negative, as the 1e-300 substitute above).
+__device__ inline int sturm_count_prod(const double* dg, const double* e2, int n, double sigma) {
+  // row 0 is the recurrence with p_{-1} = 1 and e2_{-1} = 0; rows are taken 8 at a time with
+  // their 16 LDS reads issued ahead of the chain
+  double pm = 1.0, pc = 1.0;  // p_{i-2}, p_{i-1}
+  bool sc = false;
+  int cnt = 0;
+  for (int i0 = 0; i0 < n; i0 += 8) {
+    double dv[8], ev[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      dv[u] = dg[i0 + u];
+      ev[u] = (i0 + u == 0) ? 0.0 : e2[i0 + u - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (i0 + u < n) {
+        const double t = ev[u] * pm;
+        double pn = fma(dv[u] - sigma, pc, -t);
+        if (pn == 0.0) pn = pc * 0x1p-60;
+        const bool sn = pn < 0.0;
+        cnt += (sn != sc);
+        pm = pc;
+        pc = pn;
+        sc = sn;
+      }
+    }
+    const int ex = __builtin_amdgcn_frexp_exp(pc);
+    pc = __builtin_ldexp(pc, -ex);
+    pm = __builtin_ldexp(pm, -ex);
+  }
+  return cnt;
+}
+
 __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restrict__ descs,
                                                   double* __restrict__ out) {
   constexpr int NS = 16;
@@ -406,18 +446,38 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     } else {
       dg[0] = colb[0][0];
     }
-    double lo = 0.0, hi = 0.0;
-    for (int r = 0; r < n; ++r) {
+  }
+  __syncthreads();
+  // Gershgorin interval of the tridiagonal: row r in thread r (waves 0-1), wave min/max, then
+  // the two wave results through LDS (the masks words are free until the multisection)
+  {
+    double lo = INFINITY, hi = -INFINITY;
+    if (tid < n) {
       double rr = 0.0;
-      if (r > 0) rr += sqrt(e2[r - 1]);
-      if (r + 1 < n) rr += sqrt(e2[r]);
-      const double aa = dg[r] - rr, bb = dg[r] + rr;
-      if (r == 0 || aa < lo) lo = aa;
-      if (r == 0 || bb > hi) hi = bb;
+      if (tid > 0) rr += sqrt(e2[tid - 1]);
+      if (tid + 1 < n) rr += sqrt(e2[tid]);
+      lo = dg[tid] - rr;
+      hi = dg[tid] + rr;
     }
-    const double span = hi - lo;
-    bnd[0] = lo - span * 1e-3 - 1e-300;
-    bnd[1] = hi + span * 1e-3 + 1e-300;
+    if (w < 2) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o));
+        hi = fmax(hi, __shfl_xor(hi, o));
+      }
+      if (lane == 0) {
+        reinterpret_cast<double*>(masks)[2 * w] = lo;
+        reinterpret_cast<double*>(masks)[2 * w + 1] = hi;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double* m = reinterpret_cast<const double*>(masks);
+      const double l = fmin(m[0], m[2]), h = fmax(m[1], m[3]);
+      const double span = h - l;
+      bnd[0] = l - span * 1e-3 - 1e-300;
+      bnd[1] = h + span * 1e-3 + 1e-300;
+    }
   }
   __syncthreads();
   // ---- 512-way multisection: 6 rounds of 9 bits
@@ -425,7 +485,7 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
   for (int it = 0; it < 7; ++it) {
     const double width = hi - lo;
     const double sigma = lo + width * ((double)(tid + 1) / 513.0);
-    const int cnt = sturm_count_fast(dg, e2, n, sigma);
+    const int cnt = sturm_count_prod(dg, e2, n, sigma);
     const unsigned long long mk = __ballot(cnt >= 1);
     if (lane == 0) masks[w] = mk;
     __syncthreads();
