@@ -480,9 +480,10 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     }
   }
   __syncthreads();
-  // ---- 512-way multisection: 6 rounds of 9 bits
+  // ---- 512-way multisection: 6 rounds of 9 bits bracket lambda_min to 2^-54 of the Gershgorin
+  // span, below the Sturm count's own backward error (~n eps ||T||), so a 7th round adds noise
   double lo = bnd[0], hi = bnd[1];
-  for (int it = 0; it < 7; ++it) {
+  for (int it = 0; it < 6; ++it) {
     const double width = hi - lo;
     const double sigma = lo + width * ((double)(tid + 1) / 513.0);
     const int cnt = sturm_count_prod(dg, e2, n, sigma);
