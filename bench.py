@@ -3,9 +3,14 @@
 Workload (BASELINE.json configs[2], the north-star instance): synthetic clustered low-rank SDP,
 64 clusters x 128x128 blocks (m = 1, L = 1, delta = 128), rank-1 constraints, N = 255 samples per
 cluster, n_y = 128, fp64 -- SURVEY.md §8d "C3".  One step = one full predictor-corrector
-iteration (MPMP.jl:755-887) on device-resident data.  With --gpus N the clusters are sharded
-over N ranks (one process per GPU, cluster-balanced as MPMP.jl:425-465) and the cross-cluster
-reductions are all-gathered over RCCL: strong scaling of one fixed instance.
+iteration (MPMP.jl:755-887) on device-resident data.
+
+With --gpus N (one process per GPU, clusters balanced as MPMP.jl:425-465, the cross-cluster
+partials all-gathered over RCCL) the default is WEAK scaling: every GPU keeps one C3 shard of
+64 clusters, so the instance has J = 64 N clusters (n_y = 128 couples all of them) and `value` is
+N x its iterations/s, i.e. C3-shard iterations/s summed over the GPUs (at N = 1 exactly the C3
+iterations/s).  --scaling strong keeps J = 64 and shards it (8 clusters per GPU at N = 8); that
+regime is latency-bound by the per-block chains, so it is not the default.
 
 Also reported: the Schur-assembly roofline (its kernels timed with HIP events on the library's
 stream over the timed region) and a CPU baseline (the numpy restatement of the reference
@@ -128,6 +133,9 @@ def main():
                          "(pipelined; auto = pipelined when the clusters are sharded)")
     ap.add_argument("--clusters", type=int, default=0,
                     help="override J of the config (per-rank sizing experiments; not a bench line)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="N > 1: weak = one config-sized shard per GPU (J x N clusters), strong = "
+                         "the config's J sharded over the GPUs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,6 +148,9 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.clusters:
         cfg["J"] = args.clusters
+    weak = world > 1 and args.scaling == "weak" and "J" in cfg
+    if weak:
+        cfg["J"] *= world   # one config-sized shard of clusters per GPU
     if cfg.get("kind") == "sphere_packing_shape":
         cons, b = pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, seed=args.seed)
     else:
@@ -164,8 +175,15 @@ def main():
     dev.set_state(x0, X0, y0, Y0)
     dev.initial_residuals(prm)
 
-    def step(pd_feas=False):   # synchronous loop body (instrumented pass)
-        return dev.iterate(prm, pd_feas)
+    # check_pd_feasibility (MPMP.jl:949-953) with the thresholds set above, from the previous
+    # body's log row, as solverank1sdp's synchronous loop does
+    PTHR = DTHR = 1e-30
+    feas = [False]
+
+    def step():   # one synchronous loop body
+        st = dev.iterate(prm, feas[0])
+        feas[0] = max(st.p_err, st.P_err) < PTHR and st.d_err < DTHR
+        return st
 
     pipelined = args.loop == "pipelined" or (args.loop == "auto" and world > 1)
 
@@ -180,6 +198,7 @@ def main():
         count[0] += 1
         if count[0] % RESTART == 0:
             dev.restore_state()
+            feas[0] = False   # the snapshot is the (infeasible) initial point
 
     def run_bodies(n):
         """n loop bodies as solverank1sdp runs them: the host one body behind the device
@@ -239,6 +258,7 @@ def main():
         dist.close()
         return
     its = args.steps / dt
+    value = its * world if weak else its
     fl, by = schur_flops_bytes(bi, 8 * args.precision)
     if world > 1:
         fl /= world   # per-rank share of the Schur work (the roofline is per GPU)
@@ -249,14 +269,15 @@ def main():
     peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]
     res = {
         "metric": "interior-point iterations/sec (solverank1sdp loop body, MPMP.jl:755-887)",
-        "value": its,
+        "value": value,
         "unit": "iterations/s",
+        "instance_iterations_per_s": its,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if (weak or world == 1) else "strong",
         "vs_baseline": None,
         "dtype": DTYPES[args.precision],
         "data": "synthetic (seeded splitmix64 instance, SURVEY.md §8d)",
@@ -265,7 +286,9 @@ def main():
                                if "J" in cfg else
                                f"{args.config}: sphere-packing shape, J={bi.J} clusters, blocks "
                                f"{bi.Y_blocksizes}, dim_S {bi.dim_S}, n_y={bi.n_y}",
-                   "parallelism": f"clusters sharded over {world} GPU(s)" if world > 1 else "1 GPU"},
+                   "parallelism": (f"{cfg['J'] // world} clusters per GPU on {world} GPUs (weak: "
+                                   f"value = {world} x instance iterations/s)" if weak else
+                                   f"clusters sharded over {world} GPU(s)") if world > 1 else "1 GPU"},
         "roofline": {"bound": "mfma" if args.precision == 1 else "valu",
                      "kernel": "Schur assembly (stage SCHUR)",
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",

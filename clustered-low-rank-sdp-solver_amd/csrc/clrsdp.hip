@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -108,6 +109,17 @@ X* upload_vec(const std::vector<X>& v) {
 
 inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) applies to the current device only: `seen` is
+// the caller's per-kernel bitmask of the devices it was already set on
+inline void lds_attr_once(std::atomic<unsigned long long>& seen, const void* fn, int bytes) {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (seen.load(std::memory_order_acquire) & bit) return;
+  HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  seen.fetch_or(bit, std::memory_order_acq_rel);
+}
+
 // --------------------------------------------------------------------------------------------
 // launch plans: descriptor arrays built once at creation, replayed every iteration
 // --------------------------------------------------------------------------------------------
@@ -130,8 +142,25 @@ inline std::vector<TileRef> tile_major(const std::vector<int>& ntiles) {
   return out;
 }
 
+// the plans own their device descriptor arrays (freed with the plan; plans are never copied)
+struct PlanBase {
+  std::vector<void*> owned_dev;
+  PlanBase() = default;
+  PlanBase(const PlanBase&) = delete;
+  PlanBase& operator=(const PlanBase&) = delete;
+  ~PlanBase() {
+    for (void* p : owned_dev) (void)hipFree(p);
+  }
+  template <class X>
+  X* own(const std::vector<X>& v) {
+    X* p = upload_vec(v);
+    owned_dev.push_back(p);
+    return p;
+  }
+};
+
 template <class T>
-struct GemmPlan {
+struct GemmPlan : PlanBase {
   bool ta = false, tb = false;
   int tag = 0;  // 1: the Schur-stage V^T X^-1 / V^T Y launch (named separately in profiles)
   std::vector<GemmDesc<T>> h;
@@ -162,8 +191,8 @@ struct GemmPlan {
     if (gemv)  // one workgroup per 64 outputs
       for (size_t q = 0; q < h.size(); ++q) ntiles[q] = (int)cdiv(h[q].M, 64);
     t2d = tile_major(ntiles);
-    d = upload_vec(h);
-    dt = upload_vec(t2d);
+    d = own(h);
+    dt = own(t2d);
   }
   // C = alpha op(A) op(B) + beta Cin (+ dmult * *dscal on the diagonal of square problems)
   void launch(hipStream_t s, double alpha, double beta, const T* dscal = nullptr,
@@ -197,7 +226,7 @@ struct GemmPlan {
 };
 
 template <class T>
-struct TrsmPlan {
+struct TrsmPlan : PlanBase {
   static constexpr int NB = 16, NC = 64;
   std::vector<TrsmDesc<T>> h;
   std::vector<int> t2d;
@@ -216,8 +245,8 @@ struct TrsmPlan {
   }
   void finalize() {
     if (h.empty()) return;
-    d = upload_vec(h);
-    dt = upload_vec(t2d);
+    d = own(h);
+    dt = own(t2d);
   }
   void launch(hipStream_t s, bool trans) const {
     if (h.empty()) return;
@@ -230,7 +259,7 @@ struct TrsmPlan {
 };
 
 template <class T>
-struct MatPlan {  // potrf / eigmin
+struct MatPlan : PlanBase {  // potrf / eigmin
   static constexpr int NB = 16;
   std::vector<MatDesc<T>> h;
   MatDesc<T>* d = nullptr;
@@ -242,7 +271,7 @@ struct MatPlan {  // potrf / eigmin
     nmax = std::max(nmax, n);
   }
   void finalize() {
-    if (!h.empty()) d = upload_vec(h);
+    if (!h.empty()) d = own(h);
   }
   void potrf(hipStream_t s, int* info) const {
     if (h.empty()) return;
@@ -261,19 +290,14 @@ struct MatPlan {  // potrf / eigmin
     }
     if (eig_lds_bytes<T>(nmax) <= LDS_MAX) {
       const size_t lds = eig_lds_bytes<T>(nmax);
-      static bool attr = false;
+      static std::atomic<unsigned long long> attr_t{0}, attr_f{0};
       // CLRSDP_EIG_NEWTON=0 keeps the multi-word multisection from the fp64 bracket
       static const bool newton = [] {
         const char* e = std::getenv("CLRSDP_EIG_NEWTON");
         return !(e && e[0] == '0');
       }();
-      if (!attr) {
-        HIPCHK(hipFuncSetAttribute((const void*)eigmin_lds<T, true>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX));
-        HIPCHK(hipFuncSetAttribute((const void*)eigmin_lds<T, false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX));
-        attr = true;
-      }
+      lds_attr_once(attr_t, (const void*)eigmin_lds<T, true>, (int)LDS_MAX);
+      lds_attr_once(attr_f, (const void*)eigmin_lds<T, false>, (int)LDS_MAX);
       if (newton) eigmin_lds<T, true><<<(unsigned)h.size(), 512, lds, s>>>(d, out);
       else eigmin_lds<T, false><<<(unsigned)h.size(), 512, lds, s>>>(d, out);
     } else {
@@ -286,7 +310,7 @@ struct MatPlan {  // potrf / eigmin
 
 
 template <class T>
-struct CholInvPlan {  // A_b -> L_b^-1 (and optionally L_b)
+struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
   std::vector<MatDesc<T>> hin, hout, hl;
   MatDesc<T>*din = nullptr, *dout = nullptr, *dl = nullptr;
   void add(T* A, int n, int lda, T* out, int ldo, T* L = nullptr) {
@@ -297,9 +321,9 @@ struct CholInvPlan {  // A_b -> L_b^-1 (and optionally L_b)
   }
   void finalize() {
     if (hin.empty()) return;
-    din = upload_vec(hin);
-    dout = upload_vec(hout);
-    if (!hl.empty()) dl = upload_vec(hl);
+    din = own(hin);
+    dout = own(hout);
+    if (!hl.empty()) dl = own(hl);
   }
   int nmax = 0;
   void launch(hipStream_t s, int* info) const {
@@ -317,12 +341,8 @@ struct CholInvPlan {  // A_b -> L_b^-1 (and optionally L_b)
   }
   template <int NP>
   void go(hipStream_t s, unsigned nb, int* info) const {
-    static bool attr = false;
-    if (!attr) {
-      HIPCHK(hipFuncSetAttribute((const void*)chol_inv_mfma<NP>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX));
-      attr = true;
-    }
+    static std::atomic<unsigned long long> attr{0};
+    lds_attr_once(attr, (const void*)chol_inv_mfma<NP>, (int)LDS_MAX);
     chol_inv_mfma<NP><<<nb, 512, chol_inv_mfma_lds<NP>(), s>>>(
         reinterpret_cast<const MatDesc<double>*>(din), reinterpret_cast<const MatDesc<double>*>(dout), info);
   }
@@ -400,6 +420,7 @@ struct Solver final : HandleBase {
   bool res_from_copy = false;
 
   // ---------------- plans
+  PlanBase descs;  // owner of the stage descriptor arrays below (d_blk, d_pair, ...)
   GemmPlan<T> p_XY, p_dXdY, p_xinv, p_s1x, p_s1y, p_s2x, p_s2y, p_Q, p_wA_P, p_wA_dX, p_trU_Z,
       p_trU_Y, p_By, p_Btx, p_Wt, p_Wdy, p_PY, p_Z, p_dXY, p_dY;
   TrsmPlan<T> t_Linv, t_W, t_t, t_Q, t_sX1, t_sX2, t_sY1, t_sY2;
@@ -739,9 +760,9 @@ struct Solver final : HandleBase {
     for (const LBlk& b : lb) ci_XY.add(Y + b.off, b.n, b.n, LY + b.off, b.n);
     for (const LBlk& b : lb) e_XY.add(tC + b.off, b.n, b.n);
     n_blk_m = (int)bdm.size();
-    d_blk = upload_vec(bd);
-    if (n_blk_m) d_blk_m = upload_vec(bdm);
-    d_ayd = upload_vec(ayd);
+    d_blk = descs.own(bd);
+    if (n_blk_m) d_blk_m = descs.own(bdm);
+    d_ayd = descs.own(ayd);
     n_pair = (int)pd.size();
     // tuples <-> columns 1:1 in every local cluster (m = L = 1, every rank 1): fused trace_A
     trivial_tuples = n_pair > 0;
@@ -757,8 +778,8 @@ struct Solver final : HandleBase {
         pi += 1;
       }
     }
-    d_pair = upload_vec(pd);
-    d_scale = upload_vec(sd);
+    d_pair = descs.own(pd);
+    d_scale = descs.own(sd);
     // per cluster plans
     std::vector<SchurClusterDesc> scd;
     std::vector<SchurBlockDesc> sbd;
@@ -836,12 +857,12 @@ struct Solver final : HandleBase {
     q_qinv.add(Qf, (int)n_y, Qf, (int)n_y, nullptr, 0, Qinv, (int)n_y, (int)n_y, (int)n_y, (int)n_y);
     q_qdy.add(Qinv, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
     n_zero = (int)zr.size();
-    if (n_zero) d_zero = upload_vec(zr);
+    if (n_zero) d_zero = descs.own(zr);
     if (nc()) {
-      d_scd = upload_vec(scd);
-      d_sbd = upload_vec(sbd);
-      d_td = upload_vec(td);
-      d_tb = upload_vec(tbk);
+      d_scd = descs.own(scd);
+      d_sbd = descs.own(sbd);
+      d_td = descs.own(td);
+      d_tb = descs.own(tbk);
     }
     if (fast_schur) build_fast_schur();
     for (GemmPlan<T>* g : {&p_txy, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
@@ -900,9 +921,9 @@ struct Solver final : HandleBase {
       }
       const std::vector<TileRef> pt2d = tile_major(pnt);
       n_ptiles = (int)pt2d.size();
-      if (n_ptiles) { d_ptd = upload_vec(ptd); d_pt2d = upload_vec(pt2d); }
+      if (n_ptiles) { d_ptd = descs.own(ptd); d_pt2d = descs.own(pt2d); }
       n_gsum = (int)gcd.size();
-      if (n_gsum) d_gcd = upload_vec(gcd);
+      if (n_gsum) d_gcd = descs.own(gcd);
     }
   }
 
@@ -1049,11 +1070,15 @@ struct Solver final : HandleBase {
     return p;
   }
   void set_control(const clrsdp_control* c) override {
+    if (inflight) throw ClrsdpError{CLRSDP_E_STATE, "set_control with loop bodies in flight"};
     gap_thr = limbs(c->duality_gap_threshold);
     p_thr = limbs(c->primal_error_threshold);
     d_thr = limbs(c->dual_error_threshold);
     need_p = c->need_primal_feasible != 0;
     need_d = c->need_dual_feasible != 0;
+    // the thresholds travel by value in the ScalarParams of the captured scalar launches, so
+    // every graph captured with the previous ones is stale
+    drop_graphs();
   }
   bool zero_cy = false, zero_info = false;
   // ---- scalar slots + status words: one device block, one pinned host mirror
@@ -1551,6 +1576,14 @@ struct Solver final : HandleBase {
   // the replayed graph as well
   bool graph_rccl = std::getenv("CLRSDP_GRAPH_RCCL") != nullptr;
   bool graph_ok() const { return use_graph && !timing && (world == 1 || (comm && graph_rccl)); }
+  // forget every captured loop body (they are re-captured on their next use)
+  void drop_graphs() {
+    for (hipGraphExec_t& g : gexec)
+      if (g) {
+        HIPCHK(hipGraphExecDestroy(g));
+        g = nullptr;
+      }
+  }
   void launch_graph(const clrsdp_params* prm, int pd_feas) {
     const int g = pd_feas < 0 ? 2 + (graph_launches++ & 1) : (pd_feas ? 1 : 0);
     if (!gexec[g] || std::memcmp(&gprm[g], prm, sizeof(*prm)) != 0) {
@@ -1732,16 +1765,115 @@ struct Solver final : HandleBase {
                               stream));
     HIPCHK(hipStreamSynchronize(stream));
     // graphs captured before carry no all-gathers
-    for (hipGraphExec_t& g : gexec)
-      if (g) {
-        HIPCHK(hipGraphExecDestroy(g));
-        g = nullptr;
-      }
+    drop_graphs();
   }
   void set_stream(void* s) override { stream = s ? reinterpret_cast<hipStream_t>(s) : own_stream; }
   void* get_stream() const override { return (void*)stream; }
   void synchronize() override { HIPCHK(hipStreamSynchronize(stream)); }
 };
+
+// Stand-alone compute_step_length (MPMP.jl:1829-1898) of a block-diagonal pair (M, dM), fp64:
+// the same kernels as STAGE_STEP (L^-1 on chip and two MFMA products for blocks <= 128, potrf +
+// two triangular solves above), then lambda_min per block and alpha.
+struct DevBuf {
+  std::vector<void*> p;
+  ~DevBuf() {
+    for (void* q : p) (void)hipFree(q);
+  }
+  template <class X>
+  X* alloc(size_t n) {
+    X* q = dmalloc<X>(n);
+    p.push_back(q);
+    return q;
+  }
+};
+
+int step_length_f64(int device, int64_t nblk, const int64_t* n, const double* Mh, const double* dMh,
+                    double gamma, double* alpha, double* min_eig, std::string& err) {
+  HIPCHK(hipSetDevice(device));
+  std::vector<int64_t> off(nblk + 1, 0);
+  int nmax = 0;
+  for (int64_t b = 0; b < nblk; ++b) {
+    if (n[b] <= 0 || n[b] > 4096) throw ClrsdpError{CLRSDP_E_ARG, "block size out of range"};
+    off[b + 1] = off[b] + n[b] * n[b];
+    nmax = std::max(nmax, (int)n[b]);
+  }
+  const int64_t tot = off[nblk];
+  DevBuf mem;
+  double* M = mem.alloc<double>(tot);
+  double* dM = mem.alloc<double>(tot);
+  double* L = mem.alloc<double>(tot);
+  double* t1 = mem.alloc<double>(tot);
+  double* t2 = mem.alloc<double>(tot);
+  double* eig = mem.alloc<double>(nblk);
+  int* info = mem.alloc<int>(nblk);
+  HIPCHK(hipDeviceSynchronize());  // the zero fills (null stream) before the copies below
+  HIPCHK(hipMemcpy(M, Mh, tot * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dM, dMh, tot * sizeof(double), hipMemcpyHostToDevice));
+  CholInvPlan<double> ci;
+  GemmPlan<double> g1, g2;
+  g2.tb = true;
+  MatPlan<double> fac, eg;
+  TrsmPlan<double> s1, s2;
+  std::vector<BlkDesc> big;
+  for (int64_t b = 0; b < nblk; ++b) {
+    const int nb = (int)n[b];
+    const int64_t o = off[b];
+    if (nb <= 128) {
+      ci.add(M + o, nb, nb, L + o, nb);                                    // L <- L_M^-1
+      g1.add(L + o, nb, dM + o, nb, nullptr, nb, t1 + o, nb, nb, nb, nb);  // t1 = L^-1 dM
+      g2.add(t1 + o, nb, L + o, nb, nullptr, nb, t2 + o, nb, nb, nb, nb);  // t2 = t1 L^-T
+    } else {
+      fac.add(L + o, nb, nb);          // L <- chol(M)
+      s1.add(L + o, nb, t1 + o, nb, nb, nb);
+      s2.add(L + o, nb, t2 + o, nb, nb, nb);
+      big.push_back(BlkDesc{o, nb, 0});
+    }
+    eg.add(t2 + o, nb, nb);
+  }
+  ci.finalize(); g1.finalize(); g2.finalize(); fac.finalize(); eg.finalize();
+  s1.finalize(); s2.finalize();
+  PlanBase bd_owner;
+  BlkDesc* d_big = big.empty() ? nullptr : bd_owner.own(big);
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  struct StreamGuard { hipStream_t s; ~StreamGuard() { (void)hipStreamDestroy(s); } } sg{s};
+  ci.launch(s, info);
+  g1.launch(s, 1.0, 0.0);
+  g2.launch(s, 1.0, 0.0);
+  if (!big.empty()) {
+    for (size_t q = 0; q < big.size(); ++q) {
+      const int64_t o = big[q].off, nn = (int64_t)big[q].n * big[q].n;
+      HIPCHK(hipMemcpyAsync(L + o, M + o, nn * sizeof(double), hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipMemcpyAsync(t1 + o, dM + o, nn * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    // the chol-inverse launch wrote info[0 .. #small); the potrf flags follow
+    fac.potrf(s, info + ci.hin.size());
+    s1.launch(s, false);                                             // t1 = L^-1 dM
+    blk_sym2<double><<<dim3((unsigned)big.size(), 32), 128, 0, s>>>(d_big, t2, t1, 2);  // t2 = t1^T
+    s2.launch(s, false);                                             // t2 = L^-1 dM^T L^-T
+  }
+  eg.eigmin(s, eig);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<int> hinfo(nblk);
+  std::vector<double> he(nblk);
+  HIPCHK(hipMemcpy(hinfo.data(), info, nblk * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(he.data(), eig, nblk * sizeof(double), hipMemcpyDeviceToHost));
+  for (int64_t b = 0; b < nblk; ++b)
+    if (hinfo[b]) {
+      err = "The step length could not be calculated correctly (M not positive definite).";
+      return CLRSDP_E_STEP;
+    }
+  // the eigen kernels run in the (j,l) order of the plan: small blocks and large ones alike
+  double mn = INFINITY;
+  for (int64_t b = 0; b < nblk; ++b) {
+    if (min_eig) min_eig[b] = he[b];
+    mn = std::min(mn, he[b]);
+  }
+  *alpha = (mn > -gamma) ? 1.0 : -gamma / mn;  // MPMP.jl:1893-1897
+  return CLRSDP_OK;
+}
 
 }  // namespace
 
@@ -1895,6 +2027,23 @@ int32_t clrsdp_save_state(clrsdp_handle* h) {
 int32_t clrsdp_restore_state(clrsdp_handle* h) {
   if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
   GUARD(h, { h->impl->restore_state(); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_step_length(int32_t device, int64_t nblocks, const int64_t* n, const double* M,
+                           const double* dM, double gamma, double* alpha, double* min_eig) {
+  if (nblocks <= 0 || !n || !M || !dM || !alpha) { g_last_error = "null argument or no blocks"; return CLRSDP_E_ARG; }
+  try {
+    std::string err;
+    const int rc = step_length_f64(device, nblocks, n, M, dM, gamma, alpha, min_eig, err);
+    if (rc) g_last_error = err;
+    return rc;
+  } catch (const ClrsdpError& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return CLRSDP_E_HIP;
+  }
 }
 
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on) {

@@ -304,7 +304,29 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
       const double v = (gload(d.A + ic + (size_t)jc * lda) + gload(d.A + jc + (size_t)ic * lda)) * 0.5;
       a[s][e] = (rowok && j < n) ? v : 0.0;
     }
-#define EIG_SHIFT_SLOTS()                                                    \
+  // scale the block by 2^-ex0 so that its largest entry lies in [0.5, 1): the column norms of the
+  // Householder reduction neither overflow nor underflow for any block norm in fp64 range (exact,
+  // undone on the result)
+  int ex0 = 0;
+  {
+    double amax = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) amax = fmax(amax, fmax(fabs(a[s][0]), fabs(a[s][1])));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
+    if (lane == 0) redw[w] = amax;
+    __syncthreads();
+    amax = redw[0];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) amax = fmax(amax, redw[r]);
+    ex0 = (amax > 0.0 && amax < INFINITY) ? __builtin_amdgcn_frexp_exp(amax) : 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      a[s][0] = __builtin_ldexp(a[s][0], -ex0);
+      a[s][1] = __builtin_ldexp(a[s][1], -ex0);
+    }
+  }
+#define EIG_SHIFT_SLOTS()                                                 \
   do {                                                                       \
     _Pragma("unroll") for (int s = 0; s + 1 < NS; ++s) {                     \
       a[s][0] = a[s + 1][0];                                                 \
@@ -450,6 +472,7 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
   __syncthreads();
   // Gershgorin interval of the tridiagonal: row r in thread r (waves 0-1), wave min/max, then
   // the two wave results through LDS (the masks words are free until the multisection)
+  int bnd_ex = 0;
   {
     double lo = INFINITY, hi = -INFINITY;
     if (tid < n) {
@@ -471,12 +494,25 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
       }
     }
     __syncthreads();
+    // every thread forms the interval; the tridiagonal is then scaled by 2^-ex so that the
+    // interval lies in [-1, 1]: every |d_i - sigma| <= 2 and e_i <= 1, so 8 rows of minors grow
+    // by at most 3^8 and sturm_count_prod cannot overflow whatever the norm of the block (a
+    // power-of-two scaling is exact and leaves every Sturm count unchanged)
+    const double* m = reinterpret_cast<const double*>(masks);
+    const double l = fmin(m[0], m[2]), h = fmax(m[1], m[3]);
+    const double mag = fmax(fabs(l), fabs(h));
+    const int ex = (mag > 0.0 && mag < INFINITY) ? __builtin_amdgcn_frexp_exp(mag) : 0;
+    bnd_ex = ex;
+    __syncthreads();
+    if (tid < n) {
+      dg[tid] = __builtin_ldexp(dg[tid], -ex);
+      e2[tid] = __builtin_ldexp(e2[tid], -2 * ex);
+    }
     if (tid == 0) {
-      const double* m = reinterpret_cast<const double*>(masks);
-      const double l = fmin(m[0], m[2]), h = fmax(m[1], m[3]);
-      const double span = h - l;
-      bnd[0] = l - span * 1e-3 - 1e-300;
-      bnd[1] = h + span * 1e-3 + 1e-300;
+      const double ls = __builtin_ldexp(l, -ex), hs = __builtin_ldexp(h, -ex);
+      const double span = hs - ls;
+      bnd[0] = ls - span * 1e-3 - 1e-300;
+      bnd[1] = hs + span * 1e-3 + 1e-300;
     }
   }
   __syncthreads();
@@ -502,7 +538,7 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     }
   }
   ER_STAMP(5)
-  if (tid == 0) out[blockIdx.x] = (lo + hi) * 0.5;
+  if (tid == 0) out[blockIdx.x] = __builtin_ldexp((lo + hi) * 0.5, bnd_ex + ex0);
 #undef ER_STAMP
 }
 

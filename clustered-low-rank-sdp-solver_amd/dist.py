@@ -91,8 +91,12 @@ class RcclExchange:
 
     torch.distributed (gloo, host side) is only the control plane: it broadcasts rank 0's RCCL
     unique id and provides the benchmark's barrier and max-over-ranks.  Every exchange of the
-    loop body is an ncclAllGather the library issues on its stream, so the loop body is captured
-    and replayed as one hipGraph at any world size, with no Python in the data path."""
+    loop body is an ncclAllGather the library issues on its stream, with no Python in the data
+    path.  At world size > 1 the loop body is enqueued eagerly from C++ (the pipelined host loop
+    hides the enqueue); only CLRSDP_GRAPH_RCCL=1 captures the all-gathers into the replayed
+    hipGraph.  The one-rank case (graph-captured, in place) is tested on the GPU box; across
+    distinct GPUs this path runs only in the driver's multi-GPU bench (the box has one GPU and
+    RCCL refuses two ranks on one device), so it is correct by construction, not by test."""
 
     def __init__(self, local_rank: int):
         import torch

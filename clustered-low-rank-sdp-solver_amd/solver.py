@@ -248,7 +248,8 @@ class DeviceSolver:
     def comm_init(self, uid: bytes):
         """Attach the native RCCL communicator (clrsdp_comm_init): every rank passes the id rank 0
         got from :func:`comm_unique_id`; the exchanges are then all-gathers issued by the
-        library on its stream, captured into the replayed loop-body graph."""
+        library on its stream.  With one rank they are captured into the replayed loop-body
+        graph; with more ranks the body is enqueued eagerly unless CLRSDP_GRAPH_RCCL=1."""
         if len(uid) != _lib.COMM_ID_BYTES:
             raise ValueError("RCCL unique id must be %d bytes" % _lib.COMM_ID_BYTES)
         self.check(self.L.clrsdp_comm_init(self.h, bytes(uid)))
@@ -264,6 +265,40 @@ def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(_lib.COMM_ID_BYTES)
     _lib.check(_lib.lib().clrsdp_comm_unique_id(buf))
     return buf.raw
+
+
+def compute_step_length(M, dM, gamma, device: int = 0, return_eigs: bool = False):
+    """compute_step_length(M, dM, gamma, blockinfo) of MPMP.jl:1829-1898 on the GPU (fp64,
+    clrsdp_step_length): ``min(1, -gamma / lambda_min)`` over the blocks of L^-1 dM L^-T with
+    M = L L^T.  ``M`` and ``dM`` are nested block lists (as X/Y) or flat lists of square
+    arrays.  Returns ``(alpha, bigfloat_steplength)`` as the reference does (the flag is always
+    False: there is no ball-arithmetic fallback), plus the per-block lambda_min with
+    ``return_eigs``.  Raises ClrsdpError(E_STEP) when a block of M is not positive definite."""
+    def flat(blocks):
+        out = []
+        for b in blocks:
+            if isinstance(b, (list, tuple)):
+                out.extend(flat(b))
+            else:
+                out.append(np.asarray(b, dtype=np.float64))
+        return out
+    Mb, dMb = flat(M), flat(dM)
+    if len(Mb) != len(dMb) or not Mb:
+        raise ValueError("M and dM need the same non-empty block structure")
+    for a, b in zip(Mb, dMb):
+        if a.ndim != 2 or a.shape[0] != a.shape[1] or a.shape != b.shape:
+            raise ValueError("blocks must be square and M, dM blocks of equal size")
+    n = np.array([a.shape[0] for a in Mb], dtype=np.int64)
+    Mf = np.concatenate([a.ravel(order="F") for a in Mb])
+    dMf = np.concatenate([b.ravel(order="F") for b in dMb])
+    alpha = C.c_double(0.0)
+    eig = np.zeros(len(Mb))
+    _lib.check(_lib.lib().clrsdp_step_length(device, len(Mb), n.ctypes.data_as(_lib.P_i64),
+                                              _ptr(Mf), _ptr(dMf), float(gamma), C.byref(alpha),
+                                              _ptr(eig)))
+    if return_eigs:
+        return alpha.value, False, eig
+    return alpha.value, False
 
 
 def initial_point(bi: BlockInfo, omega_p, omega_d):

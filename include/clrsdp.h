@@ -254,6 +254,15 @@ int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on);
 
 int32_t clrsdp_destroy(clrsdp_handle* h);
 
+/* Stand-alone step length of a block-diagonal pair, fp64 (replaces compute_step_length,
+ * MPMP.jl:1829-1898, without a handle): M_b = L_b L_b^T and lambda_b = lambda_min(L_b^-1 dM_b
+ * L_b^-T) per block, then *alpha = 1 if min_b lambda_b > -gamma, else -gamma / min_b lambda_b
+ * (1893-1897).  The nblocks blocks of sizes n[] are concatenated column-major in M and dM (host
+ * memory); min_eig (may be NULL) receives the nblocks lambda_b.  CLRSDP_E_STEP when some M_b is
+ * not positive definite (cho! fails, 1846-1848 / 1882). */
+int32_t clrsdp_step_length(int32_t device, int64_t nblocks, const int64_t* n, const double* M,
+                           const double* dM, double gamma, double* alpha, double* min_eig);
+
 #ifdef __cplusplus
 }
 #endif

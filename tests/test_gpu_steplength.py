@@ -1,0 +1,99 @@
+"""Step length (compute_step_length, MPMP.jl:1829-1898) through clrsdp_step_length, and the
+loop-control thresholds of a reused handle.
+
+Tolerance: lambda_min agrees with numpy.linalg.eigvalsh of the symmetrised L^-1 dM L^-T to
+1e-12 of the block's spectral radius (the Sturm multisection stops at 2^-54 of the Gershgorin
+span; Householder tridiagonalisation is backward stable to ~n eps ||T||).
+"""
+import numpy as np
+import pytest
+
+from helpers import rand_spd
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-12
+
+
+def _sym(rng, n):
+    G = rng.standard_normal((n, n))
+    return (G + G.T) / 2
+
+
+def _ref_eigs(M, dM):
+    out = []
+    for a, b in zip(M, dM):
+        L = np.linalg.cholesky(a)
+        T = np.linalg.solve(L, np.linalg.solve(L, b).T)
+        out.append(np.linalg.eigvalsh((T + T.T) / 2)[0])
+    return np.array(out)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e40, 1e-40, 1e200, 1e-200])
+@pytest.mark.parametrize("n", [5, 37, 127])
+def test_eigmin_scaled_blocks(pk, n, scale):
+    """M = I, dM = scale * G: lambda_min of blocks of very large or very small norm, n not a
+    multiple of 8 (the register eigen-solver rescales the tridiagonal before its Sturm counts;
+    without that the product-form counts overflowed near a span of 1e37)."""
+    from clrsdp_amd.solver import compute_step_length
+    rng = np.random.default_rng(n)
+    dM = [_sym(rng, n) * scale for _ in range(3)]
+    M = [np.eye(n) for _ in range(3)]
+    alpha, flag, eig = compute_step_length(M, dM, 0.7, return_eigs=True)
+    ref = _ref_eigs(M, dM)
+    rad = np.array([np.max(np.abs(np.linalg.eigvalsh(b))) for b in dM])
+    assert np.all(np.abs(eig - ref) <= TOL * rad), (eig, ref)
+    mn = ref.min()
+    ref_alpha = 1.0 if mn > -0.7 else -0.7 / mn
+    assert abs(alpha - ref_alpha) <= 1e-10 * abs(ref_alpha)
+    assert flag is False
+
+
+@pytest.mark.parametrize("sizes", [[1, 2, 18, 16, 9, 8], [64, 128], [130], [140, 33], [200]])
+def test_step_length_against_oracle(pk, oracle, sizes):
+    """Random SPD M and symmetric dM over mixed block sizes (the register path for n <= 128,
+    the LDS and global eigen-solvers and potrf + trsm above): alpha and every lambda_min against
+    the oracle's restatement (Cholesky, two triangular solves, eigenvalues)."""
+    from clrsdp_amd.solver import compute_step_length
+    rng = np.random.default_rng(sum(sizes))
+    M = [rand_spd(n, rng, 0.5) for n in sizes]
+    dM = [_sym(rng, n) for n in sizes]
+    alpha, _, eig = compute_step_length(M, dM, 0.7, return_eigs=True)
+    ref = _ref_eigs(M, dM)
+    rad = np.array([np.max(np.abs(np.linalg.eigvalsh(np.linalg.solve(np.linalg.cholesky(a), np.linalg.solve(np.linalg.cholesky(a), b).T)))) for a, b in zip(M, dM)])
+    assert np.all(np.abs(eig - ref) <= 1e-11 * rad), (eig, ref)
+    ar = oracle.Fp64()
+    bi = type("BI", (), {"J": len(sizes), "L": [1] * len(sizes)})()
+    a_or = ar.num(oracle.compute_step_length(ar, [[m] for m in M], [[d] for d in dM], 0.7, bi))
+    assert abs(alpha - float(a_or)) <= 1e-10 * abs(float(a_or))
+
+
+def test_step_length_not_pd(pk):
+    from clrsdp_amd import _lib
+    from clrsdp_amd.solver import compute_step_length
+    M = [np.eye(4), -np.eye(6)]
+    dM = [np.eye(4), np.eye(6)]
+    with pytest.raises(_lib.ClrsdpError) as e:
+        compute_step_length(M, dM, 0.7)
+    assert e.value.code == _lib.E_STEP
+
+
+def test_reused_handle_new_thresholds(pk):
+    """Two pipelined solves on one handle with different duality_gap_threshold: the second
+    stops where a fresh handle stops (the loop-body graphs carry the thresholds by value, so
+    clrsdp_set_control must drop them)."""
+    cons, b = pk.synth(J=3, delta=5, rank=1, n_y=4, seed=7)
+    bi = pk.get_block_info(cons)
+    kw = dict(omega_p=10.0, omega_d=10.0, primal_error_threshold=1e-6, dual_error_threshold=1e-6,
+              maxiterations=100, verbose=False, return_info=True, pipelined=True)
+    dev = pk.DeviceSolver(cons, b, bi)
+    try:
+        first = pk.solverank1sdp(cons, b, bi, solver=dev, duality_gap_threshold=1e-2, **kw)
+        second = pk.solverank1sdp(cons, b, bi, solver=dev, duality_gap_threshold=1e-7, **kw)
+    finally:
+        dev.close()
+    fresh = pk.solverank1sdp(cons, b, bi, duality_gap_threshold=1e-7, **kw)
+    assert first[-1].status == second[-1].status == fresh[-1].status == "terminated"
+    assert first[-1].iterations < second[-1].iterations
+    assert second[-1].iterations == fresh[-1].iterations
+    assert [r[2:] for r in second[-1].log] == [r[2:] for r in fresh[-1].log]
