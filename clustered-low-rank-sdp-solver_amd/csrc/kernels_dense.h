@@ -230,44 +230,39 @@ __device__ inline int sturm_count_fast(const double* dg, const double* e2, int n
   return cnt;
 }
 
-// The same count from the leading principal minors p_i = (d_i - sigma) p_{i-1} - e2_{i-1} p_{i-2}
-// (q_i = p_i / p_{i-1}, so q_i < 0 <=> the sign changes).  One dependent FMA per row instead of
-// a reciprocal and two Newton steps: e2_{i-1} p_{i-2} is formed a row ahead, off the chain.  The
-// pair (p_{i-1}, p_i) is rescaled by a power of two every 8 rows (exact, signs kept), so 8 rows of
-// growth must stay in range: every |d_i - sigma| + |e_i| is within twice the Gershgorin span.  A
-// zero minor becomes 2^-60 p_{i-1} (q_i = 2^-60 > 0: not counted, and the next q strongly
-// negative, as the 1e-300 substitute above).
-__device__ inline int sturm_count_prod(const double* dg, const double* e2, int n, double sigma) {
-  // row 0 is the recurrence with p_{-1} = 1 and e2_{-1} = 0; rows are taken 8 at a time with
-  // their 16 LDS reads issued ahead of the chain
-  double pm = 1.0, pc = 1.0;  // p_{i-2}, p_{i-1}
-  bool sc = false;
-  int cnt = 0;
-  for (int i0 = 0; i0 < n; i0 += 8) {
+// Is lambda_min < sigma?  The multisection only needs "count >= 1", and with p_0 = 1 > 0 the
+// Sturm sequence of leading principal minors has a sign change iff some minor is negative, so
+// the count becomes an OR of sign bits: per row one FMA on the chain (e_{i-1} p_{i-2} is formed a
+// row ahead), one subtraction, one multiplication and one integer OR; no compares, selects or
+// branches.  sd/se are the padded arrays of eigmin_reg (nr a multiple of 8, se[i] = e2_{i-1} > 0
+// inside the matrix, so a zero minor is followed by a nonzero one of the opposite sign of its
+// predecessor and the sign test stays exact); (p_{i-1}, p_i) is rescaled by a power of two every
+// 8 rows.
+__device__ inline bool sturm_any_below(const double* __restrict__ sd, const double* __restrict__ se,
+                                       int nr, double sigma) {
+  double pm = 0.0, pc = 1.0;
+  int acc = 0;
+  for (int i0 = 0; i0 < nr; i0 += 8) {
     double dv[8], ev[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      dv[u] = dg[i0 + u];
-      ev[u] = (i0 + u == 0) ? 0.0 : e2[i0 + u - 1];
+    for (int u = 0; u < 8; u += 2) {
+      const double2 a = *reinterpret_cast<const double2*>(sd + i0 + u);
+      const double2 b = *reinterpret_cast<const double2*>(se + i0 + u);
+      dv[u] = a.x; dv[u + 1] = a.y;
+      ev[u] = b.x; ev[u + 1] = b.y;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      if (i0 + u < n) {
-        const double t = ev[u] * pm;
-        double pn = fma(dv[u] - sigma, pc, -t);
-        if (pn == 0.0) pn = pc * 0x1p-60;
-        const bool sn = pn < 0.0;
-        cnt += (sn != sc);
-        pm = pc;
-        pc = pn;
-        sc = sn;
-      }
+      const double pn = fma(dv[u] - sigma, pc, -(ev[u] * pm));
+      acc |= __double2hiint(pn);
+      pm = pc;
+      pc = pn;
     }
     const int ex = __builtin_amdgcn_frexp_exp(pc);
     pc = __builtin_ldexp(pc, -ex);
     pm = __builtin_ldexp(pm, -ex);
   }
-  return cnt;
+  return acc < 0;
 }
 
 __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restrict__ descs,
@@ -286,6 +281,7 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
   __shared__ __attribute__((aligned(16))) double pb[256];
   __shared__ double redw[8];
   __shared__ double dg[128], e2[128];
+  __shared__ __attribute__((aligned(16))) double sd[128], se[128];
   __shared__ double bnd[2];
   __shared__ unsigned long long masks[8];
   const MatDesc<double> d = descs[blockIdx.x];
@@ -496,17 +492,20 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     __syncthreads();
     // every thread forms the interval; the tridiagonal is then scaled by 2^-ex so that the
     // interval lies in [-1, 1]: every |d_i - sigma| <= 2 and e_i <= 1, so 8 rows of minors grow
-    // by at most 3^8 and sturm_count_prod cannot overflow whatever the norm of the block (a
+    // by at most 3^8 and sturm_any_below cannot overflow whatever the norm of the block (a
     // power-of-two scaling is exact and leaves every Sturm count unchanged)
     const double* m = reinterpret_cast<const double*>(masks);
     const double l = fmin(m[0], m[2]), h = fmax(m[1], m[3]);
     const double mag = fmax(fabs(l), fabs(h));
     const int ex = (mag > 0.0 && mag < INFINITY) ? __builtin_amdgcn_frexp_exp(mag) : 0;
     bnd_ex = ex;
-    __syncthreads();
-    if (tid < n) {
-      dg[tid] = __builtin_ldexp(dg[tid], -ex);
-      e2[tid] = __builtin_ldexp(e2[tid], -2 * ex);
+    // the scaled, padded copy the counts read: rows n..127 get d = 4 (above every sigma, which
+    // lies in [-1.002, 1.002]) and no coupling, so they add no negative minor; se[i] = e2_{i-1}
+    // (se[0] = 0) floored at 2^-900, so that a zero minor is always followed by a nonzero one
+    // (p_{i+1} = -e2_i p_{i-1}) and the recurrence never stalls at zero
+    if (tid < 128) {
+      sd[tid] = tid < n ? __builtin_ldexp(dg[tid], -ex) : 4.0;
+      se[tid] = (tid >= 1 && tid < n) ? fmax(__builtin_ldexp(e2[tid - 1], -2 * ex), 0x1p-900) : 0.0;
     }
     if (tid == 0) {
       const double ls = __builtin_ldexp(l, -ex), hs = __builtin_ldexp(h, -ex);
@@ -519,11 +518,11 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
   // ---- 512-way multisection: 6 rounds of 9 bits bracket lambda_min to 2^-54 of the Gershgorin
   // span, below the Sturm count's own backward error (~n eps ||T||), so a 7th round adds noise
   double lo = bnd[0], hi = bnd[1];
+  const int nr = (n + 7) & ~7;
   for (int it = 0; it < 6; ++it) {
     const double width = hi - lo;
     const double sigma = lo + width * ((double)(tid + 1) / 513.0);
-    const int cnt = sturm_count_prod(dg, e2, n, sigma);
-    const unsigned long long mk = __ballot(cnt >= 1);
+    const unsigned long long mk = __ballot(sturm_any_below(sd, se, nr, sigma));
     if (lane == 0) masks[w] = mk;
     __syncthreads();
     int f = -1;
