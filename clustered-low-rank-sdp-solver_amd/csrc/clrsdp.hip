@@ -400,8 +400,10 @@ struct Solver final : HandleBase {
   hipStream_t own_stream = nullptr, stream = nullptr;
   T *X, *Y, *Xinv, *LX, *LY, *R, *P, *dX, *dY, *Z, *tA, *tB, *Cm;
   T *V, *lam, *TX, *TY, *BX, *BY, *AY, *tval, *S, *Wm, *Bm, *Qslab, *Q, *Qf, *Qinv;
+  T *TU, *TW;  // trace_A products U = Z V and the scaled vectors of compute_weighted_A (own
+               // buffers: they are produced on the side stream while SCHUR uses TX/TY)
   T *cvec, *x, *dx, *dvec, *rhs, *tvec, *tmpv, *pslab, *y, *bvec, *dyv, *pvec, *uvec;
-  T *sc, *bpart, *eigX, *eigY, *tmpsc, *tC = nullptr, *Stmp = nullptr;
+  T *sc, *bpart, *upart = nullptr, *eigX, *eigY, *tmpsc, *tC = nullptr, *Stmp = nullptr;
   T* Vt = nullptr;  // per block V^T (K x delta), fused Schur path only
   int *ksamp, *rsums, *info;
   T *xsend = nullptr, *xrecv = nullptr, *own_send = nullptr;
@@ -431,8 +433,6 @@ struct Solver final : HandleBase {
   GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2, q_qinv, q_qdy;
   GemmPlan<T> q_L21, q_S22, q_M, q_X21;  // 2x2 blocked L^-1 of S (dim_S in (128, 256])
   MatPlan<T> e_XY;                        // both step-length eigenproblems in one launch
-  RectDesc* d_zero = nullptr;            // upper-right blocks of the 2x2 S factors
-  int n_zero = 0;
   BlkDesc* d_blk = nullptr;      // all local blocks
   BlkDesc* d_blk_m = nullptr;    // local blocks with m > 1
   int n_blk_m = 0;
@@ -459,7 +459,8 @@ struct Solver final : HandleBase {
   // side stream: the local residuals overlap the Schur factorisation, chol(Q) overlaps the
   // first part of the predictor (iterate only; run_stage stays serial)
   hipStream_t aux = nullptr;
-  hipEvent_t ev_s = nullptr, ev_r = nullptr, ev_qa = nullptr, ev_q = nullptr;
+  hipEvent_t ev_m = nullptr, ev_x = nullptr, ev_s = nullptr, ev_r = nullptr, ev_qa = nullptr,
+             ev_q = nullptr;
   bool pending_q = false;
   float phase_ms[CLRSDP_NUM_STAGES];
 
@@ -562,7 +563,7 @@ struct Solver final : HandleBase {
     // graph-boundary and join idle time against the lost overlap)
     if (std::getenv("CLRSDP_ONE_STREAM")) aux = own_stream;
     else HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&ev_s, &ev_r, &ev_qa, &ev_q})
+    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
     build_plans();
@@ -570,9 +571,9 @@ struct Solver final : HandleBase {
 
   ~Solver() override {
     // device memory is released with the process / hipDeviceReset; free what we own explicitly
-    T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, BX, BY, AY,
+    T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, TU, TW, BX, BY, AY,
                  tval, S, Wm, Bm, Qslab, Q, Qf, Qinv, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
-                 bvec, dyv, pvec, uvec, bpart, eigX, tmpsc, tC, Stmp, own_send, Vt, Pres, pres, dres};
+                 bvec, dyv, pvec, uvec, bpart, upart, eigX, tmpsc, tC, Stmp, own_send, Vt, Pres, pres, dres};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
     if (comm) {
@@ -588,7 +589,7 @@ struct Solver final : HandleBase {
     for (char* r : ring_host)
       if (r) (void)hipHostFree(r);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_s, ev_r, ev_qa, ev_q, ring_ev[0], ring_ev[1]})
+    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ring_ev[0], ring_ev[1]})
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
       if (g) (void)hipGraphExecDestroy(g);
@@ -603,9 +604,10 @@ struct Solver final : HandleBase {
     dY = dmalloc<T>(B); Z = dmalloc<T>(B); tA = dmalloc<T>(B); tB = dmalloc<T>(B);
     Cm = dmalloc<T>(B);
     V = dmalloc<T>(nV); lam = dmalloc<T>(nK);
-    // TX / TY also hold the trace_A products U (m(m+1)/2 * delta*K <= (m delta)(m K)) and the
-    // scaled vectors of compute_weighted_A
-    TX = dmalloc<T>(nT); TY = dmalloc<T>(nT);
+    // TX / TY: the Schur-stage products; TU / TW (same slot layout, m(m+1)/2 * delta*K <=
+    // (m delta)(m K) per block): the trace_A products U and the scaled vectors of
+    // compute_weighted_A
+    TX = dmalloc<T>(nT); TY = dmalloc<T>(nT); TU = dmalloc<T>(nT); TW = dmalloc<T>(nT);
     BX = dmalloc<T>(nBX); BY = dmalloc<T>(nBX);
     AY = dmalloc<T>(nAY); tval = dmalloc<T>(nAY);
     S = dmalloc<T>(nS); Wm = dmalloc<T>(nB); Bm = dmalloc<T>(nB);
@@ -621,6 +623,7 @@ struct Solver final : HandleBase {
     // sc and the status words share one allocation (one D2H copy per iteration, pinned host
     // mirror) -- see stat_alloc()
     bpart = dmalloc<T>(std::max(nb(), 256));
+    upart = dmalloc<T>(3 * RED_G);  // update_state's partial sums
     eigX = dmalloc<T>(2 * std::max(nb(), 1));
     eigY = eigX + std::max(nb(), 1);  // X-side and Y-side minima of one batched eigen launch
     tC = dmalloc<T>(B);
@@ -734,12 +737,12 @@ struct Solver final : HandleBase {
       for (int r = 0; r < mm; ++r)
         for (int s = 0; s <= r; ++s) {
           const int rsi = s + r * (r + 1) / 2;
-          const int64_t uoff = b.toff + (int64_t)rsi * del * K;  // U / Vs slot in TX / TY
+          const int64_t uoff = b.toff + (int64_t)rsi * del * K;  // U / Vs slot in TU / TW
           // trace_A: U = Z[r,s] V   (Z block rows r, cols s)
           p_trU_Z.add(Z + b.off + r * del + (int64_t)s * del * n, n, V + b.voff, del, nullptr, 0,
-                      TX + uoff, del, del, K, del);
+                      TU + uoff, del, del, K, del);
           p_trU_Y.add(Y + b.off + r * del + (int64_t)s * del * n, n, V + b.voff, del, nullptr, 0,
-                      TX + uoff, del, del, K, del);
+                      TU + uoff, del, del, K, del);
           pd.push_back(PairDesc{uoff, b.voff, b.ayoff + (int64_t)rsi * K, del, K, (int)b.koff,
                                 -1});
           // weighted A: block (s, r) = Vs V^T  (MPMP.jl:1659-1667)
@@ -751,9 +754,9 @@ struct Solver final : HandleBase {
           sd.push_back(s_);
           // P = WA(x) - X and dX = WA(dx) + P: the second term rides in the GEMM's Cin
           const int64_t so = s * del + (int64_t)r * del * n;
-          p_wA_P.add(TY + uoff, del, V + b.voff, del, X + b.off + so, n, P + b.off + so, n, del,
+          p_wA_P.add(TW + uoff, del, V + b.voff, del, X + b.off + so, n, P + b.off + so, n, del,
                      del, K);
-          p_wA_dX.add(TY + uoff, del, V + b.voff, del, P + b.off + so, n, dX + b.off + so, n,
+          p_wA_dX.add(TW + uoff, del, V + b.voff, del, P + b.off + so, n, dX + b.off + so, n,
                       del, del, K);
         }
     }
@@ -787,7 +790,6 @@ struct Solver final : HandleBase {
     std::vector<TupleBlock> tbk;
     int bi = 0;
     int64_t s2off = 0;
-    std::vector<RectDesc> zr;
     for (int c = 0; c < nc(); ++c) {
       const int j = oc[c];
       const int D = (int)Ds[j];
@@ -812,12 +814,22 @@ struct Solver final : HandleBase {
         ci_S22.add(S22, D2, D, S22, D);                                       // S22 <- L22^-1
         q_M.add(S22, D, T21, D2, nullptr, 0, T21b, D2, D2, D1, D2);           // M = L22^-1 L21
         q_X21.add(T21b, D2, S11, D, nullptr, 0, S21, D, D2, D1, D1);          // S21 <- -M L11^-1
-        zr.push_back(RectDesc{Sc + (int64_t)D1 * D, D1, D2, D});             // S12 <- 0
+        // S12 (the upper-right block) still holds the assembled S: the products with L^-1
+        // below are split so that none of them reads it
+        q_W.add(S11, D, Bc, D, nullptr, 0, Wc, D, D1, (int)n_y, D1);          // W1 = L11^-1 B1
+        q_W.add(Sc + D1, D, Bc, D, nullptr, 0, Wc + D1, D, D2, (int)n_y, D);  // W2 = [X21 L22^-1] B
+        q_t.add(S11, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D1, 1, D1);
+        q_t.add(Sc + D1, D, rhs + xo, D, nullptr, 0, tvec + xo + D1, D, D2, 1, D);
+        // dx = (L^-1)^T u: columns 0..D1-1 of L^-1 are [L11^-1; X21], the rest L22^-1
+        q_dx.add(Sc, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D1, 1, D);
+        q_dx.add(S22, D, tmpv + xo + D1, D2, nullptr, 0, dx + xo + D1, D2, D2, 1, D2);
       }
-      q_W.add(Sc, D, Bc, D, nullptr, 0, Wc, D, D, (int)n_y, D);
-      q_t.add(Sc, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D, 1, D);
+      if (!(std::is_same<T, double>::value && D > 128 && D <= 256)) {
+        q_W.add(Sc, D, Bc, D, nullptr, 0, Wc, D, D, (int)n_y, D);
+        q_t.add(Sc, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D, 1, D);
+        q_dx.add(Sc, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D, 1, D);
+      }
       q_Wdy.add(Wc, D, dyv, (int)n_y, tvec + xo, D, tmpv + xo, D, D, 1, (int)n_y);
-      q_dx.add(Sc, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D, 1, D);
       t_W.add(Sc, D, Wc, D, D, (int)n_y);
       t_t.add(Sc, D, tvec + xo, D, D, 1);
       p_Q.add(Wc, D, Wc, D, nullptr, 0, Qslab + (int64_t)c * n_y * n_y, (int)n_y, (int)n_y, (int)n_y, D);
@@ -856,8 +868,6 @@ struct Solver final : HandleBase {
     q_qinv.ta = true;
     q_qinv.add(Qf, (int)n_y, Qf, (int)n_y, nullptr, 0, Qinv, (int)n_y, (int)n_y, (int)n_y, (int)n_y);
     q_qdy.add(Qinv, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
-    n_zero = (int)zr.size();
-    if (n_zero) d_zero = descs.own(zr);
     if (nc()) {
       d_scd = descs.own(scd);
       d_sbd = descs.own(sbd);
@@ -983,6 +993,8 @@ struct Solver final : HandleBase {
       put(Y + b.off, Yh, tot_blk, blkoff_g[b.gjl], (int64_t)b.n * b.n);
     }
     put(y, yh, n_y, 0, n_y);
+    refresh_xy_part();
+    HIPCHK(hipStreamSynchronize(stream));
   }
   void get_state(double* xh, double* Xh, double* yh, double* Yh) override {
     if (xh)
@@ -1144,13 +1156,13 @@ struct Solver final : HandleBase {
   void colsums() {
     if (n_pair) {
       dim3 g(cdiv(max_K, 4), n_pair);
-      colsum_dot<T><<<g, 256, 0, stream>>>(d_pair, TX, V, tval);
+      colsum_dot<T><<<g, 256, 0, stream>>>(d_pair, TU, V, tval);
     }
   }
   void weighted_A(const T* a, const GemmPlan<T>& plan, T* out, double beta = 0.0) {
     if (n_pair) {
       dim3 g(64, n_pair);
-      scale_cols<T><<<g, 256, 0, stream>>>(d_scale, V, lam, ksamp, a, TY);
+      scale_cols<T><<<g, 256, 0, stream>>>(d_scale, V, lam, ksamp, a, TW);
     }
     plan.launch(stream, 1.0, beta);
     if (anyMgt1) sym(out, out, 1, true);  // Symmetric(.) on blocks with m != 1 (MPMP.jl:1671-1674)
@@ -1158,19 +1170,22 @@ struct Solver final : HandleBase {
 
   // ---------------- stages
   void st_mu_r(const clrsdp_params* prm, int pd_feas) {
-    blk_dot(X, Y, nullptr, nullptr, 0, SC_DOT_XY, 1);
+    blk_dot(X, Y, nullptr, nullptr, 0, SC_DOT_XY, 1, upart);
     zero_info = true;  // the first scalar launch of an iteration clears the status words
     scalars(prm, pd_feas, 0);
     gemm_diag(p_XY, -1.0, 0.0, SC_MU_P);         // R = mu_p I - XY
   }
-  // sum/max over the local blocks into sc[slot], all-gathered and rank-reduced when world > 1
-  void blk_dot(const T* A, const T* B_, const T* dA, const T* dB, int op, int slot, int tag) {
+  // sum/max over the local blocks into sc[slot], all-gathered and rank-reduced when world > 1;
+  // part: the flat_reduce partials are already there (<X,Y>, from update_state)
+  void blk_dot(const T* A, const T* B_, const T* dA, const T* dB, int op, int slot, int tag,
+               const T* part = nullptr) {
     if (world == 1 && nb()) {
-      flat_reduce<T><<<RED_G, 256, 0, stream>>>(A, B_, dA, dB, nblk_el, op, bpart);
-      fold(bpart, RED_G, op == 2 ? 2 : 0, slot);  // partials folded into the next scalar launch
+      if (!part) flat_reduce<T><<<RED_G, 256, 0, stream>>>(A, B_, dA, dB, nblk_el, op, bpart);
+      fold(part ? part : bpart, RED_G, op == 2 ? 2 : 0, slot);  // folded into the next scalar launch
       return;
     }
-    local_blk_reduce(A, B_, dA, dB, op, xsend);
+    if (part && nb()) vec_reduce_tree(part, RED_G, op, xsend);
+    else local_blk_reduce(A, B_, dA, dB, op, xsend);
     exchange(tag, 1);
     reduce_ranks(1, 0, op == 2 ? 2 : 0, slot);
   }
@@ -1232,8 +1247,6 @@ struct Solver final : HandleBase {
         ci_S22.launch(stream, info + info_S0 + n1 + nc2);
         q_M.launch(stream, 1.0, 0.0);
         q_X21.launch(stream, -1.0, 0.0);
-        dim3 g(16, n_zero);
-        rect_fill<T><<<g, 256, 0, stream>>>(d_zero, 0.0);
       }
       q_W.launch(stream, 1.0, 0.0);
     } else {
@@ -1268,9 +1281,16 @@ struct Solver final : HandleBase {
   }
   // P, d, the p-slabs and the local error maxima (no exchange: may run on the side stream)
   void residuals_local(bool use_AY) {
-    // P = sum_i x_i A_i - X - C
+    residuals_P();
+    residuals_rest(use_AY);
+  }
+  // P = sum_i x_i A_i - X - C (the state only)
+  void residuals_P() {
     weighted_A(x, p_wA_P, P, -1.0);
     if (hasC) blk_lin(P, P, 1.0, Cm, -1.0);
+  }
+  // d, the p-slabs, the maxima of |P| and |d| (A_Y from SCHUR when use_AY)
+  void residuals_rest(bool use_AY) {
     // d = c - B y - Tr(A_* Y)
     p_By.launch(stream, 1.0, 0.0);
     if (!use_AY) {
@@ -1306,14 +1326,32 @@ struct Solver final : HandleBase {
     flush_scalars();
   }
   void st_direction(int tag) {
-    // Z = sym(X^-1 (P Y - R))
+    direction_Z();
+    direction_rhs();
+    direction_rest(tag);
+  }
+  // Z = sym(X^-1 (P Y - R)) and the trace_A products U = Z V (no factorisation needed: in a
+  // loop body the predictor's share runs on the side stream during FACTOR)
+  void direction_Z() {
     p_PY.launch(stream, 1.0, -1.0);
     p_Z.launch(stream, 1.0, 0.0);
     // Z is only consumed by trace_A: v^T Z v = v^T sym(Z) v, so the symmetrisation
     // (MPMP.jl:1704-1716) matters only for the off-diagonal (r != s) blocks of m > 1
     if (anyMgt1) sym(Z, Z, 0);
-    // rhs_x = -d - Tr(A_* Z)
     p_trU_Z.launch(stream, 1.0, 0.0);
+  }
+  // rhs_x = -d - Tr(A_* Z)   (MPMP.jl:1733-1739)
+  void direction_rhs() {
+    if (trivial_tuples) {
+      dim3 g(cdiv(max_K, 4), n_pair);
+      colsum_rhs<T><<<g, 256, 0, stream>>>(d_pair, TU, V, lam, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
+    } else {
+      colsums();
+      trace_aggregate(tval, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
+    }
+  }
+  // the block solve (MPMP.jl:1743-1776), dX and dY
+  void direction_rest(int tag) {
     direction_solves(tag);
     // dX = P + sum_i dx_i A_i
     weighted_A(dx, p_wA_dX, dX, 1.0);
@@ -1322,15 +1360,8 @@ struct Solver final : HandleBase {
     p_dY.launch(stream, 1.0, 0.0);
     sym(dY, dY, 0);
   }
-  // rhs, the three-stage solve and dx as separate batched launches (any word type / rank count)
+  // the three-stage solve and dx as separate batched launches (any word type / rank count)
   void direction_solves(int tag) {
-    if (trivial_tuples) {
-      dim3 g(cdiv(max_K, 4), n_pair);
-      colsum_rhs<T><<<g, 256, 0, stream>>>(d_pair, TX, V, lam, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
-    } else {
-      colsums();
-      trace_aggregate(tval, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
-    }
     // t_j = L_j^-1 rhs_j ;  u = sum_j W_j^T t_j ;  dy = Q^-1 (p - u) ; dx_j = L_j^-T (t_j + W_j dy)
     if (reg_S) {
       q_t.launch(stream, 1.0, 0.0);
@@ -1438,22 +1469,26 @@ struct Solver final : HandleBase {
     zero_cy = false;
   }
   void st_update(const clrsdp_params* prm, int pd_feas) {
-    // every launch checks the status words itself (no update after a failed factorisation)
-    const bool small = world == 1 && !hasC;  // x, y and the objectives in one workgroup
-    AxpyList<T> L;
-    L.it[0] = AxpyItem<T>{X, dX, sc + SC_ALPHA_P, nblk_el};
-    L.it[1] = AxpyItem<T>{Y, dY, sc + SC_ALPHA_D, nblk_el};
-    L.it[2] = AxpyItem<T>{x, dx, sc + SC_ALPHA_P, nx};
-    L.it[3] = AxpyItem<T>{y, dyv, sc + SC_ALPHA_D, n_y};
-    const unsigned g = std::max<unsigned>(1, std::min<unsigned>(cdiv(std::max<int64_t>(nblk_el, nx), 256), 2048));
-    vec_axpy_list<T><<<dim3(g, small ? 2 : 4), 256, 0, stream>>>(L, info, info_count);
-    if (small) {
-      const ScalarParams<T> p = sparams(prm, pd_feas);
-      update_small<T><<<1, 1024, 0, stream>>>(x, dx, nx, y, dyv, n_y, cvec, bvec, sc, info,
-                                              info_count, p);
+    // one launch updates x, y, X, Y (guarded by the status words: no update after a failed
+    // factorisation) and leaves the partial sums <X,Y> (next MU_R), <c,x> and <b,y>
+    update_state<T><<<RED_G, 256, 0, stream>>>(X, dX, Y, dY, nblk_el, x, dx, nx, cvec, y, dyv, n_y,
+                                               bvec, sc + SC_ALPHA_P, sc + SC_ALPHA_D, info,
+                                               info_count, upart);
+    if (world == 1 && !hasC) {  // the objectives from the partials, folded into one scalar launch
+      zero_cy = true;
+      fold(upart + RED_G, RED_G, 0, SC_DOT_CX);
+      fold(upart + 2 * RED_G, RED_G, 0, SC_DOT_BY);
+      scalars(prm, pd_feas, 3);
+      zero_cy = false;
       return;
     }
     objectives(prm, pd_feas);
+  }
+  // <X,Y> partials of the current state, as update_state leaves them (after a state change
+  // from the host: set_state, restore_state)
+  void refresh_xy_part() {
+    flat_reduce<T><<<RED_G, 256, 0, stream>>>(X, Y, nullptr, nullptr, nblk_el, 0, upart);
+    HIPCHK(hipGetLastError());
   }
 
   void stage(int s, const clrsdp_params* prm, int pd_feas) {
@@ -1520,22 +1555,40 @@ struct Solver final : HandleBase {
     // word), so a skipped body leaves the residuals of the last iteration that ran, which the
     // reference returns (MPMP.jl:1014-1024)
     const bool keep_res = pd_feas < 0;
-    for (int s = 0; s <= CLRSDP_STAGE_SCHUR; ++s) {
-      mark(s);
-      stage(s, prm, pd_feas);
-    }
-    // side stream: P, d, p-slabs (need the state and A_Y only)
+    // The side stream runs everything of RESIDUALS and of the predictor's right-hand side that
+    // does not need the Schur factorisation, as soon as its inputs exist, so that it overlaps
+    // XINV, SCHUR and FACTOR (whose on-chip factorisations leave most CUs idle):
+    //   after MU_R:  P = sum x_i A_i - X - C                      (state only)
+    //   after SCHUR: d, the p-slabs, the maxima (A_Y from SCHUR); Z = X^-1 (P Y - R), U = Z V
+    //                and rhs = -d - Tr(A_* Z)                     (the predictor's trace_A)
+    //   after FACTOR's Q sum: chol(Q) -> L_Q^-1, Q^-1
     const hipStream_t main_s = stream;
-    HIPCHK(hipEventRecord(ev_s, main_s));
-    HIPCHK(hipStreamWaitEvent(aux, ev_s, 0));
-    stream = aux;
-    residuals_local(true);
-    if (keep_res) {
-      copy_guarded(Pres, P, nblk_el);
-      copy_guarded(dres, dvec, nx);
-    }
-    HIPCHK(hipEventRecord(ev_r, aux));
-    stream = main_s;
+    auto side = [&](hipEvent_t ev, auto&& work) {
+      HIPCHK(hipEventRecord(ev, main_s));
+      HIPCHK(hipStreamWaitEvent(aux, ev, 0));
+      stream = aux;
+      work();
+      stream = main_s;
+    };
+    mark(CLRSDP_STAGE_MU_R);
+    stage(CLRSDP_STAGE_MU_R, prm, pd_feas);
+    side(ev_m, [&] { residuals_P(); });
+    mark(CLRSDP_STAGE_XINV);
+    stage(CLRSDP_STAGE_XINV, prm, pd_feas);
+    mark(CLRSDP_STAGE_SCHUR);
+    stage(CLRSDP_STAGE_SCHUR, prm, pd_feas);
+    // (Z waits for SCHUR although it could start after XINV: beside the MFMA-bound Schur
+    // products it only slowed them down, beside FACTOR's latency-bound factorisations it is free)
+    side(ev_s, [&] {
+      residuals_rest(true);
+      if (keep_res) {
+        copy_guarded(Pres, P, nblk_el);
+        copy_guarded(dres, dvec, nx);
+      }
+      direction_Z();
+      direction_rhs();
+      HIPCHK(hipEventRecord(ev_r, aux));
+    });
     mark(CLRSDP_STAGE_FACTOR);
     factor_local();
     // side stream: chol(Q) -> L_Q^-1, waited for just before the first Q solve
@@ -1551,7 +1604,9 @@ struct Solver final : HandleBase {
     residuals_finish();
     if (keep_res) copy_guarded(pres, pvec, n_y);
     HIPCHK(hipGetLastError());
-    for (int s = CLRSDP_STAGE_PREDICTOR; s < CLRSDP_NUM_STAGES; ++s) {
+    mark(CLRSDP_STAGE_PREDICTOR);
+    direction_rest(4);   // Z, U and rhs came from the side stream
+    for (int s = CLRSDP_STAGE_CORRECTOR_R; s < CLRSDP_NUM_STAGES; ++s) {
       mark(s);
       stage(s, prm, pd_feas);
     }
@@ -1653,6 +1708,7 @@ struct Solver final : HandleBase {
   void restore_state() override {
     if (!snapped) throw ClrsdpError{CLRSDP_E_STATE, "restore_state without save_state"};
     snap_copy(false);
+    refresh_xy_part();
   }
 
   // ---- pipelined loop: the host enqueues loop body k+1 before it reads the log row of body k.

@@ -411,6 +411,86 @@ __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restric
 // Flat 2-level reductions over a contiguous range (deterministic: fixed chunking + fixed tree)
 //   op 0: sum a.*b    op 1: sum (a+da).*(b+db)    op 2: max |a|
 // ------------------------------------------------------------------------------------------
+// acc + a b as one fused operation for fp64 (spelled out, so that flat_reduce and update_state
+// produce bitwise the same partial sums)
+template <class T>
+__device__ __forceinline__ T madd(T acc, T a, T b) {
+  if constexpr (sizeof(T) == 8) return fma(a, b, acc);
+  else return acc + a * b;
+}
+
+// flat_reduce's chunk of workgroup `blk` out of `nblk` over [0, n)
+__device__ __forceinline__ void flat_chunk(long long n, int blk, int nblk, long long& lo,
+                                           long long& hi) {
+  const long long chunk = (n + nblk - 1) / nblk;
+  lo = (long long)blk * chunk;
+  hi = lo + chunk < n ? lo + chunk : n;
+}
+
+// The state update of a loop body (MPMP.jl:877-887): X += alpha_p dX, Y += alpha_d dY,
+// x += alpha_p dx, y += alpha_d dy -- all skipped when a status word info[0..ninfo) is set (a
+// failed factorisation or a halted loop) -- with the sums the next steps need folded in: per
+// workgroup the partial <X,Y> of the new state (the next iteration's mu, with flat_reduce's
+// chunking, per-thread order and tree, so it is bitwise flat_reduce's partial), <c,x> and <b,y>
+// (the objectives, MPMP.jl:940-941).  part = [<X,Y> | <c,x> | <b,y>], gridDim.x partials each.
+template <class T>
+__global__ __launch_bounds__(256) void update_state(T* __restrict__ X, const T* __restrict__ dX,
+                                                    T* __restrict__ Y, const T* __restrict__ dY,
+                                                    long long nb, T* __restrict__ x,
+                                                    const T* __restrict__ dx, long long nx,
+                                                    const T* __restrict__ cv, T* __restrict__ y,
+                                                    const T* __restrict__ dy, long long ny,
+                                                    const T* __restrict__ bv, const T* alpha_p,
+                                                    const T* alpha_d, const int* info, int ninfo,
+                                                    T* __restrict__ part) {
+  __shared__ T red[3][256];
+  __shared__ int any;
+  const int tid = threadIdx.x, G = gridDim.x, g = blockIdx.x;
+  if (tid == 0) any = 0;
+  __syncthreads();
+  for (int i = tid; i < ninfo; i += 256)
+    if (info[i]) any = 1;
+  __syncthreads();
+  const bool upd = !any;
+  const T ap = *alpha_p, ad = *alpha_d;
+  long long lo, hi;
+  T axy = T(0.0), acx = T(0.0), aby = T(0.0);
+  flat_chunk(nb, g, G, lo, hi);
+#pragma unroll 4
+  for (long long e = lo + tid; e < hi; e += 256) {
+    T xv = X[e], yv = Y[e];
+    if (upd) {
+      xv = xv + ap * dX[e];
+      yv = yv + ad * dY[e];
+      X[e] = xv;
+      Y[e] = yv;
+    }
+    axy = madd(axy, xv, yv);
+  }
+  flat_chunk(nx, g, G, lo, hi);
+  for (long long e = lo + tid; e < hi; e += 256) {
+    T v = x[e];
+    if (upd) { v = v + ap * dx[e]; x[e] = v; }
+    acx = madd(acx, cv[e], v);
+  }
+  flat_chunk(ny, g, G, lo, hi);
+  for (long long e = lo + tid; e < hi; e += 256) {
+    T v = y[e];
+    if (upd) { v = v + ad * dy[e]; y[e] = v; }
+    aby = madd(aby, bv[e], v);
+  }
+  red[0][tid] = axy;
+  red[1][tid] = acx;
+  red[2][tid] = aby;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) red[q][tid] = red[q][tid] + red[q][tid + s];
+    __syncthreads();
+  }
+  if (tid < 3) part[tid * G + g] = red[tid][0];
+}
 template <class T>
 __global__ __launch_bounds__(256) void flat_reduce(const T* __restrict__ a, const T* __restrict__ b,
                                                    const T* __restrict__ da,
@@ -425,7 +505,7 @@ __global__ __launch_bounds__(256) void flat_reduce(const T* __restrict__ a, cons
   // the per-thread accumulation order is unchanged
   if (op == 0) {
 #pragma unroll 4
-    for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) acc += a[e] * b[e];
+    for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) acc = madd(acc, a[e], b[e]);
   } else if (op == 1) {
 #pragma unroll 4
     for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) acc += (a[e] + da[e]) * (b[e] + db[e]);
