@@ -342,8 +342,8 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
   template <int NP>
   void go(hipStream_t s, unsigned nb, int* info) const {
     static std::atomic<unsigned long long> attr{0};
-    lds_attr_once(attr, (const void*)chol_inv_mfma<NP>, (int)LDS_MAX);
-    chol_inv_mfma<NP><<<nb, 512, chol_inv_mfma_lds<NP>(), s>>>(
+    lds_attr_once(attr, (const void*)chol_inv_tiles<NP>, (int)chol_inv_tiles_lds<NP>());
+    chol_inv_tiles<NP><<<nb, 512, chol_inv_tiles_lds<NP>(), s>>>(
         reinterpret_cast<const MatDesc<double>*>(din), reinterpret_cast<const MatDesc<double>*>(dout), info);
   }
 };

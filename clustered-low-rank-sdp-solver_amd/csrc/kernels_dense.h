@@ -843,306 +843,344 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
 namespace clrsdp {
 
 // ------------------------------------------------------------------------------------------
-// chol_inv_mfma: A = L L^T and L^-1 for n <= 128 (fp64), one 512-thread workgroup per matrix.
-// A lives in LDS (swizzled column-major, padded to a multiple of 16 with the identity); L^-1
-// lives in registers as v_mfma_f64_16x16x4 accumulator tiles (the lower 16x16 tiles are dealt
-// round-robin to the 8 waves).  Blocked right-looking over 16-column panels, 3 barriers each:
-//   (a) wave 0 factors the 16x16 diagonal block and inverts it (lane-per-row, shuffles);
-//   (b) panel L21 = A21 L11^-T and row block X_k <- L11^-1 X_k   (MFMA);
-//   (c) trailing A22 -= L21 L21^T and X_ik -= L21_i X_k           (MFMA).
-// An accumulator tile is directly the B operand of the next MFMA (register r of lane l holds
-// row (l>>4)+4r = the B-operand row of K-chunk r), so X never round-trips through LDS except the
-// one row block broadcast per panel.
+// Cholesky + inverse of one fp64 block on chip with MFMA (chol_inv_tiles, below) and its
+// diagonal-tile step.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-template <int NP>
-struct CholLds {
-  // element (i, j) of the NP x NP column-major image; odd columns XOR row bit 4 so the two
-  // 16-lane halves of an operand read hit opposite bank halves
-  static __device__ __forceinline__ int idx(int i, int j) { return j * NP + (i ^ ((j & 1) << 4)); }
-};
-
-__device__ __forceinline__ void tile_of(int t, int& i, int& j) {
-  i = 0;
-  while ((i + 1) * (i + 2) / 2 <= t) ++i;
-  j = t - i * (i + 1) / 2;
+// Compile-time loop (the DPP lane selector of row_newbcast is an instruction immediate).
+template <int K, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (K < E) {
+    f(std::integral_constant<int, K>{});
+    static_for<K + 1, E>(f);
+  }
+}
+// acc += src[lane J of this lane's 16-lane DPP row] * mul: one v_fmac_f64_dpp with
+// row_newbcast (the f64 DPP form of CDNA3/4; the builtin route costs a copy + v_mov_b64_dpp +
+// v_fma_f64 and serialises on the copy register).  A DPP source needs 2 wait states after a
+// VALU write, which the compiler does not see inside inline asm: NOP = true puts an s_nop 1
+// in front.  The statements are volatile, so they keep their program order among themselves.
+template <int J, bool NOP>
+__device__ __forceinline__ void fmac_bcast(double& acc, double src, double mul) {
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(src), "v"(mul), "n"(J));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(src), "v"(mul), "n"(J));
 }
 
-// One wave: Cholesky factor and inverse of the 16x16 diagonal tile at (k0, k0) of the LDS image.
-// Lane (i = l & 15, g = l >> 4) holds row i, columns 4g..4g+3 of A_kk (-> L_kk) and of
-// X_kk (-> L_kk^-1).  Per column j: the pivot by v_readlane, column j of L and the scaled row j
-// of X through a 32-double LDS scratch (one wave: LDS order is program order, no barrier), then
-// four FMAs each for L and X (entries above the diagonal of L carry junk and are never used).
-// Writes L_kk back into the image and L_kk^-1 column-major into Dinv; a non-positive pivot sets
-// *flag = k0 + 1.
-template <int NP>
-__device__ inline void chol_diag16(double* __restrict__ A, int k0, double* __restrict__ Dinv,
-                                   int* flag, double* sc, int lane) {
-  using LI = CholLds<NP>;
-  const int i = lane & 15, g = lane >> 4;
-  double a[4], x[4];
+// One wave: Cholesky factor and inverse of the 16x16 diagonal tile at (k0, k0) of the LDS image,
+// with no LDS round trip inside the column chain.  Lane l holds row i = l & 15 of A (-> L) and
+// of X (-> L^-1) in full (each of the four 16-lane DPP rows is a replica).  Per column j the
+// pivot comes by v_readlane and every l_k / x_jm by row_newbcast from the lane that owns it, so
+// a column costs ~50 VALU instructions and one dependent chain (broadcast -> fma -> readlane ->
+// rsq).  Writes L_kk back into the image and L_kk^-1 column-major into Dinv; a non-positive
+// pivot sets *flag = k0 + 1.
+// IDX(i, j) = offset of tile element (i, j) in the image (only i >= j is read and written).
+template <class IDX>
+__device__ inline void chol_diag16_bc(double* __restrict__ A, IDX idx, int k0,
+                                     double* __restrict__ Dinv, int* flag, int lane) {
+  const int i = lane & 15;
+  double a[16], x[16];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int k = 4 * g + c;
-    a[c] = A[LI::idx(k0 + i, k0 + min(k, i))];
-    x[c] = (k == i) ? 1.0 : 0.0;
+  for (int k = 0; k < 16; ++k) {  // symmetric tile from its lower triangle
+    a[k] = A[idx(max(i, k), min(i, k))];
+    x[k] = (k == i) ? 1.0 : 0.0;
   }
-  // scratch traffic as relaxed atomics: with plain accesses the compiler may turn a predicated
-  // store into select + unconditional store, or forward a lane's own earlier value to a later
-  // load (both legal for one thread, wrong between lanes that share an address)
-  double* lsc = sc;       // column j of L below the diagonal (zeros at rows <= j)
-  double* xsc = sc + 16;  // row j of X after its scaling
+  // X = diag(r) Y: the rows of Y are left unscaled (y_i -= l_ij r_j y_j), and each lane
+  // scales its own row by its pivot's 1/l_ii at the end
   int bad = 0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int gj = j >> 2, cj = j & 3;
-    const double d = readlane_d(a[cj], 16 * gj + j);
+  double rmine = 1.0;
+  static_for<0, 16>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    const double d = readlane_d(a[j], j);
     bad |= !(d > 0.0);
     double r = __builtin_amdgcn_rsq(d);
     r = r * (1.5 - 0.5 * d * r * r);  // Newton step: r = 1/sqrt(d) to ~1 ulp
-    // l_ij = a_ij r (i >= j; l_jj = sqrt(d)) in the lanes of column group gj
-    a[cj] = (g == gj) ? a[cj] * r : a[cj];
-    if (g == gj)
-      __hip_atomic_store(lsc + i, (i > j) ? a[cj] : 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    const double s = (i == j) ? r : 1.0;
+    const double lv = a[j] * r;       // l_ij (row j: sqrt(d))
+    const double nl = (i > j) ? -lv : 0.0;
+    const double nlr = nl * r;
+    rmine = (i == j) ? r : rmine;
+    a[j] = lv;
+    // a_ik -= l_i l_k (k > j; the next pivot column first).  Only the first reads lv right
+    // after its VALU write; the y sources were last written a column ago.
+    static_for<j + 1, 16>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      fmac_bcast<k, k == j + 1>(a[k], lv, nl);
+    });
+    static_for<0, j + 1>([&](auto M) {
+      constexpr int m = decltype(M)::value;
+      fmac_bcast<j, j == 15 && m == 0>(x[m], x[m], nlr);
+    });
+  });
 #pragma unroll
-    for (int c = 0; c < 4; ++c) x[c] *= s;
-    if (i == j) {
+  for (int k = 0; k < 16; ++k) x[k] *= rmine;
+  if (lane < 16) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        __hip_atomic_store(xsc + 4 * g + c, x[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    for (int k = 0; k < 16; ++k) {
+      if (k <= i) A[idx(i, k)] = a[k];
+      Dinv[k * 16 + i] = x[k];  // column-major L_kk^-1 (zero above the diagonal)
     }
-    const double li = __hip_atomic_load(lsc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    double lk[4], xr[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      lk[c] = __hip_atomic_load(lsc + 4 * g + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      xr[c] = __hip_atomic_load(xsc + 4 * g + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      a[c] = fma(-li, lk[c], a[c]);
-      x[c] = fma(-li, xr[c], x[c]);
-    }
+    if (lane == 0 && bad) *flag = k0 + 1;
   }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int k = 4 * g + c;
-    if (k <= i) A[LI::idx(k0 + i, k0 + k)] = a[c];
-    Dinv[k * 16 + i] = x[c];  // column-major L_kk^-1
-  }
-  if (lane == 0 && bad) *flag = k0 + 1;
 }
 
-// A = L L^T and L^-1 of one SPD block (n <= NP) per 512-thread workgroup, on chip.
-// Wave 0 factors the 16x16 diagonal tiles; waves 1-7 own the 16x16 tiles of the lower triangle
-// (round robin) and keep the tiles of X = L^-1 in MFMA accumulators.  Per 16-column panel k:
-//   (b) waves 1-7: L_ik = A_ik L_kk^-T (panel) and X_kj <- L_kk^-1 X_kj (row block, also to LDS)
-//   (c) waves 1-7: trailing A_ij -= L_ik L_jk^T and X_ij -= L_ik X_kj, except the next diagonal
-//       tile, which wave 0 updates and factors at the same time (look-ahead), so the sequential
-//       16-column diagonal factorisation overlaps the trailing update.
-template <int NP>
-__global__ __launch_bounds__(512) void chol_inv_mfma(const MatDesc<double>* __restrict__ in,
-                                                     const MatDesc<double>* __restrict__ out_inv,
-                                                     int* __restrict__ info) {
-#ifdef CLRSDP_EIG_STAMPS
-  unsigned long long t_prev = __builtin_amdgcn_s_memtime();
-  const int tid_s = threadIdx.x;
-#define CH_STAMP(slot) if (tid_s == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); atomicAdd(&g_eig_stamps[slot], t_ - t_prev); t_prev = t_; }
+// ------------------------------------------------------------------------------------------
+// chol_inv_tiles: A = L L^T and L^-1 for n <= NP (fp64), one 512-thread workgroup per matrix,
+// with the off-diagonal 16x16 tiles resident in the worker waves' MFMA accumulators for the
+// whole factorisation (no LDS round trip of the trailing matrix).  Tile (i, j), i > j, of the
+// lower triangle belongs to worker (t mod 7), slot t / 7 (t = its row-major index); the slot
+// holds A_ij^T in accumulator layout (register r of lane l = A_ij[l&15][(l>>4) + 4r]) until
+// panel j turns it into L_ij, and X_ij = (L^-1)_ij (register r = X_ij[(l>>4) + 4r][l&15]) from
+// then on.  Only the diagonal tiles, one 16-column panel of L, one 16-row block of X and the
+// two diagonal inverses live in LDS (57 KB at NP = 128).  Per panel k:
+//   (b) workers: L_ik^T = Linv_kk A_ik^T (the accumulator is exactly the B operand) -> LDS
+//       panel; X_kj <- Linv_kk X_kj and X_kk = Linv_kk -> LDS row block;
+//   (c) workers: A_ij^T -= L_jk L_ik^T, X_ij -= L_ik X_kj, diagonal tiles D_i -= L_ik L_ik^T;
+//   wave 0, concurrently (look-ahead): as soon as L_{k+1,k} is in the panel, D_{k+1} -=
+//       L L^T and its Cholesky + inverse (chol_diag16_bc, no LDS inside the column chain).
+// The critical path per panel is one MFMA tile + the 16-column diagonal factorisation.
+// ------------------------------------------------------------------------------------------
+#ifdef CLRSDP_CHOL_TRACE
+__device__ unsigned long long g_chol2_trace[256 * 8 * 64];
+#define CT_TRACE() do { if ((threadIdx.x & 63) == 0 && tr_i < 64) g_chol2_trace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 64 + tr_i] = __builtin_amdgcn_s_memtime(); ++tr_i; } while (0)
 #else
-#define CH_STAMP(slot)
+#define CT_TRACE()
 #endif
-  constexpr int NT = NP / 16, NTILES = NT * (NT + 1) / 2, NWK = 7, SLOTS = (NTILES + NWK - 1) / NWK;
-  constexpr int XLD = NP + 16;  // X row-block buffer: 16 x NP, padded rows
+template <int NP>
+struct CholTiles {
+  static constexpr int NT = NP / 16, NOFF = NT * (NT - 1) / 2, NWK = 7;
+  static constexpr int SLOTS = (NOFF + NWK - 1) / NWK, DSLOTS = (NT + NWK - 1) / NWK;
+  static constexpr int LDD = 18;        // diagonal tiles: column-major 16 x 18
+  static constexpr int XLD = NP + 16;   // X row block: 16 x XLD row-major
+  static constexpr int DT = 0, PN = DT + NT * 16 * LDD, XR = PN + NT * 256, DI = XR + 16 * XLD,
+                       END = DI + 512;  // doubles; the int flags follow
+  static __device__ __forceinline__ void tile(int t, int& i, int& j) {  // row-major lower
+    i = 1;
+    while (i * (i + 1) / 2 <= t) ++i;
+    j = t - i * (i - 1) / 2;
+  }
+};
+template <int NP>
+size_t chol_inv_tiles_lds() { return sizeof(double) * CholTiles<NP>::END + 16; }
+
+template <int NP>
+__global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __restrict__ in,
+                                                      const MatDesc<double>* __restrict__ out_inv,
+                                                      int* __restrict__ info) {
+  using CT = CholTiles<NP>;
+  constexpr int NT = CT::NT, NWK = CT::NWK, SLOTS = CT::SLOTS, DSLOTS = CT::DSLOTS;
+  constexpr int LDD = CT::LDD, XLD = CT::XLD;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  double* A = reinterpret_cast<double*>(smem_raw);  // NP * NP
-  double* Dinv0 = A + NP * NP;                        // 2 x (16 x 16), column-major, by k parity
-  double* Xr = Dinv0 + 512;                           // 16 x XLD, row-major
-  int* flag = reinterpret_cast<int*>(Xr + 16 * XLD);
-  double* dsc = reinterpret_cast<double*>(flag + 4);  // 32-double scratch of chol_diag16
-  using LI = CholLds<NP>;
+  double* Dt = reinterpret_cast<double*>(smem_raw) + CT::DT;  // diagonal tiles
+  double* Pn = reinterpret_cast<double*>(smem_raw) + CT::PN;  // panel: L_ik column-major 16x16
+  double* Xr = reinterpret_cast<double*>(smem_raw) + CT::XR;  // X row block k
+  double* Di = reinterpret_cast<double*>(smem_raw) + CT::DI;  // Linv_kk by parity, col-major
+  int* flag = reinterpret_cast<int*>(reinterpret_cast<double*>(smem_raw) + CT::END);
+#ifdef CLRSDP_CHOL_TRACE
+  int tr_i = 0;
+#endif
+  CT_TRACE();
   const MatDesc<double> d = in[blockIdx.x];
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nt = (n + 15) / 16;  // active tile rows
+  const int nt = (n + 15) / 16;
   const int lr = lane & 15, lk = lane >> 4;
-  // ---- load the lower triangle (coalesced along columns); identity padding.  Nothing above
-  // the diagonal tiles is ever read, and the upper halves of diagonal tiles only carry junk.
-  {
-    // all NP*NP/512 loads in flight (clamped, unconditional), then the masked LDS stores
-    constexpr int PER = NP * NP / 512;
-    static_assert(PER * 512 == NP * NP, "NP*NP multiple of the workgroup");
-    double vl[PER];
-    const int nc = n > 0 ? n - 1 : 0;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int x = tid + 512 * e, i = x % NP, j = x / NP;
-#ifdef CLRSDP_CHOL_FULL_LOAD
-      vl[e] = gload(d.A + min(i, nc) + (size_t)min(j, nc) * d.lda);
-#else
-      vl[e] = 0.0;
-      if (i >= j) vl[e] = gload(d.A + min(i, nc) + (size_t)min(j, nc) * d.lda);  // lower only
-#endif
-    }
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int x = tid + 512 * e, i = x % NP, j = x / NP;
-      if (i >= j) A[LI::idx(i, j)] = (i < n && j < n) ? vl[e] : (i == j ? 1.0 : 0.0);
-    }
-  }
-  if (tid == 0) {
-    flag[0] = 0;  // first failing pivot + 1
-    flag[1] = 0;  // panels whose A_{k+1,k} wave 0 has read
-    flag[2] = 0;  // worker arrivals at the (b)->(c) barrier
-  }
-  // ---- X accumulators of the worker waves: identity on diagonal tiles
   const int wk = w - 1;  // worker index, -1 for wave 0
-  d4 X[SLOTS];
+  // ---- tile coordinates of this worker's slots (wave-uniform)
+  int TI[SLOTS], TJ[SLOTS];
 #pragma unroll
   for (int q = 0; q < SLOTS; ++q) {
     const int t = wk + NWK * q;
-    int ti = 0, tj = 0;
-    if (wk >= 0 && t < NTILES) tile_of(t, ti, tj);
+    TI[q] = NT; TJ[q] = 0;  // empty slot: row NT is never active
+    if (wk >= 0 && t < CT::NOFF) CT::tile(t, TI[q], TJ[q]);
+  }
+  // ---- off-diagonal tiles straight into the accumulators (A_ij^T layout, coalesced along
+  // rows), diagonal tiles into LDS with identity padding
+  d4 T[SLOTS];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      X[q][r] = (wk >= 0 && t < NTILES && ti == tj && (lk + 4 * r) == lr) ? 1.0 : 0.0;
+  for (int q = 0; q < SLOTS; ++q) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = 16 * TI[q] + lr, gj = 16 * TJ[q] + lk + 4 * r;
+      T[q][r] = (TI[q] < nt && gi < n && gj < n) ? gload(d.A + gi + (size_t)gj * d.lda) : 0.0;
+    }
+  }
+  for (int e = tid; e < NT * 256; e += 512) {
+    const int t = e >> 8, c = (e >> 4) & 15, r = e & 15;
+    const int gi = 16 * t + r, gj = 16 * t + c;
+    double v = gi == gj ? 1.0 : 0.0;
+    if (t < nt && gi < n && gj < n && r >= c) v = gload(d.A + gi + (size_t)gj * d.lda);
+    Dt[t * 16 * LDD + c * LDD + r] = v;
+  }
+  d4 XD[DSLOTS];
+#pragma unroll
+  for (int q = 0; q < DSLOTS; ++q) XD[q] = d4{0.0, 0.0, 0.0, 0.0};
+  if (tid == 0) {
+    flag[0] = 0;  // first failing pivot + 1
+    flag[1] = 0;  // panels whose L_{k+1,k} is in the panel buffer
+    flag[2] = 0;  // worker arrivals at the (b) -> (c) barrier
   }
   __syncthreads();
-  CH_STAMP(0)
-  if (w == 0) chol_diag16<NP>(A, 0, Dinv0, flag, dsc, lane);
+  CT_TRACE();
+  if (w == 0)
+    chol_diag16_bc(Dt, [](int i, int j) { return j * LDD + i; }, 0, Di, flag, lane);
   __syncthreads();
-  CH_STAMP(3)
+  CT_TRACE();
   for (int k = 0; k < nt; ++k) {
-    const int k0 = 16 * k;
     if (*flag) break;
-    const double* Dinv = Dinv0 + 256 * (k & 1);
-    // ---------------- (b) panel and X row block (waves 1-7)   ||   wave 0 runs ahead:
-    //   L_{k+1,k} = A_{k+1,k} L_kk^-T in registers, A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T, and the
-    //   factorisation of that tile, while the workers do (b) and (c) of panel k.
+    const double* Dk = Di + 256 * (k & 1);
     if (wk >= 0) {
-      // Linv_kk operands: A-op a[r] = Linv[lr][4r+lk] (Dinv column-major: Dinv[c*16 + i]);
-      // the B-op of Linv^T for K-chunk r, B[4r+lk][lr] = Linv[lr][4r+lk], is the same value
+      // ---------------- (b): Linv_kk as the A operand: a[r] = Linv[lr][4r+lk]
       double lopA[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) lopA[r] = Dinv[(4 * r + lk) * 16 + lr];
+      for (int r = 0; r < 4; ++r) lopA[r] = Dk[(4 * r + lk) * 16 + lr];
+      // the look-ahead tile L_{k+1,k} first (wave 0 waits for it)
 #pragma unroll
-      for (int q = 0; q < SLOTS; ++q) {
-        const int t = wk + NWK * q;
-        if (t >= NTILES) continue;
-        int ti, tj;
-        tile_of(t, ti, tj);
-        if (ti >= nt) continue;
-        if (tj == k && ti > k) {  // panel tile: L21_i = A_ik Linv^T
+      for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int q = 0; q < SLOTS; ++q) {
+          if (TI[q] >= nt || TJ[q] != k) continue;
+          if ((TI[q] == k + 1) != (pass == 0)) continue;
           d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            acc = mfma64(A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)], lopA[r], acc);
-          if (ti == k + 1) {  // wave 0 reads this tile's input first (in place update)
-            while (__hip_atomic_load(flag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
-              __builtin_amdgcn_s_sleep(1);
+          for (int r = 0; r < 4; ++r) acc = mfma64(lopA[r], T[q][r], acc);  // L_ik^T
+          double* P = Pn + 256 * TI[q];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) P[(lk + 4 * r) * 16 + lr] = acc[r];  // L_ik[lr][lk+4r]
+          if (pass == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(flag + 1, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, k0 + lr)] = acc[r];
-        }
-        if (ti == k && tj <= k) {  // X_kj <- Linv_kk X_kj
-          d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc = mfma64(lopA[r], X[q][r], acc);
-          X[q] = acc;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Xr[(lk + 4 * r) * XLD + 16 * tj + lr] = acc[r];
         }
       }
+#pragma unroll
+      for (int q = 0; q < SLOTS; ++q) {  // X row block: X_kj <- Linv_kk X_kj (j < k)
+        if (TI[q] != k) continue;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = mfma64(lopA[r], T[q][r], acc);
+        T[q] = acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Xr[(lk + 4 * r) * XLD + 16 * TJ[q] + lr] = acc[r];
+      }
+      if (wk == k % NWK) {  // X_kk = Linv_kk (accumulator layout: register r = Linv[lk+4r][lr])
+#pragma unroll
+        for (int q = 0; q < DSLOTS; ++q)
+          if (q == k / NWK) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              XD[q][r] = Dk[lr * 16 + lk + 4 * r];
+              Xr[(lk + 4 * r) * XLD + 16 * k + lr] = XD[q][r];
+            }
+          }
+      }
+      CT_TRACE();
       // workers-only barrier (wave 0 is busy with the next diagonal tile)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(flag + 2, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       while (__hip_atomic_load(flag + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NWK * (k + 1))
         __builtin_amdgcn_s_sleep(1);
-      CH_STAMP(1)
-      // ---------------- (c) trailing updates (the next diagonal tile is wave 0's)
+      CT_TRACE();
+      // ---------------- (c) trailing update of the rows below k
+      const double* Pk = Pn;
 #pragma unroll
       for (int q = 0; q < SLOTS; ++q) {
-        const int t = wk + NWK * q;
-        if (t >= NTILES) continue;
-        int ti, tj;
-        tile_of(t, ti, tj);
+        const int ti = TI[q], tj = TJ[q];
         if (ti >= nt || ti <= k) continue;
-        if (tj > k) {  // A_ij -= L21_i L21_j^T
-          if (ti == k + 1 && tj == k + 1) continue;
-          d4 acc;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = A[LI::idx(16 * ti + lk + 4 * r, 16 * tj + lr)];
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            acc = mfma64(-A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)],
-                         A[LI::idx(16 * tj + lr, k0 + 4 * r + lk)], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) A[LI::idx(16 * ti + lk + 4 * r, 16 * tj + lr)] = acc[r];
-        } else {  // X_ij -= L21_i X_kj  (tj <= k)
+        const double* Pi = Pk + 256 * ti;
+        if (tj > k) {  // A_ij^T -= L_jk L_ik^T
+          const double* Pj = Pk + 256 * tj;
+          d4 acc = T[q];
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            X[q] = mfma64(-A[LI::idx(16 * ti + lr, k0 + 4 * r + lk)],
-                          Xr[(4 * r + lk) * XLD + 16 * tj + lr], X[q]);
+            acc = mfma64(-Pj[(4 * r + lk) * 16 + lr], Pi[(4 * r + lk) * 16 + lr], acc);
+          T[q] = acc;
+        } else {  // X_ij -= L_ik X_kj (tj == k: the slot turns from L_ik into X_ik = -L_ik X_kk)
+          d4 acc = tj == k ? d4{0.0, 0.0, 0.0, 0.0} : T[q];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc = mfma64(-Pi[(4 * r + lk) * 16 + lr], Xr[(4 * r + lk) * XLD + 16 * tj + lr], acc);
+          T[q] = acc;
         }
       }
-    } else if (k + 1 < nt) {
-      const int t1 = 16 * (k + 1);
-      double* scr = Dinv0 + 256 * ((k + 1) & 1);  // free until diag(k+1) writes it
-      double af[4], lop[4];
+      // diagonal tiles below the look-ahead one: D_i -= L_ik L_ik^T (in LDS)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        af[r] = A[LI::idx(t1 + lr, k0 + 4 * r + lk)];
-        lop[r] = Dinv[(4 * r + lk) * 16 + lr];
+      for (int q = 0; q < DSLOTS; ++q) {
+        const int di = wk + NWK * q;
+        if (di >= nt || di <= k + 1) continue;
+        const double* Pi = Pk + 256 * di;
+        double* D = Dt + di * 16 * LDD;
+        d4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = D[lr * LDD + lk + 4 * r];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double f = Pi[(4 * r + lk) * 16 + lr];
+          acc = mfma64(-f, f, acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D[lr * LDD + lk + 4 * r] = acc[r];
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(flag + 1, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      d4 l = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) l = mfma64(af[r], lop[r], l);  // L_{k+1,k}
-#pragma unroll
-      for (int r = 0; r < 4; ++r) scr[lr * 16 + lk + 4 * r] = l[r];  // column-major 16x16
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      CT_TRACE();
+    } else if (k + 1 < nt) {
+      // ---------------- wave 0: D_{k+1} -= L L^T (L = L_{k+1,k}) and its factorisation
+      while (__hip_atomic_load(flag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
+        __builtin_amdgcn_s_sleep(1);
+      CT_TRACE();
+      const double* P = Pn + 256 * (k + 1);
+      double* D = Dt + (k + 1) * 16 * LDD;
       d4 acc;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = A[LI::idx(t1 + lk + 4 * r, t1 + lr)];
+      for (int r = 0; r < 4; ++r) acc[r] = D[lr * LDD + lk + 4 * r];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const double f = scr[(4 * r + lk) * 16 + lr];  // L_{k+1,k}[lr][4r+lk]
+        const double f = P[(4 * r + lk) * 16 + lr];
         acc = mfma64(-f, f, acc);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) A[LI::idx(t1 + lk + 4 * r, t1 + lr)] = acc[r];
+      for (int r = 0; r < 4; ++r) D[lr * LDD + lk + 4 * r] = acc[r];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      chol_diag16<NP>(A, t1, scr, flag, dsc, lane);
+      chol_diag16_bc(D, [](int i, int j) { return j * LDD + i; }, 16 * (k + 1),
+                     Di + 256 * ((k + 1) & 1), flag, lane);
+      CT_TRACE();
     }
     __syncthreads();
-    CH_STAMP(2)
+    CT_TRACE();
   }
   if (tid == 0 && info) info[blockIdx.x] = *flag;
-  // ---- write L^-1 (lower tiles from the workers' registers, zeros above)
+  // ---- write L^-1: off-diagonal and diagonal X tiles from the registers, zeros above
   const MatDesc<double> o = out_inv[blockIdx.x];
   if (wk >= 0) {
 #pragma unroll
     for (int q = 0; q < SLOTS; ++q) {
-      const int t = wk + NWK * q;
-      if (t >= NTILES) continue;
-      int ti, tj;
-      tile_of(t, ti, tj);
+      if (TI[q] >= nt) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int gi = 16 * ti + lk + 4 * r, gj = 16 * tj + lr;
-        if (gi < n && gj < n) o.A[gi + (size_t)gj * o.lda] = X[q][r];
+        const int gi = 16 * TI[q] + lk + 4 * r, gj = 16 * TJ[q] + lr;
+        if (gi < n && gj < n) o.A[gi + (size_t)gj * o.lda] = T[q][r];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < DSLOTS; ++q) {
+      const int di = wk + NWK * q;
+      if (di >= nt) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = 16 * di + lk + 4 * r, gj = 16 * di + lr;
+        if (gi < n && gj < n) o.A[gi + (size_t)gj * o.lda] = XD[q][r];
       }
     }
   }
   for (int j = tid >> 4; j < n; j += 32)
     for (int i = (tid & 15); i < (j & ~15); i += 16) o.A[i + (size_t)j * o.lda] = 0.0;  // tiles above
-  CH_STAMP(4)
+  CT_TRACE();
 }
+#undef CT_TRACE
 
-template <int NP>
-size_t chol_inv_mfma_lds() { return sizeof(double) * ((size_t)NP * NP + 512 + 16 * (NP + 16) + 32) + 16; }
 
 }  // namespace clrsdp
 

@@ -43,24 +43,16 @@ int main(int argc, char** argv) {
   }
   {
     int NPv = n <= 32 ? 32 : n <= 64 ? 64 : 128;
-    size_t lds = NPv == 32 ? chol_inv_mfma_lds<32>() : NPv == 64 ? chol_inv_mfma_lds<64>() : chol_inv_mfma_lds<128>();
-    CK(hipFuncSetAttribute((const void*)chol_inv_mfma<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    CK(hipFuncSetAttribute((const void*)chol_inv_mfma<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    size_t lds = NPv == 32 ? chol_inv_tiles_lds<32>() : NPv == 64 ? chol_inv_tiles_lds<64>() : chol_inv_tiles_lds<128>();
+    CK(hipFuncSetAttribute((const void*)chol_inv_tiles<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     for (int rep = 0; rep < 3; ++rep) {
       CK(hipEventRecord(e0));
-      if (NPv == 128) chol_inv_mfma<128><<<nb, 512, lds>>>(ddin, ddout, info);
-      else if (NPv == 64) chol_inv_mfma<64><<<nb, 512, lds>>>(ddin, ddout, info);
-      else chol_inv_mfma<32><<<nb, 512, lds>>>(ddin, ddout, info);
+      if (NPv == 128) chol_inv_tiles<128><<<nb, 512, lds>>>(ddin, ddout, info);
+      else if (NPv == 64) chol_inv_tiles<64><<<nb, 512, lds>>>(ddin, ddout, info);
+      else chol_inv_tiles<32><<<nb, 512, lds>>>(ddin, ddout, info);
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
-      printf("chol_inv_mfma<%d> n=%d batch=%d: %.1f us\n", NPv, n, nb, ms * 1e3);
+      printf("chol_inv_tiles<%d> n=%d batch=%d: %.1f us\n", NPv, n, nb, ms * 1e3);
     }
-#ifdef CLRSDP_EIG_STAMPS
-    unsigned long long st[8];
-    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_eig_stamps), sizeof(st)));
-    printf("  chol stamps per matrix: diag0 %.0f load %.0f  panel %.0f  trailing %.0f  output %.0f\n", st[3] / (3.0 * nb), st[0] / (3.0 * nb), st[1] / (3.0 * nb), st[2] / (3.0 * nb), st[4] / (3.0 * nb));
-    unsigned long long z[8] = {0};
-    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_eig_stamps), z, sizeof(z)));
-#endif
   }
   // check L^-1 A L^-T = I for matrix 0
   std::vector<double> Li((size_t)n * n);
