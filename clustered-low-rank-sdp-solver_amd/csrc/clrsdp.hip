@@ -184,13 +184,29 @@ struct GemmPlan : PlanBase {
     h.push_back(g);
   }
   bool gemv = false;
+  // sym: every problem square with an exactly symmetric result wanted (gemm_f64_lds SYM: the
+  // lower tiles only, each written with its mirror image); fp64, beta = 0
+  bool sym = false;
   void finalize() {
     if (h.empty()) return;
     gemv = true;
     for (const auto& g : h) gemv = gemv && g.N == 1;
     if (gemv)  // one workgroup per 64 outputs
       for (size_t q = 0; q < h.size(); ++q) ntiles[q] = (int)cdiv(h[q].M, 64);
-    t2d = tile_major(ntiles);
+    if (sym) {
+      if (gemv || !std::is_same<T, double>::value)
+        throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: fp64 matrices only"};
+      for (const auto& g : h)
+        if (g.M != g.N) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: square problems only"};
+      // tile-major over the lower tiles (tm >= tn) of each problem, problem fastest
+      int mx = 0;
+      for (int n : ntiles) mx = std::max(mx, n);
+      for (int t = 0; t < mx; ++t)
+        for (size_t p = 0; p < h.size(); ++p)
+          if (t < ntiles[p] && t / h[p].tn >= t % h[p].tn) t2d.push_back(TileRef{(int)p, t});
+    } else {
+      t2d = tile_major(ntiles);
+    }
     d = own(h);
     dt = own(t2d);
   }
@@ -210,6 +226,14 @@ struct GemmPlan : PlanBase {
     }
     if constexpr (std::is_same<T, double>::value) {
       const double* ds = reinterpret_cast<const double*>(dscal);
+      if (sym) {
+        if (beta != 0.0 || ds) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: beta = 0 only"};
+        if (!ta && tb) gemm_f64_lds<false, true, 0, 32, 8, true><<<grid, 512, 0, s>>>(d, dt, alpha, 0.0);
+        else if (!ta && !tb) gemm_f64_lds<false, false, 0, 32, 8, true><<<grid, 512, 0, s>>>(d, dt, alpha, 0.0);
+        else throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: op(A) = A only"};
+        HIPCHK(hipGetLastError());
+        return;
+      }
       if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
       else if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
       else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
@@ -675,6 +699,8 @@ struct Solver final : HandleBase {
     }
     q_xinv.ta = true;
     q_sx2.tb = q_sy2.tb = true;
+    // L^-1 dM L^-T exactly symmetric: eigmin_reg reads it without a transposed copy
+    q_sx2.sym = std::is_same<T, double>::value;
     q_L21.tb = true;
     q_S22.tb = true;
     q_dx.ta = true;
@@ -1869,6 +1895,7 @@ int step_length_f64(int device, int64_t nblk, const int64_t* n, const double* Mh
   CholInvPlan<double> ci;
   GemmPlan<double> g1, g2;
   g2.tb = true;
+  g2.sym = true;  // exactly symmetric L^-1 dM L^-T (eigmin_reg reads only A(i, j))
   MatPlan<double> fac, eg;
   TrsmPlan<double> s1, s2;
   std::vector<BlkDesc> big;

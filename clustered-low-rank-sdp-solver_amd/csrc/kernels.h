@@ -115,7 +115,10 @@ __device__ inline int acc_col(int wn, int ni, int lr, int wcols = 32) { return w
 // TAG only names the instantiation (a profile can tell the Schur-stage launch from the others).
 // NW = 4 (2x2 waves, 32x32 each) or 8 (2x4 waves, 32x16 each: twice the waves per tile, for
 // batches of small products that leave the CUs latency-bound).
-template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8>
+// SYM: square problems whose product is symmetric in exact arithmetic (L^-1 dM L^-T): the launch
+// covers the lower tiles only, each writes its tile and the mirror image, and a diagonal tile
+// mirrors its lower triangle -- the result is exactly symmetric (beta = 0, no diagonal term).
+template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false>
 __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
                                                         const TileRef* __restrict__ t2d,
                                                         double alpha, double beta,
@@ -183,8 +186,22 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* 
         smem[acc_row(wm, mi, lk, r) * TP + acc_col(wn, ni, lr, WC)] = acc[mi][ni][r];
   __syncthreads();
   const int row = m0 + lane;
+  constexpr int CPW = 64 / NW;  // output columns stored per wave
+  if constexpr (SYM) {
+#pragma unroll 4
+    for (int c = 0; c < CPW; ++c) {
+      const int cl = w * CPW + c;
+      if (row < M && n0 + cl < N) {
+        const double v = (m0 != n0 || cl <= lane) ? smem[lane * TP + cl] : smem[cl * TP + lane];
+        d.C[row + (size_t)(n0 + cl) * d.ldc] = alpha * v;
+      }
+      // the mirror tile: element (m0 + cl, n0 + lane) to (n0 + lane, m0 + cl)
+      if (m0 != n0 && m0 + cl < M && n0 + lane < N)
+        d.C[(n0 + lane) + (size_t)(m0 + cl) * d.ldc] = alpha * smem[cl * TP + lane];
+    }
+    return;
+  }
   if (row < M) {
-    constexpr int CPW = 64 / NW;  // output columns stored per wave
 #pragma unroll 4
     for (int c = 0; c < CPW; ++c) {
       const int cl = w * CPW + c, col = n0 + cl;

@@ -181,18 +181,46 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
 // ------------------------------------------------------------------------------------------
 // ------------------------------------------------------------------------------------------
 // eigmin_reg: lambda_min of a symmetric n <= 128 fp64 block with the matrix held in REGISTERS
-// (replaces approx_eig_qr! in compute_step_length, MPMP.jl:1857-1860).  512 threads; wave w
-// owns rows 16w..16w+15 (lane r = l & 15), lane class c = l >> 4 owns the column pairs
-// j = 2c + 8s + {0,1}, s = 0..15: 32 entries per thread.  Householder tridiagonalisation with
-// two barriers per column:
-//   (B) every wave rebuilds the reflector of column k redundantly from the column buffer
-//       (wave reduction, no barrier), p_i = sum_j A_ij v_j in registers (+ 2 shuffles across
-//       the column classes), per-wave v^T p to LDS                                 -- barrier
-//   (C) w = beta p - K v; A -= v w^T + w v^T in registers; the owners of column k+1 publish it
-//       to the other column buffer                                                -- barrier
-// then 512-way multisection with Sturm counts on the tridiagonal matrix.  No LDS image of A:
-// the only LDS traffic per column is the broadcast of v and p (two ds_read_b128 per pair).
+// (replaces approx_eig_qr! in compute_step_length, MPMP.jl:1857-1860).  The input must be exactly
+// symmetric (every caller's block comes from the symmetric GEMM epilogue).  512 threads; wave w
+// owns row block rb(w) (rows 16 rb..16 rb+15, lane r = l & 15), lane class c = l >> 4 owns the column pairs
+// j = 2c + 8s + {0,1}, s = 0..15 (fixed slots): 32 entries per thread.  Householder
+// tridiagonalisation with ONE barrier per column k:
+//   p_i = sum_j A_ij v_j in registers (+ 2 swaps across the column classes), per-wave v^T p to
+//   LDS                                                                             -- barrier
+//   w = beta p - K v; A -= v w^T + w v^T in registers; meanwhile every wave recomputes row k+1
+//   of the updated matrix from the copy its owners published a step earlier (the owners' own
+//   operations, so bitwise their registers) and builds the next reflector from it redundantly
+//   (wave reduction, no barrier); the owners of row k+2 publish it for the step after next.
+// The 16 lanes of a DPP row share a column class and so need the same 32 values of v and of p:
+// lane t of the row reads only slot t and every FMA takes slot s from lane s by row_newbcast
+// (v_fmac_f64_dpp).  Slots whose 8 columns are all <= k are skipped in groups of 4 by a uniform
+// branch; the slots never move, so the loop carries no register copies.
+// Then 512-way multisection with Sturm counts on the tridiagonal matrix.
 // ------------------------------------------------------------------------------------------
+// Compile-time loop (the DPP lane selector of row_newbcast is an instruction immediate).
+template <int K, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (K < E) {
+    f(std::integral_constant<int, K>{});
+    static_for<K + 1, E>(f);
+  }
+}
+// acc += src[lane J of this lane's 16-lane DPP row] * mul: one v_fmac_f64_dpp with
+// row_newbcast (the f64 DPP form of CDNA3/4; the builtin route costs a copy + v_mov_b64_dpp +
+// v_fma_f64 and serialises on the copy register).  A DPP source needs 2 wait states after a
+// VALU write, which the compiler does not see inside inline asm: NOP = true puts an s_nop 1
+// in front.  The statements are volatile, so they keep their program order among themselves.
+template <int J, bool NOP>
+__device__ __forceinline__ void fmac_bcast(double& acc, double src, double mul) {
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(src), "v"(mul), "n"(J));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(src), "v"(mul), "n"(J));
+}
+
 #ifdef CLRSDP_EIGREG_STAMPS
 __device__ unsigned long long g_eigreg_stamps[8];
 #endif
@@ -265,31 +293,38 @@ __device__ inline bool sturm_any_below(const double* __restrict__ sd, const doub
   return acc < 0;
 }
 
+template <int DBG = 0>  // DBG (timing experiments only): 1 = no update FMAs, 2 = no matvec FMAs
 __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restrict__ descs,
                                                   double* __restrict__ out) {
   constexpr int NS = 16;
 #ifdef CLRSDP_EIGREG_STAMPS
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
-#define ER_STAMP(slot) if (threadIdx.x == 0) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); atomicAdd(&g_eigreg_stamps[slot], t_ - t_prev); t_prev = t_; }
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define ER_STAMP(slot) { unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[slot] += t_ - t_prev; t_prev = t_; }
 #else
 #define ER_STAMP(slot)
 #endif
-  // colb[k&1] = column k of the current matrix with rows <= k-1 zeroed; pb = A'v with inactive
-  // rows zeroed; rows/columns >= n stay zero.  So v and w need no masking per element.
-  // entries 128..255 stay zero: the slots past the last column read zeros there
-  __shared__ __attribute__((aligned(16))) double colb[2][256];
-  __shared__ __attribute__((aligned(16))) double pb[256];
-  __shared__ double redw[8];
+  // rowb[r&1] = row r of the matrix before the step that reflects column r-1 (published by the
+  // lanes that own it); pb[k&1] = p = A'v of step k (inactive rows zero); vb[k&1] = v of step k;
+  // redw[k&1] = the per-wave parts of v^T p.  Every buffer alternates between two copies, so one
+  // barrier per column separates each write from the reads of the copy it replaces.
+  __shared__ __attribute__((aligned(16))) double rowb[2][128];
+  __shared__ __attribute__((aligned(16))) double pb[2][128];
+  __shared__ __attribute__((aligned(16))) double vb[2][128];
+  __shared__ double redw[2][8];
   __shared__ double dg[128], e2[128];
   __shared__ __attribute__((aligned(16))) double sd[128], se[128];
   __shared__ double bnd[2];
   __shared__ unsigned long long masks[8];
   const MatDesc<double> d = descs[blockIdx.x];
   const int n = d.n, lda = d.lda, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int c = lane >> 4, i = w * 16 + (lane & 15);
+  // row block of wave w: waves w and w+4 share a SIMD, so they get blocks that go idle early and
+  // late (0/7, 1/6, 2/5, 3/4): every SIMD then carries the same number of live-row columns
+  const int rb = w < 4 ? w : 11 - w;
+  const int c = lane >> 4, t16 = lane & 15, i = rb * 16 + t16;
   const bool rowok = i < n;
-  // slot s holds columns j = 2c + 8(s + q) + {0,1}; q advances (the slots shift down by one)
-  // each time column k+1 enters a new group of 8, so column k+1 always sits in slot 0.
+  // a[s][e] = A(i, 2c + 8s + e).  The input is exactly symmetric (the step-length product is
+  // written by the symmetric GEMM epilogue), so only coalesced A(i, j) loads are needed.
   double a[NS][2];
 #pragma unroll
   for (int s = 0; s < NS; ++s)
@@ -297,7 +332,7 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     for (int e = 0; e < 2; ++e) {
       const int j = 2 * c + 8 * s + e;
       const int ic = min(i, n - 1), jc = min(j, n - 1);  // unconditional loads, masked after
-      const double v = (gload(d.A + ic + (size_t)jc * lda) + gload(d.A + jc + (size_t)ic * lda)) * 0.5;
+      const double v = gload(d.A + ic + (size_t)jc * lda);
       a[s][e] = (rowok && j < n) ? v : 0.0;
     }
   // scale the block by 2^-ex0 so that its largest entry lies in [0.5, 1): the column norms of the
@@ -310,11 +345,11 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     for (int s = 0; s < NS; ++s) amax = fmax(amax, fmax(fabs(a[s][0]), fabs(a[s][1])));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
-    if (lane == 0) redw[w] = amax;
+    if (lane == 0) redw[0][w] = amax;
     __syncthreads();
-    amax = redw[0];
+    amax = redw[0][0];
 #pragma unroll
-    for (int r = 1; r < 8; ++r) amax = fmax(amax, redw[r]);
+    for (int r = 1; r < 8; ++r) amax = fmax(amax, redw[0][r]);
     ex0 = (amax > 0.0 && amax < INFINITY) ? __builtin_amdgcn_frexp_exp(amax) : 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -322,149 +357,174 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
       a[s][1] = __builtin_ldexp(a[s][1], -ex0);
     }
   }
-#define EIG_SHIFT_SLOTS()                                                 \
-  do {                                                                       \
-    _Pragma("unroll") for (int s = 0; s + 1 < NS; ++s) {                     \
-      a[s][0] = a[s + 1][0];                                                 \
-      a[s][1] = a[s + 1][1];                                                 \
-    }                                                                        \
-    a[NS - 1][0] = a[NS - 1][1] = 0.0;                                       \
-  } while (0)
-  if (tid < 256) {
-    pb[tid] = 0.0;
-    colb[1][tid] = 0.0;
-    if (tid >= n) colb[0][tid] = 0.0;
-  }
-  if (c == 0 && rowok) colb[0][i] = a[0][0];  // column 0
-  __syncthreads();
-  ER_STAMP(0)
-  int q = 0;
-  for (int k = 0; k + 2 < n; ++k) {
-    if (((k + 1) & 7) == 0) { EIG_SHIFT_SLOTS(); ++q; }
-    const double* col = colb[k & 1];
-    const int ns = NS - q;  // slots that hold existing columns
-    // ---- LDS reads: the column tail for the norm first (rows > k+128 read the zero padding),
-    // then the slot values, so the norm's wait does not cover the slot reads
-    const double xa = col[k + 1 + lane], xb = col[k + 65 + lane];
-    double2 cv[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      cv[s] = *reinterpret_cast<const double2*>(col + 2 * c + 8 * (s + q));
-    const double xi = col[i < 128 ? i : 0];
-    // ---- reflector of column k (every wave, redundantly)
-    double ss = fma(xa, xa, xb * xb);
-    ss = wave_sum_dpp(ss);
-    const double x0 = col[k + 1];
-    const double tail = ss - x0 * x0;
-    double beta = 0.0, v0 = x0;
-    if (tail > 0.0) {
-      const double nrm = sqrt(ss);
-      const double alpha = x0 > 0.0 ? -nrm : nrm;
-      v0 = x0 - alpha;
-      beta = 2.0 / (tail + v0 * v0);
-      if (tid == 0) e2[k] = alpha * alpha;
-    } else if (tid == 0) {
-      e2[k] = x0 * x0;
-    }
-    if (tid == 0) dg[k] = col[k];
-    ER_STAMP(6)
-    if (beta != 0.0) {
-      // ---- (B) p = A' v.  v_j = col[j] for j > k+1, v0 at k+1 (slot 0, element (k+1)&1 of
-      // class ((k+1)>>1)&3), 0 for j <= k (zeroed rows of the column buffer)
-      const int jn = k + 1;
-      const bool own = c == ((jn >> 1) & 3);
-      if (own) {
-        if (jn & 1) cv[0].y = v0; else cv[0].x = v0;
-      }
-      // the pivot entry j = k holds the diagonal in the column buffer: v_k = 0.  Column k is in
-      // slot 0 unless the slots were just shifted past it.
-      if (((k + 1) & 7) != 0 && c == ((k >> 1) & 3)) {
-        if (k & 1) cv[0].y = 0.0; else cv[0].x = 0.0;
-      }
-      const double vi = i > k ? (i == jn ? v0 : xi) : 0.0;
-      const bool wave_live = w * 16 + 15 > k;  // wave-uniform: some row of this wave is active
-      double pp = 0.0, pq = 0.0;  // two FMA chains
-      // slots in groups of 4 behind one uniform branch each (a per-slot condition gets
-      // if-converted into computing everything plus selects)
-      if (wave_live) {
-#pragma unroll
-        for (int g = 0; g < NS / 4; ++g) {
-          if (4 * g < ns) {
-#pragma unroll
-            for (int s = 4 * g; s < 4 * g + 4; ++s) {
-              pp = fma(a[s][0], cv[s].x, pp);
-              pq = fma(a[s][1], cv[s].y, pq);
-            }
-          }
-        }
-      }
-      pp += pq;
-      ER_STAMP(7)
-      pp = xsum32(xsum16(pp));
-      double t = 0.0;
-      if (c == 0) {
-        if (i < 128) pb[i] = i > k ? pp : 0.0;
-        t = vi * pp;
-      }
-      t = wave_sum_dpp(t);
-      if (lane == 0) redw[w] = t;
-      ER_STAMP(1)
-      __syncthreads();
-      ER_STAMP(2)
-      // ---- (C) w = beta p - K v;  A' -= v w^T + w v^T
-      double tot = redw[0];
-#pragma unroll
-      for (int r = 1; r < 8; ++r) tot += redw[r];
-      const double Kc = beta * beta * tot * 0.5;
-      double2 pv[NS];
+  // the owners of row r (wave r >> 4, lane r & 15 of every class) write all 32 entries
+  auto publish_row = [&](int r, double* dst) {
+    if (rb == (r >> 4) && t16 == (r & 15)) {
 #pragma unroll
       for (int s = 0; s < NS; ++s)
-        pv[s] = *reinterpret_cast<const double2*>(pb + 2 * c + 8 * (s + q));
-      // a_ij -= v_i w_j + w_i v_j with w = beta p - K v:  a_ij += g_i v_j - h_i p_j,
-      // g_i = K v_i - w_i, h_i = beta v_i
-      const double wi = beta * pp - Kc * vi;
-      const double gi = Kc * vi - wi, hi = beta * vi;
-      if (wave_live) {
-#pragma unroll
-        for (int g = 0; g < NS / 4; ++g) {
-          if (4 * g < ns) {
-#pragma unroll
-            for (int s = 4 * g; s < 4 * g + 4; ++s) {
-              a[s][0] = fma(gi, cv[s].x, fma(-hi, pv[s].x, a[s][0]));
-              a[s][1] = fma(gi, cv[s].y, fma(-hi, pv[s].y, a[s][1]));
-            }
-          }
-        }
+        *reinterpret_cast<double2*>(dst + 2 * c + 8 * s) = make_double2(a[s][0], a[s][1]);
+    }
+  };
+  const int j0 = 2 * c + 8 * t16;  // this lane's column pair (its slot of the v/p broadcasts)
+  // The reflector of column r from row r of the current matrix, computed by every wave
+  // redundantly (no barrier): x = the row at j0, j0+1 (this lane's slot), i (this lane's row),
+  // r (the diagonal) and r+1.  v_j = 0 (j <= r), v0 (j = r+1), x_j (j > r+1); H = I - beta v v^T.
+  double cx = 0.0, cy = 0.0, vi = 0.0, beta = 0.0, v0 = 0.0;
+  // the update of one group of 4 slots: a_ij += g_i v_j - h_i p_j (mhi = -h_i)
+  auto upd_group = [&](auto G, double px, double py, double gi, double mhi) {
+    constexpr int g = decltype(G)::value;
+    static_for<4 * g, 4 * g + 4>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      fmac_bcast<s, s == 4 * g>(a[s][0], px, mhi);
+      fmac_bcast<s, false>(a[s][1], py, mhi);
+      fmac_bcast<s, false>(a[s][0], cx, gi);
+      fmac_bcast<s, false>(a[s][1], cy, gi);
+    });
+  };
+  // Reflector of column r from x = row r of the current matrix (at j0, j0+1, i, r, r+1), every
+  // wave redundantly: v_j = 0 (j <= r), v0 (j = r+1), x_j (j > r+1); H = I - beta v v^T.  The
+  // sum of squares is a wave reduction whose six steps are interleaved (sched_barrier) with the
+  // four slot groups of the pending update `upd(g)` (in-order issue: the update's FMAs fill the
+  // reduction's latency).
+  auto reflector = [&](int r, double xj0, double xj1, double xi, double xr, double x0, auto&& upd) {
+    double tl = (j0 >= r + 2 ? xj0 * xj0 : 0.0);
+    tl = fma(j0 + 1 >= r + 2 ? xj1 : 0.0, xj1, tl);
+    tl += dpp_d<0xB1>(tl);
+    __builtin_amdgcn_sched_barrier(0);
+    upd(std::integral_constant<int, 0>{});
+    __builtin_amdgcn_sched_barrier(0);
+    tl += dpp_d<0x4E>(tl);
+    __builtin_amdgcn_sched_barrier(0);
+    upd(std::integral_constant<int, 1>{});
+    __builtin_amdgcn_sched_barrier(0);
+    tl += dpp_d<0x141>(tl);
+    __builtin_amdgcn_sched_barrier(0);
+    upd(std::integral_constant<int, 2>{});
+    __builtin_amdgcn_sched_barrier(0);
+    tl += dpp_d<0x140>(tl);
+    __builtin_amdgcn_sched_barrier(0);
+    upd(std::integral_constant<int, 3>{});
+    __builtin_amdgcn_sched_barrier(0);
+    tl = xsum32(xsum16(tl));  // sum_{j >= r+2} x_j^2 over the wave
+    beta = 0.0;
+    v0 = x0;
+    double e2r = x0 * x0;
+    if (tl > 0.0) {
+      const double ss = fma(x0, x0, tl);
+      double nrm;
+      if (ss > 0x1p-900) {  // Newton-refined hardware rsq / rcp (~1 ulp), no IEEE sqrt/div chain
+        double rs = __builtin_amdgcn_rsq(ss);
+        rs = rs * fma(-0.5 * ss, rs * rs, 1.5);
+        nrm = ss * rs;
+        nrm = fma(fma(-nrm, nrm, ss), 0.5 * rs, nrm);
+      } else {
+        nrm = sqrt(ss);
       }
+      const double alpha = x0 > 0.0 ? -nrm : nrm;
+      v0 = x0 - alpha;
+      const double q = fma(v0, v0, tl);
+      double rc = __builtin_amdgcn_rcp(q);
+      rc = fma(fma(-q, rc, 1.0), rc, rc);
+      rc = fma(fma(-q, rc, 1.0), rc, rc);
+      beta = 2.0 * rc;
+      e2r = alpha * alpha;
     }
-    // ---- publish column k+1 from slot 0 of its owners; rows <= k+1-1 written as 0
-    {
-      const int jn = k + 1;
-      if (c == ((jn >> 1) & 3) && i < 128) colb[jn & 1][i] = (i >= jn && rowok) ? ((jn & 1) ? a[0][1] : a[0][0]) : 0.0;
+    if (tid == 0) {
+      dg[r] = xr;
+      e2[r] = e2r;
     }
-    ER_STAMP(3)
-    __syncthreads();
-    ER_STAMP(4)
-  }
-  // trailing 2x2 (or 1x1): column n-1 from slot 0 of its owners (after the last shift)
-  if (n >= 2) {
-    const int j1 = n - 1;
-    if (n >= 3 && ((n - 2 + 1) & 7) == 0) EIG_SHIFT_SLOTS();
-    if (c == ((j1 >> 1) & 3) && rowok && i >= n - 2) pb[i] = (j1 & 1) ? a[0][1] : a[0][0];
-  }
-#undef EIG_SHIFT_SLOTS
+    cx = j0 <= r ? 0.0 : (j0 == r + 1 ? v0 : xj0);
+    cy = j0 + 1 <= r ? 0.0 : (j0 + 1 == r + 1 ? v0 : xj1);
+    vi = i > r ? (i == r + 1 ? v0 : xi) : 0.0;
+    if (w == 0) *reinterpret_cast<double2*>(&vb[r & 1][j0]) = make_double2(cx, cy);
+  };
+  publish_row(0, rowb[0]);
+  if (n >= 2) publish_row(1, rowb[1]);
   __syncthreads();
-  if (tid == 0) {
-    if (n >= 2) {
-      const double* col = colb[(n - 2) & 1];  // column n-2 (published at k = n-3, or initial)
-      dg[n - 2] = col[n - 2];
-      dg[n - 1] = pb[n - 1];
-      const double e = col[n - 1];
-      e2[n - 2] = e * e;
-    } else {
-      dg[0] = colb[0][0];
-    }
+  if (n >= 2) {
+    const double2 xr = *reinterpret_cast<const double2*>(&rowb[0][j0]);
+    reflector(0, xr.x, xr.y, rowb[0][i], rowb[0][0], rowb[0][1], [](auto) {});
+  } else if (tid == 0) {
+    dg[0] = rowb[0][0];
   }
+  ER_STAMP(0)
+  for (int k = 0; k + 2 < n; ++k) {
+    const int lo = (k + 1) >> 3;               // slots s < lo hold columns <= k only
+    const bool wave_live = rb * 16 + 15 > k;   // wave-uniform: some row of this wave is active
+    // ---- p = A' v (registers) and this wave's part of v^T p; four FMA chains
+    double pa[4] = {0.0, 0.0, 0.0, 0.0};
+    // slots in groups of 4 behind one uniform branch each (a per-slot condition gets
+    // if-converted into computing everything plus selects)
+    if (wave_live && !(DBG & 2)) {
+      static_for<0, NS / 4>([&](auto G) {
+        constexpr int g = decltype(G)::value;
+        if (4 * g + 3 >= lo) {
+          static_for<4 * g, 4 * g + 4>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            // cx/cy were written by VALU selects: wait states before the first DPP read
+            fmac_bcast<s, s == 4 * g>(pa[2 * (s & 1)], cx, a[s][0]);
+            fmac_bcast<s, false>(pa[2 * (s & 1) + 1], cy, a[s][1]);
+          });
+        }
+      });
+    }
+    ER_STAMP(1)
+    double pp = (pa[0] + pa[1]) + (pa[2] + pa[3]);
+    pp = xsum32(xsum16(pp));
+    double t = 0.0;
+    if (c == 0) {
+      pb[k & 1][i] = i > k ? pp : 0.0;
+      t = vi * pp;
+    }
+    t = row16_sum(t);  // only lanes 0..15 (class 0) carry a row's v_i p_i
+    if (lane == 0) redw[k & 1][w] = t;
+    ER_STAMP(2)
+    __syncthreads();
+    ER_STAMP(3)
+    // ---- every LDS read of the step at once
+    const int r = k + 1;
+    const double* old = rowb[r & 1];
+    const double2 w01 = *reinterpret_cast<const double2*>(&redw[k & 1][0]);
+    const double2 w23 = *reinterpret_cast<const double2*>(&redw[k & 1][2]);
+    const double2 w45 = *reinterpret_cast<const double2*>(&redw[k & 1][4]);
+    const double2 w67 = *reinterpret_cast<const double2*>(&redw[k & 1][6]);
+    const double2 pvr = *reinterpret_cast<const double2*>(&pb[k & 1][j0]);
+    const double2 o = *reinterpret_cast<const double2*>(old + j0);
+    const double oi = old[i], orr = old[r], or1 = old[r + 1];
+    const double vr = vb[k & 1][r], vr1 = vb[k & 1][r + 1];
+    const double pr = pb[k & 1][r], pr1 = pb[k & 1][r + 1];
+    // ---- w = beta p - K v;  A' -= v w^T + w v^T, i.e. a_ij += g_i v_j - h_i p_j with
+    // g_i = K v_i - w_i, h_i = beta v_i
+    const double tot = ((w01.x + w01.y) + (w23.x + w23.y)) + ((w45.x + w45.y) + (w67.x + w67.y));
+    const double Kc = beta * beta * tot * 0.5;
+    const double wi = beta * pp - Kc * vi;
+    const double gi = Kc * vi - wi, mhi = -(beta * vi);
+    // row r = k+1 after this update, recomputed by every lane from the published row with the
+    // owners' own operations (bitwise their registers): x_j = a_rj + g_r v_j - h_r p_j
+    const double wr = beta * pr - Kc * vr;
+    const double gr = Kc * vr - wr, mhr = -(beta * vr);
+    const double xj0 = fma(cx, gr, fma(pvr.x, mhr, o.x));
+    const double xj1 = fma(cy, gr, fma(pvr.y, mhr, o.y));
+    const double xi = fma(vi, gr, fma(pp, mhr, oi));
+    const double xr = fma(vr, gr, fma(pr, mhr, orr));
+    const double x0 = fma(vr1, gr, fma(pr1, mhr, or1));
+    ER_STAMP(4)
+    // the pending update (old v in cx/cy) runs inside the reflector's reduction
+    const double pxu = pvr.x, pyu = pvr.y;
+    const bool upd_live = wave_live && !(DBG & 1);
+    reflector(r, xj0, xj1, xi, xr, x0, [&](auto G) {
+      constexpr int g = decltype(G)::value;
+      if (upd_live && 4 * g + 3 >= lo) upd_group(G, pxu, pyu, gi, mhi);
+    });
+    ER_STAMP(5)
+    // the owners of row k+2 publish it (after their update) for the step after next; rowb[k&1]
+    // was last read before this step's barrier
+    publish_row(k + 2, rowb[k & 1]);
+    ER_STAMP(6)
+  }
+  // the last diagonal entry: row n-1 as its owners published it at the last step (or at the start)
+  __syncthreads();
+  if (tid == 0 && n >= 2) dg[n - 1] = rowb[(n - 1) & 1][n - 1];
   __syncthreads();
   // Gershgorin interval of the tridiagonal: row r in thread r (waves 0-1), wave min/max, then
   // the two wave results through LDS (the masks words are free until the multisection)
@@ -515,28 +575,36 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     }
   }
   __syncthreads();
-  // ---- 512-way multisection: 6 rounds of 9 bits bracket lambda_min to 2^-54 of the Gershgorin
-  // span, below the Sturm count's own backward error (~n eps ||T||), so a 7th round adds noise
+  // ---- 256-way multisection on waves 0-3 (one per SIMD: a count is a 128-row chain of ~5 VALU
+  // instructions per row, so a second wave per SIMD would double the round's issue time for one
+  // more bit): 7 rounds of 8 bits bracket lambda_min to 2^-56 of the Gershgorin span, below the
+  // Sturm count's own backward error (~n eps ||T||)
   double lo = bnd[0], hi = bnd[1];
   const int nr = (n + 7) & ~7;
-  for (int it = 0; it < 6; ++it) {
+  for (int it = 0; it < 7; ++it) {
     const double width = hi - lo;
-    const double sigma = lo + width * ((double)(tid + 1) / 513.0);
-    const unsigned long long mk = __ballot(sturm_any_below(sd, se, nr, sigma));
-    if (lane == 0) masks[w] = mk;
+    if (w < 4) {
+      const double sigma = lo + width * ((double)(tid + 1) / 257.0);
+      const unsigned long long mk = __ballot(sturm_any_below(sd, se, nr, sigma));
+      if (lane == 0) masks[w] = mk;
+    }
     __syncthreads();
     int f = -1;
-    for (int q = 0; q < 8 && f < 0; ++q)
+    for (int q = 0; q < 4 && f < 0; ++q)
       if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
     __syncthreads();
     if (f < 0) {
-      lo = lo + width * (512.0 / 513.0);
+      lo = lo + width * (256.0 / 257.0);
     } else {
-      hi = lo + width * ((double)(f + 1) / 513.0);
-      if (f > 0) lo = lo + width * ((double)f / 513.0);
+      hi = lo + width * ((double)(f + 1) / 257.0);
+      if (f > 0) lo = lo + width * ((double)f / 257.0);
     }
   }
-  ER_STAMP(5)
+  ER_STAMP(7)
+#ifdef CLRSDP_EIGREG_STAMPS
+  if (tid == 0)
+    for (int q = 0; q < 8; ++q) atomicAdd(&g_eigreg_stamps[q], st_acc[q]);
+#endif
   if (tid == 0) out[blockIdx.x] = __builtin_ldexp((lo + hi) * 0.5, bnd_ex + ex0);
 #undef ER_STAMP
 }
@@ -848,29 +916,6 @@ namespace clrsdp {
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-// Compile-time loop (the DPP lane selector of row_newbcast is an instruction immediate).
-template <int K, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (K < E) {
-    f(std::integral_constant<int, K>{});
-    static_for<K + 1, E>(f);
-  }
-}
-// acc += src[lane J of this lane's 16-lane DPP row] * mul: one v_fmac_f64_dpp with
-// row_newbcast (the f64 DPP form of CDNA3/4; the builtin route costs a copy + v_mov_b64_dpp +
-// v_fma_f64 and serialises on the copy register).  A DPP source needs 2 wait states after a
-// VALU write, which the compiler does not see inside inline asm: NOP = true puts an s_nop 1
-// in front.  The statements are volatile, so they keep their program order among themselves.
-template <int J, bool NOP>
-__device__ __forceinline__ void fmac_bcast(double& acc, double src, double mul) {
-  if constexpr (NOP)
-    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                 : "+v"(acc) : "v"(src), "v"(mul), "n"(J));
-  else
-    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                 : "+v"(acc) : "v"(src), "v"(mul), "n"(J));
 }
 
 // One wave: Cholesky factor and inverse of the 16x16 diagonal tile at (k0, k0) of the LDS image,

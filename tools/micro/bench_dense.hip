@@ -24,7 +24,7 @@ int main(int argc, char** argv) {
       }
   }
   double *dA, *dO, *dE;
-  CK(hipMalloc(&dA, h.size() * 8)); CK(hipMalloc(&dO, h.size() * 8)); CK(hipMalloc(&dE, nb * 8));
+  CK(hipMalloc(&dA, h.size() * 8)); CK(hipMalloc(&dO, h.size() * 8)); CK(hipMalloc(&dE, 2 * nb * 8));
   CK(hipMemcpy(dA, h.data(), h.size() * 8, hipMemcpyHostToDevice));
   std::vector<MatDesc<double>> din(nb), dout(nb);
   for (int b = 0; b < nb; ++b) { din[b] = {dA + (size_t)b * n * n, n, n}; dout[b] = {dO + (size_t)b * n * n, n, n}; }
@@ -86,10 +86,20 @@ int main(int argc, char** argv) {
   {
     unsigned long long st[8];
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_eigreg_stamps), sizeof(st)));
-    const char* names[] = {"load", "B:reduce", "barrier1", "C:update", "barrier2", "sturm", "reflector", "symv"};
+    const char* names[] = {"init", "matvec", "p sums+write", "barrier", "reads,Kc,x", "reflector+upd", "publish", "sturm"};
     for (int q = 0; q < 8; ++q) printf("  eigreg stamp %-12s %10.0f cycles per matrix\n", names[q], st[q] / (3.0 * nb));
   }
 #endif
+  for (int dbg : {1, 2, 3}) {
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < 3; ++r) {
+      if (dbg == 1) eigmin_reg<1><<<nb, 512>>>(ddin, dE + nb);
+      if (dbg == 2) eigmin_reg<2><<<nb, 512>>>(ddin, dE + nb);
+      if (dbg == 3) eigmin_reg<3><<<nb, 512>>>(ddin, dE + nb);
+    }
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("eigmin_reg<dbg %d (1 no update, 2 no matvec)>: %.1f us\n", dbg, ms * 1e3 / 3);
+  }
   double dmax = 0;
   for (int b = 0; b < nb; ++b) dmax = fmax(dmax, fabs(evl[b] - evr[b]));
   printf("  max |eigmin_lds - eigmin_reg| over the batch = %.3e (lambda_min[0] = %.15f)\n", dmax, evr[0]);
