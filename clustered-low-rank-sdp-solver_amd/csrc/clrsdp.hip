@@ -1196,11 +1196,16 @@ struct Solver final : HandleBase {
 
   // ---------------- stages
   void st_mu_r(const clrsdp_params* prm, int pd_feas) {
+    mu_scalars(prm, pd_feas);
+    mu_r_gemm();
+  }
+  // mu = <X,Y>/dim, mu_p (and the status words cleared, the halt word decided)
+  void mu_scalars(const clrsdp_params* prm, int pd_feas) {
     blk_dot(X, Y, nullptr, nullptr, 0, SC_DOT_XY, 1, upart);
     zero_info = true;  // the first scalar launch of an iteration clears the status words
     scalars(prm, pd_feas, 0);
-    gemm_diag(p_XY, -1.0, 0.0, SC_MU_P);         // R = mu_p I - XY
   }
+  void mu_r_gemm() { gemm_diag(p_XY, -1.0, 0.0, SC_MU_P); }  // R = mu_p I - XY
   // sum/max over the local blocks into sc[slot], all-gathered and rank-reduced when world > 1;
   // part: the flat_reduce partials are already there (<X,Y>, from update_state)
   void blk_dot(const T* A, const T* B_, const T* dA, const T* dB, int op, int slot, int tag,
