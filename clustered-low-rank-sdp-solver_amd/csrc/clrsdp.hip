@@ -179,9 +179,21 @@ struct GemmPlan : PlanBase {
     g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldcin = ldcin; g.ldc = ldc;
     g.tn = cdiv(N, TILE);
     g.tile0 = 0;
-    g.pad = 0;
+    g.flags = 0;
+    g.alpha = g.beta = 0.0;
     ntiles.push_back((int)(cdiv(M, TILE) * g.tn));
     h.push_back(g);
+  }
+  // dyn: a mixed batch (fp64): op(A), op(B), alpha and beta per problem (gemm_f64_dyn)
+  bool dyn = false;
+  void add_op(bool opa, bool opb, double al, double be, const T* A, int lda, const T* B, int ldb,
+              const T* Cin, int ldcin, T* C, int ldc, int M, int N, int K) {
+    if (M <= 0 || N <= 0) return;
+    dyn = true;
+    add(A, lda, B, ldb, Cin, ldcin, C, ldc, M, N, K);
+    h.back().flags = (opa ? 1 : 0) | (opb ? 2 : 0) | 4;
+    h.back().alpha = al;
+    h.back().beta = be;
   }
   bool gemv = false;
   // sym: every problem square with an exactly symmetric result wanted (gemm_f64_lds SYM: the
@@ -189,10 +201,12 @@ struct GemmPlan : PlanBase {
   bool sym = false;
   void finalize() {
     if (h.empty()) return;
-    gemv = true;
+    gemv = !dyn;  // (a mixed batch always takes the tiled kernel)
     for (const auto& g : h) gemv = gemv && g.N == 1;
     if (gemv)  // one workgroup per 64 outputs
       for (size_t q = 0; q < h.size(); ++q) ntiles[q] = (int)cdiv(h[q].M, 64);
+    if (dyn && (gemv || sym || !std::is_same<T, double>::value))
+      throw ClrsdpError{CLRSDP_E_ARG, "mixed GEMM batch: fp64 matrices only"};
     if (sym) {
       if (gemv || !std::is_same<T, double>::value)
         throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: fp64 matrices only"};
@@ -226,6 +240,11 @@ struct GemmPlan : PlanBase {
     }
     if constexpr (std::is_same<T, double>::value) {
       const double* ds = reinterpret_cast<const double*>(dscal);
+      if (dyn) {  // alpha/beta come from the descriptors
+        gemm_f64_dyn<><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
+        HIPCHK(hipGetLastError());
+        return;
+      }
       if (sym) {
         if (beta != 0.0 || ds) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: beta = 0 only"};
         if (!ta && tb) gemm_f64_lds<false, true, 0, 32, 8, true><<<grid, 512, 0, s>>>(d, dt, alpha, 0.0);
@@ -453,9 +472,16 @@ struct Solver final : HandleBase {
   MatPlan<T> f_X, f_Y, f_S, f_Q, e_X, e_Y;
   // on-chip factorisation path (all sizes <= reg_nmax<T>()): L^-1 and MFMA products
   bool reg_blk = false, reg_S = false, reg_Q = false;
-  CholInvPlan<T> ci_XY, ci_S, ci_S11, ci_S22, ci_Q;
+  CholInvPlan<T> ci_XY, ci_S, ci_S22, ci_Q;
   GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2, q_qinv, q_qdy;
-  GemmPlan<T> q_L21, q_S22, q_M, q_X21;  // 2x2 blocked L^-1 of S (dim_S in (128, 256])
+  // fp64 FACTOR with every dim_S <= 256 (fac2): f_a = {W = L^-1 B | L21^T = L11^-1 S12, W1} and
+  // f_b = {W^T W | S22 - L21 L21^T, W1^T W1, B2 - L21 W1} as mixed batches, then (dim_S > 128)
+  // chol_inv(S22), f_c: W2 = L22^-1 B2', f_d: slab += W2^T W2; f_x1/f_x2: X21 (side stream)
+  GemmPlan<T> f_a, f_b, f_c, f_d, f_x1, f_x2;
+  bool fac2 = false;
+  T* B2p = nullptr;
+  bool pending_x21 = false;  // the solves wait for X21 (side stream, iterate)
+  hipEvent_t ev_x2 = nullptr, ev_x21 = nullptr;
   MatPlan<T> e_XY;                        // both step-length eigenproblems in one launch
   BlkDesc* d_blk = nullptr;      // all local blocks
   BlkDesc* d_blk_m = nullptr;    // local blocks with m > 1
@@ -587,7 +613,7 @@ struct Solver final : HandleBase {
     // graph-boundary and join idle time against the lost overlap)
     if (std::getenv("CLRSDP_ONE_STREAM")) aux = own_stream;
     else HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q})
+    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
     build_plans();
@@ -597,7 +623,7 @@ struct Solver final : HandleBase {
     // device memory is released with the process / hipDeviceReset; free what we own explicitly
     T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, TU, TW, BX, BY, AY,
                  tval, S, Wm, Bm, Qslab, Q, Qf, Qinv, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
-                 bvec, dyv, pvec, uvec, bpart, upart, eigX, tmpsc, tC, Stmp, own_send, Vt, Pres, pres, dres};
+                 bvec, dyv, pvec, uvec, bpart, upart, eigX, tmpsc, tC, Stmp, B2p, own_send, Vt, Pres, pres, dres};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
     if (comm) {
@@ -613,7 +639,7 @@ struct Solver final : HandleBase {
     for (char* r : ring_host)
       if (r) (void)hipHostFree(r);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ring_ev[0], ring_ev[1]})
+    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ring_ev[0], ring_ev[1]})
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
       if (g) (void)hipGraphExecDestroy(g);
@@ -656,6 +682,10 @@ struct Solver final : HandleBase {
       for (int c = 0; c < nc(); ++c)
         if (std::is_same<T, double>::value && Ds[oc[c]] > 128 && Ds[oc[c]] <= 256) ns += 2 * (Ds[oc[c]] - 128) * 128;
       Stmp = dmalloc<T>(ns);
+      int64_t nb2 = 0;
+      for (int c = 0; c < nc(); ++c)
+        if (std::is_same<T, double>::value && Ds[oc[c]] > 128 && Ds[oc[c]] <= 256) nb2 += (Ds[oc[c]] - 128) * n_y;
+      B2p = dmalloc<T>(nb2);
     }
     tmpsc = dmalloc<T>(8);
     ksamp = dmalloc<int>(nK);
@@ -701,8 +731,9 @@ struct Solver final : HandleBase {
     q_sx2.tb = q_sy2.tb = true;
     // L^-1 dM L^-T exactly symmetric: eigmin_reg reads it without a transposed copy
     q_sx2.sym = std::is_same<T, double>::value;
-    q_L21.tb = true;
-    q_S22.tb = true;
+    f_d.ta = true;
+    f_x1.tb = true;
+    fac2 = std::is_same<T, double>::value && reg_S;
     q_dx.ta = true;
     q_q2.ta = true;
     p_xinv.ta = true;
@@ -815,7 +846,8 @@ struct Solver final : HandleBase {
     std::vector<TupleDesc> td;
     std::vector<TupleBlock> tbk;
     int bi = 0;
-    int64_t s2off = 0;
+    int64_t s2off = 0, b2off = 0;
+    std::vector<MatDesc<T>> s11;  // S11 blocks of the 2x2-blocked clusters (chol_inv in ci_S)
     for (int c = 0; c < nc(); ++c) {
       const int j = oc[c];
       const int D = (int)Ds[j];
@@ -824,41 +856,56 @@ struct Solver final : HandleBase {
       T* Bc = Bm + c_Boff[c];
       const int64_t xo = c_xoff[c];
       f_S.add(Sc, D, D);
+      T* slab = Qslab + (int64_t)c * n_y * n_y;
+      const int ny = (int)n_y;
       if (!std::is_same<T, double>::value || D <= 128) {
         ci_S.add(Sc, D, D, Sc, D);
+        q_W.add(Sc, D, Bc, D, nullptr, 0, Wc, D, D, ny, D);
+        if (std::is_same<T, double>::value) {  // (mixed batches are fp64 only)
+          f_a.add_op(false, false, 1.0, 0.0, Sc, D, Bc, D, nullptr, 0, Wc, D, D, ny, D);    // W = L^-1 B
+          f_b.add_op(true, false, 1.0, 0.0, Wc, D, Wc, D, nullptr, 0, slab, ny, ny, ny, D); // W^T W
+        }
+        q_t.add(Sc, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D, 1, D);
+        q_dx.add(Sc, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D, 1, D);
       } else if (D <= 256) {
+        // S = [S11 S12; S21 S22] = L L^T with L = [L11 0; L21 L22] (SURVEY.md §3D with Cholesky):
+        // the critical path only needs W = L^-1 B and Q's slab; X21 = -L22^-1 L21 L11^-1 (the
+        // lower-left block of L^-1, for the solves) is formed on the side stream
         const int D1 = 128, D2 = D - 128;
         T* S11 = Sc;
+        T* S12 = Sc + (int64_t)D1 * D;
         T* S21 = Sc + D1;
         T* S22 = Sc + D1 + (int64_t)D1 * D;
-        T* T21 = Stmp + s2off;
-        T* T21b = T21 + (int64_t)D2 * D1;
+        T* T12 = Stmp + s2off;               // L11^-1 S12 = L21^T   (D1 x D2)
+        T* Mb = T12 + (int64_t)D2 * D1;      // L22^-1 L21           (D2 x D1)
+        T* B2 = B2p + b2off;                 // B2 - L21 W1          (D2 x n_y)
         s2off += 2 * (int64_t)D2 * D1;
-        ci_S11.add(S11, D1, D, S11, D);                                       // S11 <- L11^-1
-        q_L21.add(S21, D, S11, D, nullptr, 0, T21, D2, D2, D1, D1);           // L21 = S21 L11^-T
-        q_S22.add(T21, D2, T21, D2, S22, D, S22, D, D2, D2, D1);             // S22 -= L21 L21^T
-        ci_S22.add(S22, D2, D, S22, D);                                       // S22 <- L22^-1
-        q_M.add(S22, D, T21, D2, nullptr, 0, T21b, D2, D2, D1, D2);           // M = L22^-1 L21
-        q_X21.add(T21b, D2, S11, D, nullptr, 0, S21, D, D2, D1, D1);          // S21 <- -M L11^-1
-        // S12 (the upper-right block) still holds the assembled S: the products with L^-1
-        // below are split so that none of them reads it
-        q_W.add(S11, D, Bc, D, nullptr, 0, Wc, D, D1, (int)n_y, D1);          // W1 = L11^-1 B1
-        q_W.add(Sc + D1, D, Bc, D, nullptr, 0, Wc + D1, D, D2, (int)n_y, D);  // W2 = [X21 L22^-1] B
+        b2off += (int64_t)D2 * n_y;
+        s11.push_back(MatDesc<T>{S11, D1, D});                                          // S11 <- L11^-1
+        f_a.add_op(false, false, 1.0, 0.0, S11, D, S12, D, nullptr, 0, T12, D1, D1, D2, D1);
+        f_a.add_op(false, false, 1.0, 0.0, S11, D, Bc, D, nullptr, 0, Wc, D, D1, ny, D1);  // W1
+        f_b.add_op(true, false, -1.0, 1.0, T12, D1, T12, D1, S22, D, S22, D, D2, D2, D1);  // S22 - L21 L21^T
+        f_b.add_op(true, false, 1.0, 0.0, Wc, D, Wc, D, nullptr, 0, slab, ny, ny, ny, D1); // W1^T W1
+        f_b.add_op(true, false, -1.0, 1.0, T12, D1, Wc, D, Bc + D1, D, B2, D2, D2, ny, D1);  // B2'
+        ci_S22.add(S22, D2, D, S22, D);                                                 // S22 <- L22^-1
+        f_c.add(S22, D, B2, D2, nullptr, 0, Wc + D1, D, D2, ny, D2);                   // W2 = L22^-1 B2'
+        f_d.add(Wc + D1, D, Wc + D1, D, slab, ny, slab, ny, ny, ny, D2);               // slab += W2^T W2
+        f_x1.add(S22, D, T12, D1, nullptr, 0, Mb, D2, D2, D1, D2);                      // M = L22^-1 L21
+        f_x2.add(Mb, D2, S11, D, nullptr, 0, S21, D, D2, D1, D1);                       // S21 <- -M L11^-1
+        // S12 keeps the assembled S: the products with L^-1 below are split so that none reads it
         q_t.add(S11, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D1, 1, D1);
         q_t.add(Sc + D1, D, rhs + xo, D, nullptr, 0, tvec + xo + D1, D, D2, 1, D);
         // dx = (L^-1)^T u: columns 0..D1-1 of L^-1 are [L11^-1; X21], the rest L22^-1
         q_dx.add(Sc, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D1, 1, D);
         q_dx.add(S22, D, tmpv + xo + D1, D2, nullptr, 0, dx + xo + D1, D2, D2, 1, D2);
-      }
-      if (!(std::is_same<T, double>::value && D > 128 && D <= 256)) {
-        q_W.add(Sc, D, Bc, D, nullptr, 0, Wc, D, D, (int)n_y, D);
+      } else {
         q_t.add(Sc, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D, 1, D);
         q_dx.add(Sc, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D, 1, D);
       }
       q_Wdy.add(Wc, D, dyv, (int)n_y, tvec + xo, D, tmpv + xo, D, D, 1, (int)n_y);
       t_W.add(Sc, D, Wc, D, D, (int)n_y);
       t_t.add(Sc, D, tvec + xo, D, D, 1);
-      p_Q.add(Wc, D, Wc, D, nullptr, 0, Qslab + (int64_t)c * n_y * n_y, (int)n_y, (int)n_y, (int)n_y, D);
+      p_Q.add(Wc, D, Wc, D, nullptr, 0, slab, ny, ny, ny, D);
       p_By.add(Bc, D, y, (int)n_y, nullptr, 0, tmpv + xo, D, D, 1, (int)n_y);
       p_Btx.add(Bc, D, x + xo, D, nullptr, 0, pslab + (int64_t)c * n_y, (int)n_y, (int)n_y, 1, D);
       p_Wt.add(Wc, D, tvec + xo, D, nullptr, 0, pslab + (int64_t)c * n_y, (int)n_y, (int)n_y, 1, D);
@@ -884,6 +931,7 @@ struct Solver final : HandleBase {
         tbk.push_back(t);
       }
     }
+    for (const MatDesc<T>& m1 : s11) ci_S.add(m1.A, m1.n, m1.lda, m1.A, m1.lda);  // after the single blocks
     t_Q.add(Qf, (int)n_y, dyv, (int)n_y, (int)n_y, 1);
     t_dxadd_init();
     f_Q.add(Qf, (int)n_y, (int)n_y);
@@ -904,9 +952,9 @@ struct Solver final : HandleBase {
     for (GemmPlan<T>* g : {&p_txy, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
-                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &q_L21, &q_S22, &q_M, &q_X21})
+                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &f_a, &f_b, &f_c, &f_d, &f_x1, &f_x2})
       g->finalize();
-    for (CholInvPlan<T>* c : {&ci_XY, &ci_S, &ci_S11, &ci_S22, &ci_Q}) c->finalize();
+    for (CholInvPlan<T>* c : {&ci_XY, &ci_S, &ci_S22, &ci_Q}) c->finalize();
     e_XY.finalize();
     for (TrsmPlan<T>* t : {&t_Linv, &t_W, &t_t, &t_Q, &t_sX1, &t_sX2, &t_sY1, &t_sY2, &t_dx})
       t->finalize();
@@ -1267,18 +1315,34 @@ struct Solver final : HandleBase {
     factor_local();
     factor_q();
   }
-  void factor_local() {
+  // side_x21: X21 on the side stream (the loop body), joined before the first solve
+  void factor_local(bool side_x21 = false) {
+    if (fac2) {                               // fp64: S_j <- L_j^-1 in place, W_j and Q's slabs
+      ci_S.launch(stream, info + info_S0);    // S (dim_S <= 128) and S11 blocks
+      f_a.launch(stream, 1.0, 0.0);
+      f_b.launch(stream, 1.0, 0.0);
+      if (nc2) {
+        ci_S22.launch(stream, info + info_S0 + nc());
+        if (side_x21) {
+          const hipStream_t main_s = stream;
+          HIPCHK(hipEventRecord(ev_x2, main_s));
+          HIPCHK(hipStreamWaitEvent(aux, ev_x2, 0));
+          f_x1.launch(aux, 1.0, 0.0);
+          f_x2.launch(aux, -1.0, 0.0);
+          HIPCHK(hipEventRecord(ev_x21, aux));
+          pending_x21 = true;
+        } else {
+          f_x1.launch(stream, 1.0, 0.0);
+          f_x2.launch(stream, -1.0, 0.0);
+        }
+        f_c.launch(stream, 1.0, 0.0);
+        f_d.launch(stream, 1.0, 1.0);
+      }
+      sum_q_slabs();
+      return;
+    }
     if (reg_S) {                              // S_j <- L_j^-1 in place; W_j = L_j^-1 B_j (MFMA)
       ci_S.launch(stream, info + info_S0);
-      if (nc2) {                              // 2x2 blocked L^-1 for 128 < dim_S <= 256
-        const int n1 = (int)ci_S.hin.size();
-        ci_S11.launch(stream, info + info_S0 + n1);
-        q_L21.launch(stream, 1.0, 0.0);
-        q_S22.launch(stream, -1.0, 1.0);
-        ci_S22.launch(stream, info + info_S0 + n1 + nc2);
-        q_M.launch(stream, 1.0, 0.0);
-        q_X21.launch(stream, -1.0, 0.0);
-      }
       q_W.launch(stream, 1.0, 0.0);
     } else {
       f_S.potrf(stream, info + info_S0);
@@ -1286,6 +1350,10 @@ struct Solver final : HandleBase {
       t_W.launch(stream, false);              // W_j = L_j^-1 B_j
     }
     p_Q.launch(stream, 1.0, 0.0);             // slab_j = W_j^T W_j
+    sum_q_slabs();
+  }
+  // Q = sum_j slab_j (all-gathered over the ranks)
+  void sum_q_slabs() {
     const int64_t q2 = n_y * n_y;
     if (world == 1 && nc()) {
       slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(Qslab, nc(), q2, q2, Q);
@@ -1394,6 +1462,10 @@ struct Solver final : HandleBase {
   // the three-stage solve and dx as separate batched launches (any word type / rank count)
   void direction_solves(int tag) {
     // t_j = L_j^-1 rhs_j ;  u = sum_j W_j^T t_j ;  dy = Q^-1 (p - u) ; dx_j = L_j^-T (t_j + W_j dy)
+    if (pending_x21) {  // X21 (lower-left block of L^-1) comes from the side stream
+      HIPCHK(hipStreamWaitEvent(stream, ev_x21, 0));
+      pending_x21 = false;
+    }
     if (reg_S) {
       q_t.launch(stream, 1.0, 0.0);
     } else {
@@ -1621,7 +1693,7 @@ struct Solver final : HandleBase {
       HIPCHK(hipEventRecord(ev_r, aux));
     });
     mark(CLRSDP_STAGE_FACTOR);
-    factor_local();
+    factor_local(true);
     // side stream: chol(Q) -> L_Q^-1, waited for just before the first Q solve
     HIPCHK(hipEventRecord(ev_qa, main_s));
     HIPCHK(hipStreamWaitEvent(aux, ev_qa, 0));
@@ -1644,6 +1716,10 @@ struct Solver final : HandleBase {
     if (pending_q) {
       HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
       pending_q = false;
+    }
+    if (pending_x21) {
+      HIPCHK(hipStreamWaitEvent(stream, ev_x21, 0));
+      pending_x21 = false;
     }
     if (timing) HIPCHK(hipEventRecord(ev[CLRSDP_NUM_STAGES], stream));
   }

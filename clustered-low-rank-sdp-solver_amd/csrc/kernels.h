@@ -37,7 +37,8 @@ template <class T> struct GemmDesc {
   int M, N, K, lda, ldb, ldcin, ldc;
   int tn;     // tiles along N
   int tile0;  // (unused by the TileRef kernels)
-  int pad;
+  int flags;  // gemm_f64_dyn: bit 0 op(A) = A^T, bit 1 op(B) = B^T, bit 2 alpha/beta below
+  double alpha, beta;  // gemm_f64_dyn with flags bit 2 (else the launch's)
 };
 
 template <class T> struct MatDesc {
@@ -118,22 +119,22 @@ __device__ inline int acc_col(int wn, int ni, int lr, int wcols = 32) { return w
 // SYM: square problems whose product is symmetric in exact arithmetic (L^-1 dM L^-T): the launch
 // covers the lower tiles only, each writes its tile and the mirror image, and a diagonal tile
 // mirrors its lower triangle -- the result is exactly symmetric (beta = 0, no diagonal term).
-template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false>
-__global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
-                                                        const TileRef* __restrict__ t2d,
-                                                        double alpha, double beta,
-                                                        const double* __restrict__ dscal = nullptr,
-                                                        double dmult = 0.0) {
+template <int BK, int NW>
+constexpr int gemm_f64_smem() {
+  return 2 * lds_gemm::Slab<BK, 64 * NW>::SZ > 64 * lds_gemm::TP ? 2 * lds_gemm::Slab<BK, 64 * NW>::SZ
+                                                                 : 64 * lds_gemm::TP;
+}
+// one 64x64 output tile t of problem d (the body of every fp64 GEMM launch)
+template <bool TA, bool TB, int BK, int NW, bool SYM>
+__device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, double* smem,
+                                              double alpha, double beta,
+                                              const double* __restrict__ dscal, double dmult) {
   using namespace lds_gemm;
   constexpr int NTH = 64 * NW, WN = NW / 2, NI = 4 / WN, WC = 64 / WN;
   using SL = Slab<BK, NTH>;
   constexpr int PER = SL::PER;
-  __shared__ double smem[2 * SL::SZ > 64 * TP ? 2 * SL::SZ : 64 * TP];
   double* As = smem;
   double* Bs = smem + SL::SZ;
-  const TileRef tr = t2d[blockIdx.x];
-  const GemmDesc<double> d = descs[tr.p];
-  const int t = tr.t;
   const int m0 = (t / d.tn) * 64, n0 = (t % d.tn) * 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w % WN, lr = lane & 15, lk = lane >> 4;
@@ -212,6 +213,36 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* 
         d.C[row + (size_t)col * d.ldc] = v;
       }
     }
+  }
+}
+
+template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false>
+__global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
+                                                        const TileRef* __restrict__ t2d,
+                                                        double alpha, double beta,
+                                                        const double* __restrict__ dscal = nullptr,
+                                                        double dmult = 0.0) {
+  __shared__ double smem[gemm_f64_smem<BK, NW>()];
+  const TileRef tr = t2d[blockIdx.x];
+  const GemmDesc<double> d = descs[tr.p];
+  gemm_f64_tile<TA, TB, BK, NW, SYM>(d, tr.t, smem, alpha, beta, dscal, dmult);
+}
+
+// Mixed batch: op(A), op(B) and (flags bit 2) alpha/beta per problem, so independent products of
+// different shapes share one launch (one uniform branch per workgroup picks the instantiation).
+template <int BK = 32, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void gemm_f64_dyn(const GemmDesc<double>* __restrict__ descs,
+                                                        const TileRef* __restrict__ t2d,
+                                                        double alpha, double beta) {
+  __shared__ double smem[gemm_f64_smem<BK, NW>()];
+  const TileRef tr = t2d[blockIdx.x];
+  const GemmDesc<double> d = descs[tr.p];
+  const double al = (d.flags & 4) ? d.alpha : alpha, be = (d.flags & 4) ? d.beta : beta;
+  switch (d.flags & 3) {
+    case 0: gemm_f64_tile<false, false, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
+    case 1: gemm_f64_tile<true, false, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
+    case 2: gemm_f64_tile<false, true, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
+    default: gemm_f64_tile<true, true, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
   }
 }
 
