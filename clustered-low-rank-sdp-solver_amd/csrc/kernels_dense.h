@@ -293,10 +293,12 @@ __device__ inline bool sturm_any_below(const double* __restrict__ sd, const doub
   return acc < 0;
 }
 
-template <int DBG = 0>  // DBG (timing experiments only): 1 = no update FMAs, 2 = no matvec FMAs
-__global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restrict__ descs,
-                                                  double* __restrict__ out) {
-  constexpr int NS = 16;
+// NWV waves (8: one row block per wave, two waves per SIMD; 4: two row blocks per lane, one wave
+// per SIMD, so the redundant per-column reflector chain costs each SIMD half the issue slots).
+template <int DBG = 0, int NWV = 8>  // DBG (timing experiments only): 1 = no update FMAs, 2 = no matvec FMAs
+__global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __restrict__ descs,
+                                                        double* __restrict__ out) {
+  constexpr int NS = 16, RPL = 8 / NWV;
 #ifdef CLRSDP_EIGREG_STAMPS
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -311,30 +313,41 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
   __shared__ __attribute__((aligned(16))) double rowb[2][128];
   __shared__ __attribute__((aligned(16))) double pb[2][128];
   __shared__ __attribute__((aligned(16))) double vb[2][128];
-  __shared__ double redw[2][8];
+  __shared__ __attribute__((aligned(16))) double redw[2][8];
   __shared__ double dg[128], e2[128];
   __shared__ __attribute__((aligned(16))) double sd[128], se[128];
   __shared__ double bnd[2];
   __shared__ unsigned long long masks[8];
   const MatDesc<double> d = descs[blockIdx.x];
   const int n = d.n, lda = d.lda, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  // row block of wave w: waves w and w+4 share a SIMD, so they get blocks that go idle early and
-  // late (0/7, 1/6, 2/5, 3/4): every SIMD then carries the same number of live-row columns
-  const int rb = w < 4 ? w : 11 - w;
-  const int c = lane >> 4, t16 = lane & 15, i = rb * 16 + t16;
-  const bool rowok = i < n;
-  // a[s][e] = A(i, 2c + 8s + e).  The input is exactly symmetric (the step-length product is
-  // written by the symmetric GEMM epilogue), so only coalesced A(i, j) loads are needed.
-  double a[NS][2];
+  // row blocks of the lanes of wave w, paired so that every SIMD carries blocks that go idle
+  // early and late (0/7, 1/6, 2/5, 3/4): NWV = 8, waves w and w+4 share a SIMD; NWV = 4, one
+  // wave holds both blocks
+  int blk[RPL];
+  if constexpr (RPL == 1) {
+    blk[0] = w < 4 ? w : 11 - w;
+  } else {
+    blk[0] = w;
+    blk[1] = 7 - w;
+  }
+  const int c = lane >> 4, t16 = lane & 15;
+  int i[RPL];
 #pragma unroll
-  for (int s = 0; s < NS; ++s)
+  for (int h = 0; h < RPL; ++h) i[h] = blk[h] * 16 + t16;
+  // a[h][s][e] = A(i_h, 2c + 8s + e).  The input is exactly symmetric (the step-length product
+  // is written by the symmetric GEMM epilogue), so only coalesced A(i, j) loads are needed.
+  double a[RPL][NS][2];
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = 2 * c + 8 * s + e;
-      const int ic = min(i, n - 1), jc = min(j, n - 1);  // unconditional loads, masked after
-      const double v = gload(d.A + ic + (size_t)jc * lda);
-      a[s][e] = (rowok && j < n) ? v : 0.0;
-    }
+  for (int h = 0; h < RPL; ++h)
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * c + 8 * s + e;
+        const int ic = min(i[h], n - 1), jc = min(j, n - 1);  // unconditional loads, masked after
+        const double v = gload(d.A + ic + (size_t)jc * lda);
+        a[h][s][e] = (i[h] < n && j < n) ? v : 0.0;
+      }
   // scale the block by 2^-ex0 so that its largest entry lies in [0.5, 1): the column norms of the
   // Householder reduction neither overflow nor underflow for any block norm in fp64 range (exact,
   // undone on the result)
@@ -342,51 +355,62 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
   {
     double amax = 0.0;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) amax = fmax(amax, fmax(fabs(a[s][0]), fabs(a[s][1])));
+    for (int h = 0; h < RPL; ++h)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) amax = fmax(amax, fmax(fabs(a[h][s][0]), fabs(a[h][s][1])));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
     if (lane == 0) redw[0][w] = amax;
     __syncthreads();
     amax = redw[0][0];
 #pragma unroll
-    for (int r = 1; r < 8; ++r) amax = fmax(amax, redw[0][r]);
+    for (int r = 1; r < NWV; ++r) amax = fmax(amax, redw[0][r]);
     ex0 = (amax > 0.0 && amax < INFINITY) ? __builtin_amdgcn_frexp_exp(amax) : 0;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      a[s][0] = __builtin_ldexp(a[s][0], -ex0);
-      a[s][1] = __builtin_ldexp(a[s][1], -ex0);
-    }
-  }
-  // the owners of row r (wave r >> 4, lane r & 15 of every class) write all 32 entries
-  auto publish_row = [&](int r, double* dst) {
-    if (rb == (r >> 4) && t16 == (r & 15)) {
+    for (int h = 0; h < RPL; ++h)
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-        *reinterpret_cast<double2*>(dst + 2 * c + 8 * s) = make_double2(a[s][0], a[s][1]);
-    }
+      for (int s = 0; s < NS; ++s) {
+        a[h][s][0] = __builtin_ldexp(a[h][s][0], -ex0);
+        a[h][s][1] = __builtin_ldexp(a[h][s][1], -ex0);
+      }
+  }
+  // the owners of row r (lane r & 15 of every class, in the wave holding block r >> 4) write all
+  // 32 entries
+  auto publish_row = [&](int r, double* dst) {
+#pragma unroll
+    for (int h = 0; h < RPL; ++h)
+      if (blk[h] == (r >> 4) && t16 == (r & 15)) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          *reinterpret_cast<double2*>(dst + 2 * c + 8 * s) = make_double2(a[h][s][0], a[h][s][1]);
+      }
   };
   const int j0 = 2 * c + 8 * t16;  // this lane's column pair (its slot of the v/p broadcasts)
-  // The reflector of column r from row r of the current matrix, computed by every wave
-  // redundantly (no barrier): x = the row at j0, j0+1 (this lane's slot), i (this lane's row),
-  // r (the diagonal) and r+1.  v_j = 0 (j <= r), v0 (j = r+1), x_j (j > r+1); H = I - beta v v^T.
-  double cx = 0.0, cy = 0.0, vi = 0.0, beta = 0.0, v0 = 0.0;
-  // the update of one group of 4 slots: a_ij += g_i v_j - h_i p_j (mhi = -h_i)
-  auto upd_group = [&](auto G, double px, double py, double gi, double mhi) {
-    constexpr int g = decltype(G)::value;
+  double cx = 0.0, cy = 0.0, beta = 0.0, v0 = 0.0, vi[RPL];
+#pragma unroll
+  for (int h = 0; h < RPL; ++h) vi[h] = 0.0;
+  // the update of one group of 4 slots of row set h: a_ij += g_i v_j - h_i p_j (mhi = -h_i)
+  // (the p terms of the 8 entries first, then the v terms: a dependent pair is 8 issues apart)
+  auto upd_group = [&](auto G, auto H, double px, double py, double gi, double mhi) {
+    constexpr int g = decltype(G)::value, h = decltype(H)::value;
     static_for<4 * g, 4 * g + 4>([&](auto S) {
       constexpr int s = decltype(S)::value;
-      fmac_bcast<s, s == 4 * g>(a[s][0], px, mhi);
-      fmac_bcast<s, false>(a[s][1], py, mhi);
-      fmac_bcast<s, false>(a[s][0], cx, gi);
-      fmac_bcast<s, false>(a[s][1], cy, gi);
+      fmac_bcast<s, s == 4 * g>(a[h][s][0], px, mhi);
+      fmac_bcast<s, false>(a[h][s][1], py, mhi);
+    });
+    static_for<4 * g, 4 * g + 4>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      fmac_bcast<s, false>(a[h][s][0], cx, gi);
+      fmac_bcast<s, false>(a[h][s][1], cy, gi);
     });
   };
-  // Reflector of column r from x = row r of the current matrix (at j0, j0+1, i, r, r+1), every
-  // wave redundantly: v_j = 0 (j <= r), v0 (j = r+1), x_j (j > r+1); H = I - beta v v^T.  The
-  // sum of squares is a wave reduction whose six steps are interleaved (sched_barrier) with the
-  // four slot groups of the pending update `upd(g)` (in-order issue: the update's FMAs fill the
-  // reduction's latency).
-  auto reflector = [&](int r, double xj0, double xj1, double xi, double xr, double x0, auto&& upd) {
+  // Reflector of column r from x = row r of the current matrix (at j0, j0+1, the lane's rows,
+  // r and r+1), every wave redundantly: v_j = 0 (j <= r), v0 (j = r+1), x_j (j > r+1);
+  // H = I - beta v v^T.  The sum of squares is a wave reduction whose six steps are interleaved
+  // (sched_barrier) with the slot groups of the pending update `upd(g)` (in-order issue: the
+  // update's FMAs fill the reduction's latency).
+  auto reflector = [&](int r, double xj0, double xj1, const double* xi, double xr, double x0,
+                       auto&& upd) {
     double tl = (j0 >= r + 2 ? xj0 * xj0 : 0.0);
     tl = fma(j0 + 1 >= r + 2 ? xj1 : 0.0, xj1, tl);
     tl += dpp_d<0xB1>(tl);
@@ -435,7 +459,8 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     }
     cx = j0 <= r ? 0.0 : (j0 == r + 1 ? v0 : xj0);
     cy = j0 + 1 <= r ? 0.0 : (j0 + 1 == r + 1 ? v0 : xj1);
-    vi = i > r ? (i == r + 1 ? v0 : xi) : 0.0;
+#pragma unroll
+    for (int h = 0; h < RPL; ++h) vi[h] = i[h] > r ? (i[h] == r + 1 ? v0 : xi[h]) : 0.0;
     if (w == 0) *reinterpret_cast<double2*>(&vb[r & 1][j0]) = make_double2(cx, cy);
   };
   publish_row(0, rowb[0]);
@@ -443,40 +468,52 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
   __syncthreads();
   if (n >= 2) {
     const double2 xr = *reinterpret_cast<const double2*>(&rowb[0][j0]);
-    reflector(0, xr.x, xr.y, rowb[0][i], rowb[0][0], rowb[0][1], [](auto) {});
+    double xi0[RPL];
+#pragma unroll
+    for (int h = 0; h < RPL; ++h) xi0[h] = rowb[0][i[h]];
+    reflector(0, xr.x, xr.y, xi0, rowb[0][0], rowb[0][1], [](auto) {});
   } else if (tid == 0) {
     dg[0] = rowb[0][0];
   }
   ER_STAMP(0)
   for (int k = 0; k + 2 < n; ++k) {
-    const int lo = (k + 1) >> 3;               // slots s < lo hold columns <= k only
-    const bool wave_live = rb * 16 + 15 > k;   // wave-uniform: some row of this wave is active
-    // ---- p = A' v (registers) and this wave's part of v^T p; four FMA chains
-    double pa[4] = {0.0, 0.0, 0.0, 0.0};
-    // slots in groups of 4 behind one uniform branch each (a per-slot condition gets
-    // if-converted into computing everything plus selects)
-    if (wave_live && !(DBG & 2)) {
-      static_for<0, NS / 4>([&](auto G) {
-        constexpr int g = decltype(G)::value;
-        if (4 * g + 3 >= lo) {
-          static_for<4 * g, 4 * g + 4>([&](auto S) {
-            constexpr int s = decltype(S)::value;
-            // cx/cy were written by VALU selects: wait states before the first DPP read
-            fmac_bcast<s, s == 4 * g>(pa[2 * (s & 1)], cx, a[s][0]);
-            fmac_bcast<s, false>(pa[2 * (s & 1) + 1], cy, a[s][1]);
-          });
-        }
-      });
-    }
-    ER_STAMP(1)
-    double pp = (pa[0] + pa[1]) + (pa[2] + pa[3]);
-    pp = xsum32(xsum16(pp));
+    const int lo = (k + 1) >> 3;  // slots s < lo hold columns <= k only
+    bool live[RPL];               // wave-uniform: some row of row set h is active
+#pragma unroll
+    for (int h = 0; h < RPL; ++h) live[h] = blk[h] * 16 + 15 > k;
+    // ---- p = A' v (registers) and this wave's part of v^T p; two FMA chains per row set
+    double pp[RPL];
     double t = 0.0;
-    if (c == 0) {
-      pb[k & 1][i] = i > k ? pp : 0.0;
-      t = vi * pp;
+    static_for<0, RPL>([&](auto H) {
+      constexpr int h = decltype(H)::value;
+      double pa[4] = {0.0, 0.0, 0.0, 0.0};
+      // slots in groups of 4 behind one uniform branch each (a per-slot condition gets
+      // if-converted into computing everything plus selects)
+      if (live[h] && !(DBG & 2)) {
+        static_for<0, NS / 4>([&](auto G) {
+          constexpr int g = decltype(G)::value;
+          if (4 * g + 3 >= lo) {
+            static_for<4 * g, 4 * g + 4>([&](auto S) {
+              constexpr int s = decltype(S)::value;
+              // cx/cy were written by VALU selects: wait states before the first DPP read
+              fmac_bcast<s, s == 4 * g>(pa[2 * (s & 1)], cx, a[h][s][0]);
+              fmac_bcast<s, false>(pa[2 * (s & 1) + 1], cy, a[h][s][1]);
+            });
+          }
+        });
+      }
+      pp[h] = (pa[0] + pa[1]) + (pa[2] + pa[3]);
+    });
+    ER_STAMP(1)
+#pragma unroll
+    for (int h = 0; h < RPL; ++h) {
+      pp[h] = xsum32(xsum16(pp[h]));
+      if (c == 0) {
+        pb[k & 1][i[h]] = i[h] > k ? pp[h] : 0.0;
+        t = fma(vi[h], pp[h], t);
+      }
     }
-    t = row16_sum(t);  // only lanes 0..15 (class 0) carry a row's v_i p_i
+    t = row16_sum(t);  // only lanes 0..15 (class 0) carry the rows' v_i p_i
     if (lane == 0) redw[k & 1][w] = t;
     ER_STAMP(2)
     __syncthreads();
@@ -484,37 +521,56 @@ __global__ __launch_bounds__(512) void eigmin_reg(const MatDesc<double>* __restr
     // ---- every LDS read of the step at once
     const int r = k + 1;
     const double* old = rowb[r & 1];
-    const double2 w01 = *reinterpret_cast<const double2*>(&redw[k & 1][0]);
-    const double2 w23 = *reinterpret_cast<const double2*>(&redw[k & 1][2]);
-    const double2 w45 = *reinterpret_cast<const double2*>(&redw[k & 1][4]);
-    const double2 w67 = *reinterpret_cast<const double2*>(&redw[k & 1][6]);
+    double rw[NWV];
+#pragma unroll
+    for (int q = 0; q < NWV; q += 2) {
+      const double2 v2 = *reinterpret_cast<const double2*>(&redw[k & 1][q]);
+      rw[q] = v2.x;
+      rw[q + 1] = v2.y;
+    }
     const double2 pvr = *reinterpret_cast<const double2*>(&pb[k & 1][j0]);
     const double2 o = *reinterpret_cast<const double2*>(old + j0);
-    const double oi = old[i], orr = old[r], or1 = old[r + 1];
+    double oi[RPL];
+#pragma unroll
+    for (int h = 0; h < RPL; ++h) oi[h] = old[i[h]];
+    const double orr = old[r], or1 = old[r + 1];
     const double vr = vb[k & 1][r], vr1 = vb[k & 1][r + 1];
     const double pr = pb[k & 1][r], pr1 = pb[k & 1][r + 1];
     // ---- w = beta p - K v;  A' -= v w^T + w v^T, i.e. a_ij += g_i v_j - h_i p_j with
     // g_i = K v_i - w_i, h_i = beta v_i
-    const double tot = ((w01.x + w01.y) + (w23.x + w23.y)) + ((w45.x + w45.y) + (w67.x + w67.y));
+    double tot;
+    if constexpr (NWV == 8)
+      tot = ((rw[0] + rw[1]) + (rw[2] + rw[3])) + ((rw[4] + rw[5]) + (rw[6] + rw[7]));
+    else
+      tot = (rw[0] + rw[1]) + (rw[2] + rw[3]);
     const double Kc = beta * beta * tot * 0.5;
-    const double wi = beta * pp - Kc * vi;
-    const double gi = Kc * vi - wi, mhi = -(beta * vi);
+    double gi[RPL], mhi[RPL];
+#pragma unroll
+    for (int h = 0; h < RPL; ++h) {
+      const double wi = beta * pp[h] - Kc * vi[h];
+      gi[h] = Kc * vi[h] - wi;
+      mhi[h] = -(beta * vi[h]);
+    }
     // row r = k+1 after this update, recomputed by every lane from the published row with the
     // owners' own operations (bitwise their registers): x_j = a_rj + g_r v_j - h_r p_j
     const double wr = beta * pr - Kc * vr;
     const double gr = Kc * vr - wr, mhr = -(beta * vr);
     const double xj0 = fma(cx, gr, fma(pvr.x, mhr, o.x));
     const double xj1 = fma(cy, gr, fma(pvr.y, mhr, o.y));
-    const double xi = fma(vi, gr, fma(pp, mhr, oi));
+    double xi[RPL];
+#pragma unroll
+    for (int h = 0; h < RPL; ++h) xi[h] = fma(vi[h], gr, fma(pp[h], mhr, oi[h]));
     const double xr = fma(vr, gr, fma(pr, mhr, orr));
     const double x0 = fma(vr1, gr, fma(pr1, mhr, or1));
     ER_STAMP(4)
     // the pending update (old v in cx/cy) runs inside the reflector's reduction
     const double pxu = pvr.x, pyu = pvr.y;
-    const bool upd_live = wave_live && !(DBG & 1);
     reflector(r, xj0, xj1, xi, xr, x0, [&](auto G) {
       constexpr int g = decltype(G)::value;
-      if (upd_live && 4 * g + 3 >= lo) upd_group(G, pxu, pyu, gi, mhi);
+      static_for<0, RPL>([&](auto H) {
+        constexpr int h = decltype(H)::value;
+        if (live[h] && !(DBG & 1) && 4 * g + 3 >= lo) upd_group(G, H, pxu, pyu, gi[h], mhi[h]);
+      });
     });
     ER_STAMP(5)
     // the owners of row k+2 publish it (after their update) for the step after next; rowb[k&1]

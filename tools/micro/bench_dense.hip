@@ -77,6 +77,19 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(evl.data(), dE, nb * 8, hipMemcpyDeviceToHost));
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipEventRecord(e0));
+    eigmin_reg<0, 4><<<nb, 256>>>(ddin, dE);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("eigmin_reg<4 waves> n=%d batch=%d: %.1f us\n", n, nb, ms * 1e3);
+  }
+  {
+    std::vector<double> ev4(nb);
+    CK(hipMemcpy(ev4.data(), dE, nb * 8, hipMemcpyDeviceToHost));
+    double dm = 0;
+    for (int b = 0; b < nb; ++b) dm = fmax(dm, fabs(ev4[b] - evl[b]));
+    printf("  max |eigmin_lds - eigmin_reg<4 waves>| = %.3e\n", dm);
+  }
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipEventRecord(e0));
     eigmin_reg<<<nb, 512>>>(ddin, dE);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
     printf("eigmin_reg n=%d batch=%d: %.1f us\n", n, nb, ms * 1e3);
@@ -93,9 +106,9 @@ int main(int argc, char** argv) {
   for (int dbg : {1, 2, 3}) {
     CK(hipEventRecord(e0));
     for (int r = 0; r < 3; ++r) {
-      if (dbg == 1) eigmin_reg<1><<<nb, 512>>>(ddin, dE + nb);
-      if (dbg == 2) eigmin_reg<2><<<nb, 512>>>(ddin, dE + nb);
-      if (dbg == 3) eigmin_reg<3><<<nb, 512>>>(ddin, dE + nb);
+      if (dbg == 1) eigmin_reg<1, 4><<<nb, 256>>>(ddin, dE + nb);
+      if (dbg == 2) eigmin_reg<2, 4><<<nb, 256>>>(ddin, dE + nb);
+      if (dbg == 3) eigmin_reg<3, 4><<<nb, 256>>>(ddin, dE + nb);
     }
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
     printf("eigmin_reg<dbg %d (1 no update, 2 no matvec)>: %.1f us\n", dbg, ms * 1e3 / 3);
