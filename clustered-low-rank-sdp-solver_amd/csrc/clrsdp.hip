@@ -476,10 +476,13 @@ struct Solver final : HandleBase {
   GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2, q_qinv, q_qdy;
   // fp64 FACTOR with every dim_S <= 256 (fac2): f_a = {W = L^-1 B | L21^T = L11^-1 S12, W1} and
   // f_b = {W^T W | S22 - L21 L21^T, W1^T W1, B2 - L21 W1} as mixed batches, then (dim_S > 128)
-  // chol_inv(S22), f_c: W2 = L22^-1 B2', f_d: slab += W2^T W2; f_x1/f_x2: X21 (side stream)
+  // chol_inv(S22), f_c: W2 = L22^-1 B2', f_d: slab += W2^T W2 (measured 1% faster than one
+  // W^T W product after W2); f_x1/f_x2: X21 (side stream)
   GemmPlan<T> f_a, f_b, f_c, f_d, f_x1, f_x2;
   bool fac2 = false;
   T* B2p = nullptr;
+  // CLRSDP_EXP: development A/B switch for the variant under measurement (0 = the default)
+  const int exp_knob = std::getenv("CLRSDP_EXP") ? std::atoi(std::getenv("CLRSDP_EXP")) : 0;
   bool pending_x21 = false;  // the solves wait for X21 (side stream, iterate)
   hipEvent_t ev_x2 = nullptr, ev_x21 = nullptr;
   MatPlan<T> e_XY;                        // both step-length eigenproblems in one launch
