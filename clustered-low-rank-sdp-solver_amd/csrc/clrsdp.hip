@@ -163,6 +163,7 @@ template <class T>
 struct GemmPlan : PlanBase {
   bool ta = false, tb = false;
   int tag = 0;  // 1: the Schur-stage V^T X^-1 / V^T Y launch (named separately in profiles)
+  unsigned long long* stamp = nullptr;  // tag 1: earliest workgroup start (SCHUR timing)
   std::vector<GemmDesc<T>> h;
   std::vector<int> ntiles;  // per problem
   std::vector<TileRef> t2d;
@@ -181,8 +182,19 @@ struct GemmPlan : PlanBase {
     g.tile0 = 0;
     g.flags = 0;
     g.alpha = g.beta = 0.0;
+    g.sa = g.sl = nullptr;
     ntiles.push_back((int)(cdiv(M, TILE) * g.tn));
     h.push_back(g);
+  }
+  // sca: op(A) = A with column k scaled by sa[k] * sl[k] (fp64, NT: the weighted-A products)
+  bool sca = false;
+  void add_scaled(const T* A, int lda, const T* B, int ldb, const T* Cin, int ldcin, T* C, int ldc,
+                  int M, int N, int K, const T* sa, const T* sl) {
+    if (M <= 0 || N <= 0) return;
+    sca = true;
+    add(A, lda, B, ldb, Cin, ldcin, C, ldc, M, N, K);
+    h.back().sa = sa;
+    h.back().sl = sl;
   }
   // dyn: a mixed batch (fp64): op(A), op(B), alpha and beta per problem (gemm_f64_dyn)
   bool dyn = false;
@@ -201,7 +213,9 @@ struct GemmPlan : PlanBase {
   bool sym = false;
   void finalize() {
     if (h.empty()) return;
-    gemv = !dyn;  // (a mixed batch always takes the tiled kernel)
+    if (sca && (ta || !tb || !std::is_same<T, double>::value))
+      throw ClrsdpError{CLRSDP_E_ARG, "scaled-A GEMM: fp64 A B^T only"};
+    gemv = !dyn && !sca;  // (a mixed or scaled batch always takes the tiled kernel)
     for (const auto& g : h) gemv = gemv && g.N == 1;
     if (gemv)  // one workgroup per 64 outputs
       for (size_t q = 0; q < h.size(); ++q) ntiles[q] = (int)cdiv(h[q].M, 64);
@@ -240,6 +254,11 @@ struct GemmPlan : PlanBase {
     }
     if constexpr (std::is_same<T, double>::value) {
       const double* ds = reinterpret_cast<const double*>(dscal);
+      if (sca) {
+        gemm_f64_lds<false, true, 0, 32, 8, false, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
+        HIPCHK(hipGetLastError());
+        return;
+      }
       if (dyn) {  // alpha/beta come from the descriptors
         gemm_f64_dyn<><<<grid, 512, 0, s>>>(d, dt, alpha, beta);
         HIPCHK(hipGetLastError());
@@ -253,7 +272,7 @@ struct GemmPlan : PlanBase {
         HIPCHK(hipGetLastError());
         return;
       }
-      if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
+      if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult, stamp);
       else if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
       else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
       else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
@@ -481,6 +500,10 @@ struct Solver final : HandleBase {
   GemmPlan<T> f_a, f_b, f_c, f_d, f_x1, f_x2;
   bool fac2 = false;
   T* B2p = nullptr;
+  // weighted A with the column scaling inside the GEMM's slab staging (fp64, every local block
+  // m = L = 1 with rank-1 samples): no scale_cols launch, no scaled copy of V
+  bool wa_fused = false;
+  GemmPlan<T> p_wA_Ps, p_wA_dXs;
   // CLRSDP_EXP: development A/B switch for the variant under measurement (0 = the default)
   const int exp_knob = std::getenv("CLRSDP_EXP") ? std::atoi(std::getenv("CLRSDP_EXP")) : 0;
   bool pending_x21 = false;  // the solves wait for X21 (side stream, iterate)
@@ -843,6 +866,20 @@ struct Solver final : HandleBase {
     }
     d_pair = descs.own(pd);
     d_scale = descs.own(sd);
+    // trivial tuples + fp64 + the fused Schur layout: x_i / dx_i of column p is entry p of the
+    // cluster's slice, lambda_p entry p of the block's
+    wa_fused = std::is_same<T, double>::value && trivial_tuples && fast_schur;
+    if (wa_fused) {
+      p_wA_Ps.tb = p_wA_dXs.tb = true;
+      for (const LBlk& b : lb) {
+        const int n = b.n, del = b.del, K = b.K;
+        const int64_t xo = c_xoff[b.c];
+        p_wA_Ps.add_scaled(V + b.voff, del, V + b.voff, del, X + b.off, n, P + b.off, n, del, del, K,
+                           x + xo, lam + b.koff);
+        p_wA_dXs.add_scaled(V + b.voff, del, V + b.voff, del, P + b.off, n, dX + b.off, n, del, del, K,
+                            dx + xo, lam + b.koff);
+      }
+    }
     // per cluster plans
     std::vector<SchurClusterDesc> scd;
     std::vector<SchurBlockDesc> sbd;
@@ -955,7 +992,8 @@ struct Solver final : HandleBase {
     for (GemmPlan<T>* g : {&p_txy, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
-                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &f_a, &f_b, &f_c, &f_d, &f_x1, &f_x2})
+                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &f_a, &f_b, &f_c, &f_d, &f_x1, &f_x2,
+                           &p_wA_Ps, &p_wA_dXs})
       g->finalize();
     for (CholInvPlan<T>* c : {&ci_XY, &ci_S, &ci_S22, &ci_Q}) c->finalize();
     e_XY.finalize();
@@ -967,6 +1005,7 @@ struct Solver final : HandleBase {
   void build_fast_schur() {
     if constexpr (std::is_same<T, double>::value) {
       p_txy.tag = 1;
+      p_txy.stamp = stamps;  // the SCHUR stage's start (clock stamps in the stat block)
       p_txy.tb = true;  // TXt = Vt * X^-1^T (X^-1 and Y are symmetric)
       for (const LBlk& b : lb)
         if (b.K > 0) {
@@ -1173,14 +1212,18 @@ struct Solver final : HandleBase {
   // ---- scalar slots + status words: one device block, one pinned host mirror
   char* stat_dev = nullptr;
   char* stat_host = nullptr;
-  size_t stat_bytes = 0, stat_info_off = 0;
+  size_t stat_bytes = 0, stat_info_off = 0, stat_stamp_off = 0;
+  unsigned long long* stamps = nullptr;
   void stat_alloc() {
     stat_info_off = ((SC_COUNT * sizeof(T)) + 63) / 64 * 64;
-    stat_bytes = stat_info_off + (info_count + 1) * sizeof(int);  // + the OR (update guard)
+    // + the OR (update guard), then the SCHUR clock stamps (8-byte aligned)
+    stat_stamp_off = (stat_info_off + (info_count + 1) * sizeof(int) + 7) / 8 * 8;
+    stat_bytes = stat_stamp_off + 2 * sizeof(unsigned long long);
     stat_dev = dmalloc<char>(stat_bytes);
     HIPCHK(hipHostMalloc((void**)&stat_host, stat_bytes, hipHostMallocDefault));
     sc = reinterpret_cast<T*>(stat_dev);
     info = reinterpret_cast<int*>(stat_dev + stat_info_off);
+    stamps = reinterpret_cast<unsigned long long*>(stat_dev + stat_stamp_off);
   }
   // copy scalars + status to the host mirror and wait
   void stat_fetch() {
@@ -1193,6 +1236,7 @@ struct Solver final : HandleBase {
     p.zero_n = zero_info ? info_count - 1 : 0;  // status words of this iteration (not the halt word)
     p.zero_ptr = info;
     p.halt_ptr = zero_info ? info + info_H : nullptr;  // which == 0 at the start of a loop body
+    p.stamps = zero_info ? stamps : nullptr;
     zero_info = false;
     size_t q = 0;
     while (q < pend.size() || q == 0) {  // at most 6 folded reductions per launch
@@ -1237,6 +1281,10 @@ struct Solver final : HandleBase {
     }
   }
   void weighted_A(const T* a, const GemmPlan<T>& plan, T* out, double beta = 0.0) {
+    if (wa_fused) {
+      (a == x ? p_wA_Ps : p_wA_dXs).launch(stream, 1.0, beta);
+      return;
+    }
     if (n_pair) {
       dim3 g(64, n_pair);
       scale_cols<T><<<g, 256, 0, stream>>>(d_scale, V, lam, ksamp, a, TW);
@@ -1296,7 +1344,7 @@ struct Solver final : HandleBase {
     if constexpr (std::is_same<T, double>::value) {
       if (fast_schur) {
         p_txy.launch(stream, 1.0, 0.0);
-        if (n_ptiles) schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d);
+        if (n_ptiles) schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d, stamps + 1);
         if (n_gsum) {
           dim3 g((unsigned)std::min<int64_t>(cdiv((int64_t)max_gD * max_gD, 256), 64), n_gsum);
           schur_gsum<T><<<g, 256, 0, stream>>>(d_gcd, d_sbd, rsums, BX, S);
@@ -1655,7 +1703,7 @@ struct Solver final : HandleBase {
   void enqueue_iteration(const clrsdp_params* prm, int pd_feas) {
     // (the status words are cleared by the first scalar launch of MU_R)
     auto mark = [&](int s) {
-      if (timing) HIPCHK(hipEventRecord(ev[s], stream));
+      if (timing == 1) HIPCHK(hipEventRecord(ev[s], stream));
     };
     // pipelined loop: P, p, d of every body that runs are copied aside (guarded by the halt
     // word), so a skipped body leaves the residuals of the last iteration that ran, which the
@@ -1724,7 +1772,7 @@ struct Solver final : HandleBase {
       HIPCHK(hipStreamWaitEvent(stream, ev_x21, 0));
       pending_x21 = false;
     }
-    if (timing) HIPCHK(hipEventRecord(ev[CLRSDP_NUM_STAGES], stream));
+    if (timing == 1) HIPCHK(hipEventRecord(ev[CLRSDP_NUM_STAGES], stream));
   }
 
   // One hipGraph per pd_feas value replays the whole loop body with a single launch (one
@@ -1740,7 +1788,7 @@ struct Solver final : HandleBase {
   // pipelined host loop hides the enqueue); CLRSDP_GRAPH_RCCL=1 captures the all-gathers into
   // the replayed graph as well
   bool graph_rccl = std::getenv("CLRSDP_GRAPH_RCCL") != nullptr;
-  bool graph_ok() const { return use_graph && !timing && (world == 1 || (comm && graph_rccl)); }
+  bool graph_ok() const { return use_graph && timing != 1 && (world == 1 || (comm && graph_rccl)); }
   // forget every captured loop body (they are re-captured on their next use)
   void drop_graphs() {
     for (hipGraphExec_t& g : gexec)
@@ -1780,7 +1828,11 @@ struct Solver final : HandleBase {
     std::memset(st, 0, sizeof(*st));
     stat_fetch();
     read_stats(st);
-    if (timing)
+    if (timing == 2) {  // the SCHUR stage of the body that just ran (device clock stamps)
+      const unsigned long long* t = reinterpret_cast<const unsigned long long*>(stat_host + stat_stamp_off);
+      st->phase_ms[CLRSDP_STAGE_SCHUR] = t[1] > t[0] ? (double)(t[1] - t[0]) * 1e-5 : 0.0;  // 100 MHz
+    }
+    if (timing == 1)
       for (int s = 0; s < CLRSDP_NUM_STAGES; ++s) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ev[s], ev[s + 1]));
@@ -1790,7 +1842,13 @@ struct Solver final : HandleBase {
     st->status = rc;
     return rc;
   }
-  void set_timing(int on) override { timing = on; }
+  // 0: off (graph replay); 1: every stage between HIP events, no graph; 2: graph replay, and the
+  // SCHUR stage timed inside the replayed body by the 100 MHz clock (earliest start of its first
+  // launch, latest end of its second, atomics in the stat block)
+  void set_timing(int on) override {
+    if (on < 0 || on > 2) throw ClrsdpError{CLRSDP_E_ARG, "timing mode must be 0, 1 or 2"};
+    timing = on;
+  }
 
   // device-side snapshot of the iterate (x, X, y, Y) and the scalar slots, stream-ordered
   T* snap = nullptr;

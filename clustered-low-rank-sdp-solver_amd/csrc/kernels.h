@@ -39,6 +39,8 @@ template <class T> struct GemmDesc {
   int tile0;  // (unused by the TileRef kernels)
   int flags;  // gemm_f64_dyn: bit 0 op(A) = A^T, bit 1 op(B) = B^T, bit 2 alpha/beta below
   double alpha, beta;  // gemm_f64_dyn with flags bit 2 (else the launch's)
+  const T* sa;  // SCA launches: column k of op(A) is scaled by sa[k] * sl[k] (weighted A)
+  const T* sl;
 };
 
 template <class T> struct MatDesc {
@@ -125,7 +127,9 @@ constexpr int gemm_f64_smem() {
                                                                  : 64 * lds_gemm::TP;
 }
 // one 64x64 output tile t of problem d (the body of every fp64 GEMM launch)
-template <bool TA, bool TB, int BK, int NW, bool SYM>
+// SCA (op(A) = A only): A(i, k) * (sa[k] * sl[k]) -- compute_weighted_A's V diag(x lambda)
+// (MPMP.jl:1659) formed while the slab is staged, with scale_cols's operation order
+template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false>
 __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, double* smem,
                                               double alpha, double beta,
                                               const double* __restrict__ dscal, double dmult) {
@@ -147,8 +151,30 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < NI; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  static_assert(!SCA || !TA, "scaled A: op(A) = A only");
+  double wa[SCA ? PER : 1], wl[SCA ? PER : 1];  // the slab's column factors (loaded with it)
+  auto load_w = [&](int k0) {
+    if constexpr (SCA) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        int i, k;
+        SL::template kk<AK>(tid, q, i, k);
+        const int kc = min(k0 + k, K - 1);
+        wa[q] = gload(d.sa + kc);
+        wl[q] = gload(d.sl + kc);
+      }
+    }
+  };
+  auto scale_a = [&]() {
+    if constexpr (SCA) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) ra[q] = ra[q] * (wa[q] * wl[q]);
+    }
+  };
   SL::template load<AK>(ra, d.A, d.lda, m0, M, 0, K, tid);
   SL::template load<BKc>(rb, d.B, d.ldb, n0, N, 0, K, tid);
+  load_w(0);
+  scale_a();
   SL::template store<AK>(ra, As, tid, 0, K);
   SL::template store<BKc>(rb, Bs, tid, 0, K);
   __syncthreads();
@@ -157,6 +183,7 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
     if (more) {
       SL::template load<AK>(ra, d.A, d.lda, m0, M, k0 + BK, K, tid);
       SL::template load<BKc>(rb, d.B, d.ldb, n0, N, k0 + BK, K, tid);
+      load_w(k0 + BK);
     }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
@@ -173,6 +200,7 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
     }
     if (!more) break;
     __syncthreads();
+    scale_a();
     SL::template store<AK>(ra, As, tid, k0 + BK, K);
     SL::template store<BKc>(rb, Bs, tid, k0 + BK, K);
     __syncthreads();
@@ -216,16 +244,20 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
   }
 }
 
-template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false>
+// stamp (TAG 1, the Schur-stage launch): the earliest workgroup start on the 100 MHz clock
+template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false, bool SCA = false>
 __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
                                                         const TileRef* __restrict__ t2d,
                                                         double alpha, double beta,
                                                         const double* __restrict__ dscal = nullptr,
-                                                        double dmult = 0.0) {
+                                                        double dmult = 0.0,
+                                                        unsigned long long* stamp = nullptr) {
+  if constexpr (TAG == 1)
+    if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   __shared__ double smem[gemm_f64_smem<BK, NW>()];
   const TileRef tr = t2d[blockIdx.x];
   const GemmDesc<double> d = descs[tr.p];
-  gemm_f64_tile<TA, TB, BK, NW, SYM>(d, tr.t, smem, alpha, beta, dscal, dmult);
+  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA>(d, tr.t, smem, alpha, beta, dscal, dmult);
 }
 
 // Mixed batch: op(A), op(B) and (flags bit 2) alpha/beta per problem, so independent products of
@@ -994,8 +1026,10 @@ struct PairTileDesc {
 };
 
 template <int BK = 16>
+// stamp: the latest workgroup end of the launch on the 100 MHz clock (SCHUR-stage timing)
 __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __restrict__ descs,
-                                                       const TileRef* __restrict__ t2d) {
+                                                       const TileRef* __restrict__ t2d,
+                                                       unsigned long long* stamp = nullptr) {
   using namespace lds_gemm;
   using SLB = Slab<BK>;
   constexpr int PER = SLB::PER, SL = BK * LSM;
@@ -1105,6 +1139,10 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
         if (p < K && (I < J || p < q)) d.G[q + (size_t)p * d.ldG] = lamS[pl] * lq * Tt[pl * TP + ql];
       }
     }
+  }
+  if (stamp) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 }
 
@@ -1629,6 +1667,7 @@ template <class T> struct ScalarParams {
   int zero_n;   // zero the status words zero_ptr[0..zero_n) (start of an iteration)
   int* zero_ptr;
   int* halt_ptr;  // which == 0: status word "skip this loop body" (device-decided termination)
+  unsigned long long* stamps;  // which == 0: reset the SCHUR-stage clock pair (min start, max end)
   FoldRed<T> red[6];
 };
 
@@ -1697,6 +1736,10 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
   if (which == 0) {  // mu, mu_p
     const bool pdf = pd_feasible(sc, p);
     if (p.halt_ptr) *p.halt_ptr = (p.pd_feas < 0 && sc[SC_HALT] > T(0.5)) ? 1 : 0;
+    if (p.stamps) {
+      p.stamps[0] = ~0ull;
+      p.stamps[1] = 0ull;
+    }
     sc[SC_MU] = sc[SC_DOT_XY] / dim;
     sc[SC_MU_P] = pdf ? T(0.0) : p.beta_inf * sc[SC_MU];
   } else if (which == 1) {  // r, beta, beta_c, mu_c

@@ -220,10 +220,13 @@ class DeviceSolver:
     def synchronize(self):
         self.check(self.L.clrsdp_synchronize(self.h))
 
-    def set_timing(self, on: bool):
-        """Per-stage HIP-event timing on/off (off + one rank: iterate replays a hipGraph)."""
-        self.check(self.L.clrsdp_set_timing(self.h, 1 if on else 0))
-        self.timing = bool(on)
+    def set_timing(self, on):
+        """Per-stage HIP-event timing: False/0 off, True/1 every stage (no graph), 2 only the
+        SCHUR stage, from events inside the replayed loop-body graph (off or 2 + one rank:
+        iterate replays a hipGraph)."""
+        mode = 2 if on == 2 else (1 if on else 0)
+        self.check(self.L.clrsdp_set_timing(self.h, mode))
+        self.timing = mode == 1
 
     def save_state(self):
         """Device-side snapshot of x, X, y, Y and the scalar slots (clrsdp_save_state)."""

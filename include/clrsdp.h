@@ -247,9 +247,10 @@ int32_t clrsdp_set_stream(clrsdp_handle* h, void* stream);
 void* clrsdp_get_stream(const clrsdp_handle* h);
 int32_t clrsdp_synchronize(clrsdp_handle* h);
 
-/* Turn the per-stage HIP-event timing (clrsdp_iter_stats.phase_ms) on or off.  With timing
- * off and world_size 1 (or a native RCCL communicator), clrsdp_iterate replays a captured
- * hipGraph of the loop body. */
+/* Per-stage HIP-event timing (clrsdp_iter_stats.phase_ms): 0 = off, 1 = every stage (the loop
+ * body is enqueued stage by stage, no graph), 2 = only phase_ms[CLRSDP_STAGE_SCHUR], from events
+ * captured inside the replayed loop-body graph.  With timing 0 or 2 and world_size 1 (or a
+ * native RCCL communicator), clrsdp_iterate replays a captured hipGraph of the loop body. */
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on);
 
 int32_t clrsdp_destroy(clrsdp_handle* h);
