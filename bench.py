@@ -232,10 +232,9 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # the SCHUR stage (the roofline kernel pair) is timed inside the timed region: the library's
-    # timing mode 2 stamps the 100 MHz device clock at the first workgroup start of its first
-    # launch and the last workgroup end of its second, inside the replayed graph (synchronous
-    # loop only)
+    # the SCHUR stage (the roofline kernels) is timed inside the timed region: the library's
+    # timing mode 2 stamps the 100 MHz device clock at the first workgroup start and the last
+    # workgroup end of each of its launches inside the replayed graph (synchronous loop only)
     schur_live = [0.0, 0]
     if not pipelined and not os.environ.get("CLRSDP_BENCH_NO_LIVE"):
         dev.set_timing(2)
@@ -286,9 +285,9 @@ def main():
     schur_src = "instrumented pass (per-stage events, no graph)"
     if schur_live[1]:
         sch_s = schur_live[0] / 1e3 / schur_live[1]
-        schur_src = ("device clock (s_memrealtime) from the first workgroup start of the SCHUR "
-                     "stage to the last workgroup end, inside the replayed graph, averaged over "
-                     "the timed region")
+        schur_src = ("device clock (s_memrealtime): the sum over the SCHUR launches (V^T X^-1, "
+                     "V^T Y, pairs) of first workgroup start to last workgroup end, inside the "
+                     "replayed graph, averaged over the timed region")
     traffic, traffic_src = schur_pmc_traffic(args.config, args.precision, world)
     achieved = fl / sch_s / 1e12   # in flops of the word type (multi-word flops when w > 1)
     peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]

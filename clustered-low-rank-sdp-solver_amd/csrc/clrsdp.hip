@@ -273,6 +273,7 @@ struct GemmPlan : PlanBase {
         return;
       }
       if (tag == 1 && !ta && tb) gemm_f64_lds<false, true, 1><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult, stamp);
+      else if (tag == 3 && !ta && tb) gemm_f64_lds<false, true, 3><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult, stamp);
       else if (!ta && !tb) gemm_f64_lds<false, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
       else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
       else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
@@ -515,7 +516,9 @@ struct Solver final : HandleBase {
   // fused Schur path (fp64, every local block m = 1): TXt/TYt = V^T X^-1 / V^T Y, then the
   // paired Hadamard tiles; clusters with L > 1 or ranks != 1 are summed from G (BX arena)
   bool fast_schur = false;
-  GemmPlan<T> p_txy;
+  GemmPlan<T> p_txy, p_ty;  // V^T X^-1 (SCHUR) and V^T Y (ahead on the side stream in a loop body)
+  bool ty_ahead = false;     // p_ty already enqueued on the side stream (joined by ev_ty)
+  hipEvent_t ev_ty = nullptr;
   PairTileDesc* d_ptd = nullptr;
   TileRef* d_pt2d = nullptr;
   int n_ptiles = 0;
@@ -639,7 +642,7 @@ struct Solver final : HandleBase {
     // graph-boundary and join idle time against the lost overlap)
     if (std::getenv("CLRSDP_ONE_STREAM")) aux = own_stream;
     else HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21})
+    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21, &ev_ty})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
     build_plans();
@@ -665,7 +668,7 @@ struct Solver final : HandleBase {
     for (char* r : ring_host)
       if (r) (void)hipHostFree(r);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ring_ev[0], ring_ev[1]})
+    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ev_ty, ring_ev[0], ring_ev[1]})
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
       if (g) (void)hipGraphExecDestroy(g);
@@ -989,7 +992,7 @@ struct Solver final : HandleBase {
       d_tb = descs.own(tbk);
     }
     if (fast_schur) build_fast_schur();
-    for (GemmPlan<T>* g : {&p_txy, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
+    for (GemmPlan<T>* g : {&p_txy, &p_ty, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
                            &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &f_a, &f_b, &f_c, &f_d, &f_x1, &f_x2,
@@ -1007,10 +1010,13 @@ struct Solver final : HandleBase {
       p_txy.tag = 1;
       p_txy.stamp = stamps;  // the SCHUR stage's start (clock stamps in the stat block)
       p_txy.tb = true;  // TXt = Vt * X^-1^T (X^-1 and Y are symmetric)
+      p_ty.tag = 3;
+      p_ty.stamp = stamps + 2;
+      p_ty.tb = true;
       for (const LBlk& b : lb)
         if (b.K > 0) {
           p_txy.add(Vt + b.voff, b.K, Xinv + b.off, b.n, nullptr, 0, TX + b.toff, b.K, b.K, b.del, b.del);
-          p_txy.add(Vt + b.voff, b.K, Y + b.off, b.n, nullptr, 0, TY + b.toff, b.K, b.K, b.del, b.del);
+          p_ty.add(Vt + b.voff, b.K, Y + b.off, b.n, nullptr, 0, TY + b.toff, b.K, b.K, b.del, b.del);
         }
       std::vector<PairTileDesc> ptd;
       std::vector<int> pnt;
@@ -1218,7 +1224,7 @@ struct Solver final : HandleBase {
     stat_info_off = ((SC_COUNT * sizeof(T)) + 63) / 64 * 64;
     // + the OR (update guard), then the SCHUR clock stamps (8-byte aligned)
     stat_stamp_off = (stat_info_off + (info_count + 1) * sizeof(int) + 7) / 8 * 8;
-    stat_bytes = stat_stamp_off + 2 * sizeof(unsigned long long);
+    stat_bytes = stat_stamp_off + 6 * sizeof(unsigned long long);
     stat_dev = dmalloc<char>(stat_bytes);
     HIPCHK(hipHostMalloc((void**)&stat_host, stat_bytes, hipHostMallocDefault));
     sc = reinterpret_cast<T*>(stat_dev);
@@ -1344,7 +1350,13 @@ struct Solver final : HandleBase {
     if constexpr (std::is_same<T, double>::value) {
       if (fast_schur) {
         p_txy.launch(stream, 1.0, 0.0);
-        if (n_ptiles) schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d, stamps + 1);
+        if (ty_ahead) {  // V^T Y came from the side stream
+          HIPCHK(hipStreamWaitEvent(stream, ev_ty, 0));
+          ty_ahead = false;
+        } else {
+          p_ty.launch(stream, 1.0, 0.0);
+        }
+        if (n_ptiles) schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d, stamps + 4);
         if (n_gsum) {
           dim3 g((unsigned)std::min<int64_t>(cdiv((int64_t)max_gD * max_gD, 256), 64), n_gsum);
           schur_gsum<T><<<g, 256, 0, stream>>>(d_gcd, d_sbd, rsums, BX, S);
@@ -1726,7 +1738,16 @@ struct Solver final : HandleBase {
     };
     mark(CLRSDP_STAGE_MU_R);
     stage(CLRSDP_STAGE_MU_R, prm, pd_feas);
-    side(ev_m, [&] { residuals_P(); });
+    side(ev_m, [&] {
+      // V^T Y of the Schur stage only needs the state: it runs beside chol_inv(X, Y), which leaves
+      // half the CUs idle, and SCHUR waits for it (ev_ty) before the pairs launch
+      if (fast_schur && !p_ty.h.empty() && exp_knob != 4) {
+        p_ty.launch(stream, 1.0, 0.0);
+        HIPCHK(hipEventRecord(ev_ty, stream));
+        ty_ahead = true;
+      }
+      residuals_P();
+    });
     mark(CLRSDP_STAGE_XINV);
     stage(CLRSDP_STAGE_XINV, prm, pd_feas);
     mark(CLRSDP_STAGE_SCHUR);
@@ -1830,7 +1851,12 @@ struct Solver final : HandleBase {
     read_stats(st);
     if (timing == 2) {  // the SCHUR stage of the body that just ran (device clock stamps)
       const unsigned long long* t = reinterpret_cast<const unsigned long long*>(stat_host + stat_stamp_off);
-      st->phase_ms[CLRSDP_STAGE_SCHUR] = t[1] > t[0] ? (double)(t[1] - t[0]) * 1e-5 : 0.0;  // 100 MHz
+      // the durations of its three launches (V^T X^-1, V^T Y -- ahead on the side stream in a
+      // loop body -- and the pairs), first workgroup start to last workgroup end each
+      double ticks = 0.0;
+      for (int q = 0; q < 3; ++q)
+        if (t[2 * q + 1] > t[2 * q]) ticks += (double)(t[2 * q + 1] - t[2 * q]);
+      st->phase_ms[CLRSDP_STAGE_SCHUR] = ticks * 1e-5;  // 100 MHz
     }
     if (timing == 1)
       for (int s = 0; s < CLRSDP_NUM_STAGES; ++s) {
@@ -1843,8 +1869,8 @@ struct Solver final : HandleBase {
     return rc;
   }
   // 0: off (graph replay); 1: every stage between HIP events, no graph; 2: graph replay, and the
-  // SCHUR stage timed inside the replayed body by the 100 MHz clock (earliest start of its first
-  // launch, latest end of its second, atomics in the stat block)
+  // SCHUR stage timed inside the replayed body by the 100 MHz clock: the sum over its launches of
+  // first workgroup start to last workgroup end (atomics in the stat block)
   void set_timing(int on) override {
     if (on < 0 || on > 2) throw ClrsdpError{CLRSDP_E_ARG, "timing mode must be 0, 1 or 2"};
     timing = on;

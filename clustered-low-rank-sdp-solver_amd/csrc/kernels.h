@@ -244,7 +244,8 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
   }
 }
 
-// stamp (TAG 1, the Schur-stage launch): the earliest workgroup start on the 100 MHz clock
+// stamp (TAG 1 and 3, the Schur-stage V^T X^-1 and V^T Y launches): stamp[0] = the earliest
+// workgroup start and stamp[1] = the latest workgroup end on the 100 MHz clock
 template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false, bool SCA = false>
 __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* __restrict__ descs,
                                                         const TileRef* __restrict__ t2d,
@@ -252,12 +253,17 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* 
                                                         const double* __restrict__ dscal = nullptr,
                                                         double dmult = 0.0,
                                                         unsigned long long* stamp = nullptr) {
-  if constexpr (TAG == 1)
+  if constexpr (TAG == 1 || TAG == 3)
     if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   __shared__ double smem[gemm_f64_smem<BK, NW>()];
   const TileRef tr = t2d[blockIdx.x];
   const GemmDesc<double> d = descs[tr.p];
   gemm_f64_tile<TA, TB, BK, NW, SYM, SCA>(d, tr.t, smem, alpha, beta, dscal, dmult);
+  if constexpr (TAG == 1 || TAG == 3)
+    if (stamp) {
+      __syncthreads();
+      if (threadIdx.x == 0) atomicMax(stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 }
 
 // Mixed batch: op(A), op(B) and (flags bit 2) alpha/beta per problem, so independent products of
@@ -1026,10 +1032,12 @@ struct PairTileDesc {
 };
 
 template <int BK = 16>
-// stamp: the latest workgroup end of the launch on the 100 MHz clock (SCHUR-stage timing)
+// stamp[0] / stamp[1]: the earliest workgroup start / latest end of the launch on the 100 MHz
+// clock (SCHUR-stage timing)
 __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __restrict__ descs,
                                                        const TileRef* __restrict__ t2d,
                                                        unsigned long long* stamp = nullptr) {
+  if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   using namespace lds_gemm;
   using SLB = Slab<BK>;
   constexpr int PER = SLB::PER, SL = BK * LSM;
@@ -1142,7 +1150,7 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
   }
   if (stamp) {
     __syncthreads();
-    if (threadIdx.x == 0) atomicMax(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (threadIdx.x == 0) atomicMax(stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 }
 
@@ -1737,8 +1745,8 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     const bool pdf = pd_feasible(sc, p);
     if (p.halt_ptr) *p.halt_ptr = (p.pd_feas < 0 && sc[SC_HALT] > T(0.5)) ? 1 : 0;
     if (p.stamps) {
-      p.stamps[0] = ~0ull;
-      p.stamps[1] = 0ull;
+      p.stamps[0] = p.stamps[2] = p.stamps[4] = ~0ull;
+      p.stamps[1] = p.stamps[3] = p.stamps[5] = 0ull;
     }
     sc[SC_MU] = sc[SC_DOT_XY] / dim;
     sc[SC_MU_P] = pdf ? T(0.0) : p.beta_inf * sc[SC_MU];
