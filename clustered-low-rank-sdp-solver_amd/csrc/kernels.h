@@ -1055,6 +1055,7 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1, lr = lane & 15, lk = lane >> 4;
   const int K = d.K, D = d.del;
+  const bool diag_skip = I == J && wm > wn;  // wave-uniform
   double ra[PER], rx[PER], ry[PER];
   d4 ax[2][2], ay[2][2];
   // lambda of the tile's rows and columns (read before the K loop, used in the epilogue)
@@ -1079,8 +1080,11 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
       SLB::template load<false>(ry, d.TYt, K, q0, K, k0 + BK, D, tid);
     }
 #endif
+    // a diagonal tile (I == J) stores only p <= q: the wave of rows 32..63 x columns 0..31 lies
+    // strictly below the diagonal and leaves its SIMD to the other workgroups on the CU
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
+      if (diag_skip) break;
       const int kr = (kk + lk) * LSM;
       const double a0 = As[kr + wm * 32 + lr], a1 = As[kr + wm * 32 + 16 + lr];
       const double x0 = Xs[kr + wn * 32 + lr], x1 = Xs[kr + wn * 32 + 16 + lr];

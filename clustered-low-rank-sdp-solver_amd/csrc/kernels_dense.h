@@ -331,6 +331,12 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
     blk[1] = 7 - w;
   }
   const int c = lane >> 4, t16 = lane & 15;
+  // the wave that holds the block of row n-1 (live to the last column) writes v, the diagonal
+  // and the off-diagonal of every step; a wave with no row in (k+1, n) skips the reflector and
+  // the update of step k (its rows are never read again, or are padding)
+  bool writer = false;
+#pragma unroll
+  for (int h = 0; h < RPL; ++h) writer = writer || blk[h] == ((n - 1) >> 4);
   int i[RPL];
 #pragma unroll
   for (int h = 0; h < RPL; ++h) i[h] = blk[h] * 16 + t16;
@@ -453,7 +459,7 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
       beta = 2.0 * rc;
       e2r = alpha * alpha;
     }
-    if (tid == 0) {
+    if (writer && lane == 0) {
       dg[r] = xr;
       e2[r] = e2r;
     }
@@ -461,7 +467,7 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
     cy = j0 + 1 <= r ? 0.0 : (j0 + 1 == r + 1 ? v0 : xj1);
 #pragma unroll
     for (int h = 0; h < RPL; ++h) vi[h] = i[h] > r ? (i[h] == r + 1 ? v0 : xi[h]) : 0.0;
-    if (w == 0) *reinterpret_cast<double2*>(&vb[r & 1][j0]) = make_double2(cx, cy);
+    if (writer) *reinterpret_cast<double2*>(&vb[r & 1][j0]) = make_double2(cx, cy);
   };
   publish_row(0, rowb[0]);
   if (n >= 2) publish_row(1, rowb[1]);
@@ -480,7 +486,7 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
     const int lo = (k + 1) >> 3;  // slots s < lo hold columns <= k only
     bool live[RPL];               // wave-uniform: some row of row set h is active
 #pragma unroll
-    for (int h = 0; h < RPL; ++h) live[h] = blk[h] * 16 + 15 > k;
+    for (int h = 0; h < RPL; ++h) live[h] = blk[h] * 16 + 15 > k && blk[h] * 16 < n;
     // ---- p = A' v (registers) and this wave's part of v^T p; two FMA chains per row set
     double pp[RPL];
     double t = 0.0;
@@ -518,6 +524,10 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
     ER_STAMP(2)
     __syncthreads();
     ER_STAMP(3)
+    bool need = false;  // wave-uniform: some row of this wave lies beyond k+1
+#pragma unroll
+    for (int h = 0; h < RPL; ++h) need = need || (blk[h] * 16 + 15 > k + 1 && blk[h] * 16 < n);
+    if (!need) continue;  // (the barrier of the next step is at its top, after the matvec)
     // ---- every LDS read of the step at once
     const int r = k + 1;
     const double* old = rowb[r & 1];
@@ -569,7 +579,8 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
       constexpr int g = decltype(G)::value;
       static_for<0, RPL>([&](auto H) {
         constexpr int h = decltype(H)::value;
-        if (live[h] && !(DBG & 1) && 4 * g + 3 >= lo) upd_group(G, H, pxu, pyu, gi[h], mhi[h]);
+        if (blk[h] * 16 + 15 > k + 1 && blk[h] * 16 < n && !(DBG & 1) && 4 * g + 3 >= lo)
+          upd_group(G, H, pxu, pyu, gi[h], mhi[h]);
       });
     });
     ER_STAMP(5)
