@@ -71,7 +71,7 @@ def schur_pmc_traffic(config, precision, world):
     import glob
     if config != "c3" or precision != 1 or world != 1:
         return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_schur_pmc.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_schur_pmc.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -283,7 +283,7 @@ def main():
         by /= world
     sch_s = schur_ms / 1e3 / n_inst
     schur_src = "instrumented pass (per-stage events, no graph)"
-    if schur_live[1]:
+    if schur_live[1] and schur_live[0] > 0.0:   # (the clock stamps exist on the fused fp64 path)
         sch_s = schur_live[0] / 1e3 / schur_live[1]
         schur_src = ("device clock (s_memrealtime): the sum over the SCHUR launches (V^T X^-1, "
                      "V^T Y, pairs) of first workgroup start to last workgroup end, inside the "
