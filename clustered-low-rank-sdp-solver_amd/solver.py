@@ -222,7 +222,7 @@ class DeviceSolver:
 
     def set_timing(self, on):
         """Per-stage HIP-event timing: False/0 off, True/1 every stage (no graph), 2 only the
-        SCHUR stage, from events inside the replayed loop-body graph (off or 2 + one rank:
+        SCHUR stage, from device-clock stamps inside the replayed loop-body graph (off or 2 + one rank:
         iterate replays a hipGraph)."""
         mode = 2 if on == 2 else (1 if on else 0)
         self.check(self.L.clrsdp_set_timing(self.h, mode))

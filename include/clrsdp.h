@@ -248,8 +248,10 @@ void* clrsdp_get_stream(const clrsdp_handle* h);
 int32_t clrsdp_synchronize(clrsdp_handle* h);
 
 /* Per-stage HIP-event timing (clrsdp_iter_stats.phase_ms): 0 = off, 1 = every stage (the loop
- * body is enqueued stage by stage, no graph), 2 = only phase_ms[CLRSDP_STAGE_SCHUR], from events
- * captured inside the replayed loop-body graph.  With timing 0 or 2 and world_size 1 (or a
+ * body is enqueued stage by stage, no graph), 2 = only phase_ms[CLRSDP_STAGE_SCHUR]: the sum of
+ * the three Schur launches' first-workgroup-start..last-workgroup-end on the 100 MHz device clock,
+ * stamped by the kernels inside the replayed loop-body graph (fp64 fast path; 0 elsewhere).
+ * With timing 0 or 2 and world_size 1 (or a
  * native RCCL communicator), clrsdp_iterate replays a captured hipGraph of the loop body. */
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on);
 

@@ -222,6 +222,32 @@ def test_iterate_equals_stagewise(pk):
         assert np.array_equal(a[1][j][0], c[1][j][0])
 
 
+def test_live_schur_timing_keeps_iterates_bitwise(pk):
+    """Timing mode 2 (device-clock stamps inside the replayed graph, clrsdp_set_timing) reports a
+    positive Schur time and changes nothing else: iterates equal the untimed run bitwise."""
+    from clrsdp_amd import _lib as L
+    cons, b = pk.synth(seed=4, J=8, delta=32, rank=1, n_y=16)
+    bi = pk.get_block_info(cons)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    st0 = pk.initial_point(bi, 10.0, 10.0)
+    outs, schur = [], []
+    for timing in (0, 2):
+        dev = pk.DeviceSolver(cons, b, bi)
+        dev.set_timing(timing)
+        dev.set_state(*st0)
+        for _ in range(3):
+            st = dev.iterate(P, False)
+            schur.append(st.phase_ms[L.STAGE_SCHUR])
+        outs.append(dev.get_state())
+        dev.close()
+    assert all(t > 0 for t in schur[3:]) and all(t < 1e3 for t in schur[3:])
+    a, c = outs
+    assert np.array_equal(a[0], c[0]) and np.array_equal(a[2], c[2])
+    for j in range(bi.J):
+        assert np.array_equal(a[1][j][0], c[1][j][0])
+        assert np.array_equal(a[3][j], c[3][j])
+
+
 def test_not_positive_definite_reports_error(pk):
     from clrsdp_amd import _lib as L
     cons, b = pk.synth(seed=9, J=2, delta=4, rank=1, n_y=3)
