@@ -94,6 +94,16 @@ int main(int argc, char** argv) {
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
     printf("eigmin_reg n=%d batch=%d: %.1f us\n", n, nb, ms * 1e3);
   }
+  {  // workgroup placement: the same launch with 100 KB of unused dynamic LDS (one per CU)
+    const int pad = 100 * 1024;
+    CK(hipFuncSetAttribute((const void*)eigmin_reg<0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, pad + 16384));
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipEventRecord(e0));
+      eigmin_reg<0, 8><<<nb, 512, pad>>>(ddin, dE);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("eigmin_reg n=%d batch=%d, one workgroup per CU (LDS pad): %.1f us\n", n, nb, ms * 1e3);
+    }
+  }
   CK(hipMemcpy(evr.data(), dE, nb * 8, hipMemcpyDeviceToHost));
 #ifdef CLRSDP_EIGREG_STAMPS
   {
