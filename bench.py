@@ -141,6 +141,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("CLRSDP_BENCH_ONE_GPU"):
+        # rehearsal of the multi-rank bench on a one-GPU box: every rank on device 0 (RCCL then
+        # refuses the communicator and the exchange falls back to host-staged gloo, loudly)
+        local_rank = 0
     import _clrsdp_pkg
     pk = _clrsdp_pkg.load()
     from clrsdp_amd import _lib
