@@ -128,7 +128,10 @@ template <class T> struct RegCfg { static constexpr int TR = 4, TC = 8, GR = 32,
 template <> struct RegCfg<dd> { static constexpr int TR = 2, TC = 4, GR = 32, GC = 16; };
 template <> struct RegCfg<qd> { static constexpr int TR = 1, TC = 2, GR = 32, GC = 16; };
 template <class T> constexpr int reg_nmax() { return std::is_same<T, double>::value ? 128 : RegCfg<T>::TR * RegCfg<T>::GR; }
-template <class T> size_t eig_lds_bytes(int n) { return sizeof(T) * ((size_t)n * n + 10 * (size_t)n + 40); }
+// eigmin_lds: A (n^2), v, NC = 8 (n <= 64) or 4 partial vectors, dg, e2, w, scalars
+template <class T> size_t eig_lds_bytes(int n) {
+  return sizeof(T) * ((size_t)n * n + (n <= 64 ? 14 : 10) * (size_t)n + 40);
+}
 constexpr size_t LDS_MAX = 160 * 1024;
 
 // workgroup order for a batched launch: tile-major, problem fastest (see TileRef)

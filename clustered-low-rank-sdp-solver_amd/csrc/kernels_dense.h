@@ -687,6 +687,98 @@ __device__ unsigned long long g_eig_stamps[8];
 #else
 #define EIG_STAMP(slot)
 #endif
+// Wave sum of a (multi-word) value by DPP and permlane swaps, limb by limb, with the word
+// type's own addition at every step (commutative, so partner lanes agree): against the
+// ds_bpermute butterfly of wave_sum, whose six dependent LDS-unit round trips per limb set the
+// reflector's critical path in eigmin_lds.
+template <int CTRL, class T>
+__device__ inline T dpp_mw(const T& v) {
+  T o;
+  const double* a = reinterpret_cast<const double*>(&v);
+  double* b = reinterpret_cast<double*>(&o);
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(T) / 8); ++q) b[q] = dpp_d<CTRL>(a[q]);
+  return o;
+}
+__device__ inline double swap32_d(double x) {  // value of lane ^ 32
+  const auto rl = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(x), false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(x), false, false);
+  const bool low = __lane_id() < 32;
+  return low ? __hiloint2double(rh[1], rl[1]) : __hiloint2double(rh[0], rl[0]);
+}
+template <int SW, class T>
+__device__ inline T swap_mw(const T& v) {
+  T o;
+  const double* a = reinterpret_cast<const double*>(&v);
+  double* b = reinterpret_cast<double*>(&o);
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(T) / 8); ++q) b[q] = SW == 16 ? swap16_d(a[q]) : swap32_d(a[q]);
+  return o;
+}
+template <class T>
+__device__ inline T wave_sum_mw(T v) {
+  v = v + dpp_mw<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = v + dpp_mw<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = v + dpp_mw<0x141>(v);  // row_half_mirror
+  v = v + dpp_mw<0x140>(v);  // row_mirror
+  v = v + swap_mw<16>(v);
+  v = v + swap_mw<32>(v);
+  return v;
+}
+
+// exact power-of-two scaling of every limb
+__device__ inline double scale2(double v, int e) { return ldexp(v, e); }
+__device__ inline mw::dd scale2(const mw::dd& v, int e) { return mw::dd(ldexp(v.hi, e), ldexp(v.lo, e)); }
+__device__ inline mw::qd scale2(const mw::qd& v, int e) {
+  return mw::qd(ldexp(v.x[0], e), ldexp(v.x[1], e), ldexp(v.x[2], e), ldexp(v.x[3], e));
+}
+// Multi-word "count >= 1" of the Sturm sequence (some eigenvalue of the tridiagonal below sigma),
+// division-free as sturm_any_below: with p_0 = 1 the count is >= 1 iff some leading principal
+// minor p_i = (d_i - sigma) p_{i-1} - e2_{i-1} p_{i-2} is negative (a zero minor is followed by a
+// nonzero one of the sign opposite to its predecessor's, as the pivot form's q = 0 -> +tiny
+// convention counts it; a zero last minor is not counted there either).  (p_{i-1}, p_i) is
+// rescaled by the power of two of the larger every 4 rows (exact), so no minor overflows.  Per
+// row two multi-word products and two differences, against a multi-word division in the pivot
+// form (sturm_count), whose fp64 division sequences made the multi-word rounds of the
+// multisection 56 % of eigmin_lds<dd>.
+template <class T>
+__device__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict__ e2, int n,
+                                   const T& sigma) {
+  T pm = T(0.0), pc = T(1.0);
+  bool neg = false;
+  // groups of 4 rows: the group's coefficients are read and d_i - sigma formed ahead of the
+  // chain (LDS latency and the differences off the dependent path), then one rescale
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    T dv[4], fv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      dv[u] = dg[i + u] - sigma;
+      fv[u] = i + u > 0 ? e2[i + u - 1] : T(0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const T pn = dv[u] * pc - fv[u] * pm;
+      neg = neg || (pn < T(0.0));
+      pm = pc;
+      pc = pn;
+    }
+    const double mx = fmax(fabs(Num<T>::hi(pc)), fabs(Num<T>::hi(pm)));
+    if (mx > 0.0 && mx < INFINITY) {
+      const int ex = __builtin_amdgcn_frexp_exp(mx);
+      pc = scale2(pc, -ex);
+      pm = scale2(pm, -ex);
+    }
+  }
+  for (; i < n; ++i) {
+    const T pn = (dg[i] - sigma) * pc - (i > 0 ? e2[i - 1] : T(0.0)) * pm;
+    neg = neg || (pn < T(0.0));
+    pm = pc;
+    pc = pn;
+  }
+  return neg;
+}
+
 template <class T, bool NEWTON = true>
 __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__ descs,
                                                   T* __restrict__ out) {
@@ -694,15 +786,23 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
   constexpr int NT = 512, NW = 8;
+  // the multi-word count >= 1 tests (CLRSDP_EIG_PIVOT_COUNT: the pivot form, for A/B timing)
+#ifdef CLRSDP_EIG_PIVOT_COUNT
+#define ANY_BELOW(sg) (sturm_count(dg, e2, n, (sg)) >= 1)
+#else
+#define ANY_BELOW(sg) sturm_any_below_mw(dg, e2, n, (sg))
+#endif
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const MatDesc<T> d = descs[blockIdx.x];
   const int n = d.n, tid = threadIdx.x;
+  // rows per pass and column classes of the matrix-vector product and the rank-2 update: every
+  // wave holds rows when n <= 64 (64 rows x 8 classes), else 128 rows x 4 classes
+  const int RW = n <= 64 ? 64 : 128, NC = NT / RW;
   T* A = reinterpret_cast<T*>(smem_raw);  // n x n
   T* v = A + (size_t)n * n;               // n
-  T* p = v + n;                            // 4 * n partials, then p
-  T* dg = p + 4 * n;                       // n
+  T* p = v + n;                            // NC * n partials (eig_lds_bytes)
+  T* dg = p + NC * n;                      // n
   T* e2 = dg + n;                          // n
-  T* red = e2 + 3 * n + 12;                // NW + 4 (after w, scalars and partials)
   // coalesced load, then symmetrise in LDS: A = (A + A^T)/2
   for (int j = tid >> 6; j < n; j += NT / 64)
     for (int i = tid & 63; i < n; i += 64) A[i + (size_t)j * n] = d.A[i + (size_t)j * d.lda];
@@ -728,7 +828,7 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
         v[i] = xi;
         s += xi * xi;
       }
-      s = wave_sum(s);
+      s = wave_sum_mw(s);
       const T x0 = A[(k + 1) + (size_t)k * n];
       const T tail = s - x0 * x0;
       if (tid == 0) {
@@ -750,51 +850,53 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     EIG_STAMP(0)
     const T beta = scal[0];
     if (beta == T(0.0)) continue;  // uniform: nothing to update
-    // ---- (B) partial rows of A'v (4 column classes) and v^T A' v
-    const int ri = tid & 127, cq = tid >> 7;
+    // ---- (B) partial rows of A'v (NC column classes) and v^T A' v
+    const int ri = tid & (RW - 1), cq = tid / RW;
     T vav = T(0.0);
-    for (int ii = ri; ii < m; ii += 128) {
+    for (int ii = ri; ii < m; ii += RW) {
       T a0 = T(0.0), a1 = T(0.0), a2 = T(0.0), a3 = T(0.0);
       int j = cq;
-      for (; j + 12 < m; j += 16) {
+      for (; j + 3 * NC < m; j += 4 * NC) {
         a0 += Ak[ii + (size_t)j * n] * v[j];
-        a1 += Ak[ii + (size_t)(j + 4) * n] * v[j + 4];
-        a2 += Ak[ii + (size_t)(j + 8) * n] * v[j + 8];
-        a3 += Ak[ii + (size_t)(j + 12) * n] * v[j + 12];
+        a1 += Ak[ii + (size_t)(j + NC) * n] * v[j + NC];
+        a2 += Ak[ii + (size_t)(j + 2 * NC) * n] * v[j + 2 * NC];
+        a3 += Ak[ii + (size_t)(j + 3 * NC) * n] * v[j + 3 * NC];
       }
-      for (; j < m; j += 4) a0 += Ak[ii + (size_t)j * n] * v[j];
+      for (; j < m; j += NC) a0 += Ak[ii + (size_t)j * n] * v[j];
       const T part = (a0 + a1) + (a2 + a3);
       p[cq * n + ii] = part;
       vav += part * v[ii];
     }
     EIG_STAMP(1)
-    vav = wave_sum(vav);
+    vav = wave_sum_mw(vav);
     if ((tid & 63) == 0) redw[tid >> 6] = vav;
     __syncthreads();
     EIG_STAMP(2)
     // ---- (C) w = beta A'v - K v,  K = beta^2 v^T A' v / 2
     {
-      T tot = redw[0];
-#pragma unroll
-      for (int q = 1; q < 8; ++q) tot += redw[q];
+      // pairwise (three dependent multi-word additions instead of seven)
+      const T tot = ((redw[0] + redw[1]) + (redw[2] + redw[3])) + ((redw[4] + redw[5]) + (redw[6] + redw[7]));
       const T Kc = beta * beta * tot * T(0.5);
-      for (int i = tid; i < m; i += NT)
-        Wv[i] = ((p[i] + p[n + i]) + (p[2 * n + i] + p[3 * n + i])) * beta - Kc * v[i];
+      for (int i = tid; i < m; i += NT) {
+        T ps = (p[i] + p[n + i]) + (p[2 * n + i] + p[3 * n + i]);
+        if (NC == 8) ps = ps + ((p[4 * n + i] + p[5 * n + i]) + (p[6 * n + i] + p[7 * n + i]));
+        Wv[i] = ps * beta - Kc * v[i];
+      }
     }
     __syncthreads();
     EIG_STAMP(3)
     // ---- (D) A' -= v w^T + w v^T
-    for (int ii = ri; ii < m; ii += 128) {
+    for (int ii = ri; ii < m; ii += RW) {
       const T vi = v[ii], wi = Wv[ii];
       int j = cq;
-      for (; j + 12 < m; j += 16) {
+      for (; j + 3 * NC < m; j += 4 * NC) {
 #pragma unroll
-        for (int u = 0; u < 16; u += 4) {
-          T* a = Ak + ii + (size_t)(j + u) * n;
-          *a = *a - (vi * Wv[j + u] + wi * v[j + u]);
+        for (int u = 0; u < 4; ++u) {
+          T* a = Ak + ii + (size_t)(j + u * NC) * n;
+          *a = *a - (vi * Wv[j + u * NC] + wi * v[j + u * NC]);
         }
       }
-      for (; j < m; j += 4) {
+      for (; j < m; j += NC) {
         T* a = Ak + ii + (size_t)j * n;
         *a = *a - (vi * Wv[j] + wi * v[j]);
       }
@@ -814,7 +916,6 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     }
   }
   __syncthreads();
-  (void)red;
   if (n == 1) {
     if (tid == 0) out[blockIdx.x] = dg[0];
     return;
@@ -888,6 +989,7 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     }
   }
   __syncthreads();
+  EIG_STAMP(7)
   if constexpr (NEWTON && Num<T>::BITS > 120) {
     // (2') quad-double: Newton on det(T - sigma I) from the fp64 centre (at dd the 11 parallel
     // multisection rounds are as fast as the sequential Newton chain, so dd keeps them).  With the pivots of
@@ -928,8 +1030,8 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     const T s = nres[0];
     const T dl = T(ldexp(mag, 12 - Num<T>::BITS) + 1e-300);
     int c = 0;
-    if (tid == 0) c = masks[2] && sturm_count(dg, e2, n, s - dl) == 0;
-    if (tid == 64) c = sturm_count(dg, e2, n, s + dl) >= 1;
+    if (tid == 0) c = masks[2] && !ANY_BELOW(s - dl);
+    if (tid == 64) c = ANY_BELOW(s + dl);
     __syncthreads();
     if (tid == 0 || tid == 64) masks[tid >> 6] = (unsigned long long)c;
     __syncthreads();
@@ -945,8 +1047,8 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
   // check the start bracket at full width: count(lo) == 0 and count(hi) >= 1
   {
     int c = 0;
-    if (tid == 0) c = sturm_count(dg, e2, n, lo) == 0;
-    if (tid == 64) c = sturm_count(dg, e2, n, hi) >= 1;
+    if (tid == 0) c = !ANY_BELOW(lo);
+    if (tid == 64) c = ANY_BELOW(hi);
     if (tid == 0 || tid == 64) masks[tid >> 6] = (unsigned long long)c;
     __syncthreads();
     const bool ok = masks[0] && masks[1];
@@ -955,23 +1057,36 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
       lo = T(bnd[0]);
       hi = T(bnd[1]);
     }
-    // rounds to shrink the bracket to ~2^-BITS of the spectrum's magnitude
-    const int rounds = ok ? (Num<T>::BITS - 25) / 9 + 2 : Num<T>::BITS / 9 + 3;
+    // rounds to shrink the bracket to ~2^-BITS of the spectrum's magnitude.  The multi-word
+    // counts are VALU-issue bound, so they run 256-way on waves 0-3 (one wave per SIMD: 8 bits
+    // per round) rather than 512-way on two waves per SIMD (9 bits per round at twice the issue)
+#ifdef CLRSDP_EIG_MW512
+    constexpr int MS = 512, MB = 9;
+#else
+    constexpr int MS = 256, MB = 8;
+#endif
+    constexpr double MD = MS + 1.0;
+    const int rounds = ok ? (Num<T>::BITS - 25) / MB + 2 : Num<T>::BITS / MB + 3;
     for (int it = 0; it < rounds; ++it) {
       const T width = hi - lo;
-      const T sigma = lo + width * T((double)(tid + 1) / 513.0);
-      const int f = first_hit(sturm_count(dg, e2, n, sigma) >= 1);
+      bool hit = false;
+      if (tid < MS) {  // wave-uniform
+        const T sigma = lo + width * T((double)(tid + 1) / MD);
+        hit = ANY_BELOW(sigma);
+      }
+      const int f = first_hit(hit);
       if (f < 0) {
-        lo = lo + width * T(512.0 / 513.0);
+        lo = lo + width * T((double)MS / MD);
       } else {
-        hi = lo + width * T((double)(f + 1) / 513.0);
-        if (f > 0) lo = lo + width * T((double)f / 513.0);
+        hi = lo + width * T((double)(f + 1) / MD);
+        if (f > 0) lo = lo + width * T((double)f / MD);
       }
     }
   }
   if (tid == 0) out[blockIdx.x] = (lo + hi) * T(0.5);
   EIG_STAMP(6)
 }
+#undef ANY_BELOW
 
 }  // namespace clrsdp
 

@@ -28,7 +28,7 @@ void run(const char* name, int n, int nb, const std::vector<double>& h) {
   MatDesc<T>* ddin;
   CK(hipMalloc(&ddin, nb * sizeof(MatDesc<T>)));
   CK(hipMemcpy(ddin, din.data(), nb * sizeof(MatDesc<T>), hipMemcpyHostToDevice));
-  const size_t lds = sizeof(T) * ((size_t)n * n + 10 * n + 40);
+  const size_t lds = sizeof(T) * ((size_t)n * n + (n <= 64 ? 14 : 10) * n + 40);  // eig_lds_bytes
   CK(hipFuncSetAttribute((const void*)eigmin_lds<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   CK(hipFuncSetAttribute((const void*)eigmin_lds<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipEvent_t e0, e1;
@@ -57,7 +57,10 @@ void run(const char* name, int n, int nb, const std::vector<double>& h) {
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_eig_stamps), sizeof(st)));
     double hh = 0;
     for (int q = 0; q < 6; ++q) hh += st[q];
-    printf("  cycles per matrix: householder %.0f  eigenvalue phase %.0f\n", hh / (3.0 * nb), st[6] / (3.0 * nb));
+    printf("  cycles per matrix: householder %.0f  eigenvalue phase %.0f (fp64 bracket %.0f, multi-word %.0f)\n",
+           hh / (3.0 * nb), (st[6] + st[7]) / (3.0 * nb), st[7] / (3.0 * nb), st[6] / (3.0 * nb));
+    printf("  householder: reflector %.0f, A'v %.0f, reduce+barrier %.0f, w %.0f, update %.0f\n",
+           st[0] / (3.0 * nb), st[1] / (3.0 * nb), st[2] / (3.0 * nb), st[3] / (3.0 * nb), st[4] / (3.0 * nb));
 #endif
   }
   std::vector<T> ev(2 * nb);
