@@ -699,15 +699,21 @@ __global__ __launch_bounds__(256) void potrf_batched(const MatDesc<T>* __restric
     const int k1 = k0 + nb, pm = n - k1;
     if (pm <= 0) break;
     // panel L21 = A21 L11^-T, one row per thread
+    // (row[] in registers: the loops run to the compile-time NB with a uniform guard, so every
+    // index is static -- a runtime bound put the array in scratch memory)
     for (int i = tid; i < pm; i += blockDim.x) {
       T row[NB];
-      for (int q = 0; q < nb; ++q) {
-        T x = A[(k1 + i) + (size_t)(k0 + q) * lda];
-        for (int p = 0; p < q; ++p) x = x - row[p] * D[q + p * NB];
-        x = x / D[q + q * NB];
-        row[q] = x;
-        P[q * pm + i] = x;
-        A[(k1 + i) + (size_t)(k0 + q) * lda] = x;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        if (q < nb) {
+          T x = A[(k1 + i) + (size_t)(k0 + q) * lda];
+#pragma unroll
+          for (int p = 0; p < q; ++p) x = x - row[p] * D[q + p * NB];
+          x = x / D[q + q * NB];
+          row[q] = x;
+          P[q * pm + i] = x;
+          A[(k1 + i) + (size_t)(k0 + q) * lda] = x;
+        }
       }
     }
     __syncthreads();
@@ -762,23 +768,36 @@ __global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restric
     }
     __syncthreads();
     if (tid < nc) {
+      // x[] in registers: compile-time loops to NB, uniform guards on the block size nb
       T x[NB];
       if (!TRANS) {
-        for (int r = 0; r < nb; ++r) {
-          T v = B[(i0 + r) + (size_t)tid * d.ldb];
-          for (int q = 0; q < r; ++q) v = v - D[r + q * NB] * x[q];
-          x[r] = v / D[r + r * NB];
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+          if (r < nb) {
+            T v = B[(i0 + r) + (size_t)tid * d.ldb];
+#pragma unroll
+            for (int q = 0; q < r; ++q) v = v - D[r + q * NB] * x[q];
+            x[r] = v / D[r + r * NB];
+          }
         }
       } else {
-        for (int r = nb - 1; r >= 0; --r) {
-          T v = B[(i0 + r) + (size_t)tid * d.ldb];
-          for (int q = r + 1; q < nb; ++q) v = v - D[q + r * NB] * x[q];
-          x[r] = v / D[r + r * NB];
+#pragma unroll
+        for (int r = NB - 1; r >= 0; --r) {
+          if (r < nb) {
+            T v = B[(i0 + r) + (size_t)tid * d.ldb];
+#pragma unroll
+            for (int q = r + 1; q < NB; ++q)
+              if (q < nb) v = v - D[q + r * NB] * x[q];
+            x[r] = v / D[r + r * NB];
+          }
         }
       }
-      for (int r = 0; r < nb; ++r) {
-        B[(i0 + r) + (size_t)tid * d.ldb] = x[r];
-        Xs[r * NC + tid] = x[r];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        if (r < nb) {
+          B[(i0 + r) + (size_t)tid * d.ldb] = x[r];
+          Xs[r * NC + tid] = x[r];
+        }
       }
     }
     __syncthreads();
