@@ -658,6 +658,7 @@ __global__ __launch_bounds__(256) void potrf_batched(const MatDesc<T>* __restric
   T* D = reinterpret_cast<T*>(smem_raw);  // NB x NB diagonal block (column-major)
   T* P = D + NB * NB;                      // panel: P[q * pm + i]
   __shared__ int fail;
+  __shared__ T rdg[NB];  // reciprocals of the block's pivots (one division each, by thread 0)
   const MatDesc<T> d = descs[blockIdx.x];
   T* A = d.A;
   const int n = d.n, lda = d.lda, tid = threadIdx.x;
@@ -676,13 +677,15 @@ __global__ __launch_bounds__(256) void potrf_batched(const MatDesc<T>* __restric
         if (!(djj > T(0.0))) {
           fail = k0 + j + 1;
         } else {
-          D[j + j * NB] = Num<T>::sqrt_(djj);
+          const T sj = Num<T>::sqrt_(djj);
+          D[j + j * NB] = sj;
+          rdg[j] = T(1.0) / sj;
         }
       }
       __syncthreads();
       if (fail) break;
-      const T piv = D[j + j * NB];
-      for (int i = j + 1 + tid; i < nb; i += blockDim.x) D[i + j * NB] = D[i + j * NB] / piv;
+      const T rpiv = rdg[j];
+      for (int i = j + 1 + tid; i < nb; i += blockDim.x) D[i + j * NB] = D[i + j * NB] * rpiv;
       __syncthreads();
       const int r = nb - j - 1;
       for (int e = tid; e < r * r; e += blockDim.x) {
@@ -709,7 +712,7 @@ __global__ __launch_bounds__(256) void potrf_batched(const MatDesc<T>* __restric
           T x = A[(k1 + i) + (size_t)(k0 + q) * lda];
 #pragma unroll
           for (int p = 0; p < q; ++p) x = x - row[p] * D[q + p * NB];
-          x = x / D[q + q * NB];
+          x = x * rdg[q];
           row[q] = x;
           P[q * pm + i] = x;
           A[(k1 + i) + (size_t)(k0 + q) * lda] = x;
@@ -735,7 +738,9 @@ __global__ __launch_bounds__(256) void potrf_batched(const MatDesc<T>* __restric
 // Triangular solves with L from potrf (lower, non-unit), in place on B:
 //   TRANS = false:  B <- L^-1 B     (forward substitution)
 //   TRANS = true :  B <- L^-T B     (backward substitution)
-// One workgroup per (matrix, NC-column tile of B); NB-row blocks; L panel staged in LDS.
+// One workgroup per (matrix, NC-column tile of B); NB-row blocks; L panel staged in LDS.  The
+// diagonal enters as reciprocals (one division per row, not per right-hand side: a multi-word
+// division is an order of magnitude dearer than a product).
 // ------------------------------------------------------------------------------------------
 template <class T, bool TRANS, int NB, int NC>
 __global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restrict__ descs,
@@ -744,6 +749,7 @@ __global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restric
   T* D = reinterpret_cast<T*>(smem_raw);  // NB x NB diagonal block of L (column-major)
   T* Xs = D + NB * NB;                     // NB x NC solved rows
   T* P = Xs + NB * NC;                     // panel NB x n
+  __shared__ T rdg[NB];                    // reciprocals of the block's diagonal
   const TrsmDesc<T> d = descs[t2d[blockIdx.x]];
   const int c0 = (blockIdx.x - d.tile0) * NC;
   const int nc = min(NC, d.nrhs - c0);
@@ -758,6 +764,7 @@ __global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restric
       const int i = e % nb, j = e / nb;
       D[i + j * NB] = L[(i0 + i) + (size_t)(i0 + j) * d.ldl];
     }
+    if (tid < nb) rdg[tid] = T(1.0) / L[(i0 + tid) + (size_t)(i0 + tid) * d.ldl];
     // panel of the rows still to be updated
     const int pr0 = TRANS ? 0 : i0 + nb;
     const int pm = TRANS ? i0 : n - i0 - nb;
@@ -777,7 +784,7 @@ __global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restric
             T v = B[(i0 + r) + (size_t)tid * d.ldb];
 #pragma unroll
             for (int q = 0; q < r; ++q) v = v - D[r + q * NB] * x[q];
-            x[r] = v / D[r + r * NB];
+            x[r] = v * rdg[r];
           }
         }
       } else {
@@ -788,7 +795,7 @@ __global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restric
 #pragma unroll
             for (int q = r + 1; q < NB; ++q)
               if (q < nb) v = v - D[q + r * NB] * x[q];
-            x[r] = v / D[r + r * NB];
+            x[r] = v * rdg[r];
           }
         }
       }

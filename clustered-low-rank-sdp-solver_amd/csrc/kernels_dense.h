@@ -45,7 +45,8 @@ __device__ T block_sum_w(T v, T* red) {
 // chol_inv_reg: for each matrix b of the batch, read A_b (n x n, SPD, lower triangle used),
 // write Linv_b = L^-1 (lower triangular, exact zeros above the diagonal) and optionally L_b.
 // Thread t owns rows [tr*TR, tr*TR+TR) x cols [tc*TC, tc*TC+TC) with tr = t % GR, tc = t / GR.
-// Right-looking: step j broadcasts column j of L and row j of L^-1 through LDS (2 barriers).
+// Right-looking: step j broadcasts column j of L and row j of L^-1 through LDS (2 barriers); the
+// column is scaled by the reciprocal of the pivot, formed once by the pivot's owner.
 // In-place safe (out == A): every thread reads its own tile before anything is written.
 // ------------------------------------------------------------------------------------------
 template <class T, int TR, int TC, int GR, int GC>
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
   static_assert(TR * GR == TC * GC, "square tile grid");
   __shared__ T col[NMAX];
   __shared__ T row[NMAX];
-  __shared__ T sd;
+  __shared__ T sd, rsd;  // pivot and its reciprocal (one division per column, by its owner)
   __shared__ int fail;
   const MatDesc<T> d = in[blockIdx.x];
   const int n = d.n;
@@ -77,11 +78,12 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
     const T d0 = d.A[0];
     if (!(d0 > T(0.0))) fail = 1;
     sd = Num<T>::sqrt_(d0);
+    rsd = T(1.0) / sd;
   }
   __syncthreads();
   for (int j = 0; j < n; ++j) {
     if (fail) break;
-    const T s = sd;
+    const T s = sd, rs = rsd;
     // phase B: column j of L -> col[], row j of L^-1 -> row[]  (static register indices only)
     const int jc = j % TC, jr = j % TR;
     if (tc == j / TC) {
@@ -92,7 +94,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
           for (int i = 0; i < TR; ++i) {
             const int gi = r0 + i;
             if (gi >= j && gi < n) {
-              const T l = (gi == j) ? s : a[i][c] / s;
+              const T l = (gi == j) ? s : a[i][c] * rs;
               a[i][c] = l;
               col[gi] = l;
             }
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
         if (i == jr) {
 #pragma unroll
           for (int c = 0; c < TC; ++c) {
-            x[i][c] = x[i][c] / s;
+            x[i][c] = x[i][c] * rs;
             row[c0 + c] = x[i][c];
           }
         }
@@ -150,6 +152,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
           if (i == jn % TR && c == jn % TC) dn = a[i][c];
       if (!(dn > T(0.0))) fail = jn + 1;
       sd = Num<T>::sqrt_(dn);
+      rsd = T(1.0) / sd;
     }
     __syncthreads();
   }
