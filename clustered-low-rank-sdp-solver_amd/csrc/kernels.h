@@ -400,6 +400,16 @@ __device__ __forceinline__ T shfl_xor_t(T v, int o) {
   }
 }
 
+template <class T>
+__device__ __forceinline__ T shfl_t(T v, int src) {  // the value of lane src (of the wave)
+  T t;
+  double* td = reinterpret_cast<double*>(&t);
+  const double* vd = reinterpret_cast<const double*>(&v);
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(T) / 8); ++q) td[q] = __shfl(vd[q], src);
+  return t;
+}
+
 // sum over the 16 lanes of a row (lanes 16r..16r+15)
 template <class T>
 __device__ __forceinline__ T row16_sum_t(T v) {
@@ -774,37 +784,38 @@ __global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restric
       P[q * pm + i] = TRANS ? L[(i0 + q) + (size_t)i * d.ldl] : L[(pr0 + i) + (size_t)(i0 + q) * d.ldl];
     }
     __syncthreads();
-    if (tid < nc) {
-      // x[] in registers: compile-time loops to NB, uniform guards on the block size nb
-      T x[NB];
+    // the diagonal block, column-oriented: lane r of a 16-lane group holds row r of one
+    // right-hand side; per q the owner of row q finalises x_q (times 1/l_qq), the group reads it
+    // by a shuffle and rows beyond it subtract l_rq x_q -- 16 short steps instead of one
+    // thread's serial chain of nb(nb+1)/2 multi-word products per column (forward: the same
+    // operation order per row as the row-oriented form)
+    for (int cb = 0; cb < nc; cb += 16) {  // uniform: 16 right-hand sides per pass
+      const int r = tid & 15, c = cb + (tid >> 4), base = tid & 48;
+      const bool act = r < nb && c < nc;
+      T v = act ? B[(i0 + r) + (size_t)c * d.ldb] : T(0.0);
+      T xr = T(0.0);
       if (!TRANS) {
 #pragma unroll
-        for (int r = 0; r < NB; ++r) {
-          if (r < nb) {
-            T v = B[(i0 + r) + (size_t)tid * d.ldb];
-#pragma unroll
-            for (int q = 0; q < r; ++q) v = v - D[r + q * NB] * x[q];
-            x[r] = v * rdg[r];
+        for (int q = 0; q < NB; ++q) {
+          if (q < nb) {
+            if (r == q) xr = v * rdg[q];
+            const T xq = shfl_t(xr, base + q);
+            if (r > q) v = v - D[r + q * NB] * xq;
           }
         }
       } else {
 #pragma unroll
-        for (int r = NB - 1; r >= 0; --r) {
-          if (r < nb) {
-            T v = B[(i0 + r) + (size_t)tid * d.ldb];
-#pragma unroll
-            for (int q = r + 1; q < NB; ++q)
-              if (q < nb) v = v - D[q + r * NB] * x[q];
-            x[r] = v * rdg[r];
+        for (int q = NB - 1; q >= 0; --q) {
+          if (q < nb) {
+            if (r == q) xr = v * rdg[q];
+            const T xq = shfl_t(xr, base + q);
+            if (r < q) v = v - D[q + r * NB] * xq;
           }
         }
       }
-#pragma unroll
-      for (int r = 0; r < NB; ++r) {
-        if (r < nb) {
-          B[(i0 + r) + (size_t)tid * d.ldb] = x[r];
-          Xs[r * NC + tid] = x[r];
-        }
+      if (act) {
+        B[(i0 + r) + (size_t)c * d.ldb] = xr;
+        Xs[r * NC + c] = xr;
       }
     }
     __syncthreads();
