@@ -661,8 +661,8 @@ __device__ T block_max(T v, T* red) {
 // memory (L2-resident at the sizes of this solver).  info[b] = 0 on success, else the 1-based
 // column at which a non-positive pivot appeared (the reference's status 0 of spd_inv!/cho!).
 // ------------------------------------------------------------------------------------------
-template <class T, int NB>
-__global__ __launch_bounds__(256) void potrf_batched(const MatDesc<T>* __restrict__ descs,
+template <class T, int NB, int NT = 256>
+__global__ __launch_bounds__(NT) void potrf_batched(const MatDesc<T>* __restrict__ descs,
                                                      int* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   T* D = reinterpret_cast<T*>(smem_raw);  // NB x NB diagonal block (column-major)
