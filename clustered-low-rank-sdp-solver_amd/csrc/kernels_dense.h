@@ -923,8 +923,8 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     if (tid == 0) out[blockIdx.x] = dg[0];
     return;
   }
-  // ---- multisection with all 512 threads (9 bits per round), in two phases:
-  //  (1) fp64 on the leading limbs of the tridiagonal: Gershgorin bracket, 7 rounds;
+  // ---- multisection, 256-way on waves 0-3 (8 bits per round), in two phases:
+  //  (1) fp64 on the leading limbs of the tridiagonal: Gershgorin bracket, 8 rounds;
   //  (2) multi-word, started from the fp64 eigenvalue +- delta, where delta bounds the effect of
   //      the rounding to fp64 (Weyl: |dlambda| <= ||dT|| <= ~3 eps64 ||T||) and of the fp64 Sturm
   //      counts (exact for a matrix perturbed by a few eps64 relative), with a wide margin.  The
@@ -971,16 +971,18 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     return f;
   };
   {
+    // 8 rounds of 256 division-free counts on waves 0-3 (64 bits of the Gershgorin span)
     double lo = bnd[0], hi = bnd[1];
-    for (int it = 0; it < 7; ++it) {
+    for (int it = 0; it < 8; ++it) {
       const double width = hi - lo;
-      const double sigma = lo + width * ((double)(tid + 1) / 513.0);
-      const int f = first_hit(sturm_count_fast(dgh, e2h, n, sigma) >= 1);
+      bool hit = false;
+      if (tid < 256) hit = sturm_any_below_mw(dgh, e2h, n, lo + width * ((double)(tid + 1) / 257.0));
+      const int f = first_hit(hit);
       if (f < 0) {
-        lo = lo + width * (512.0 / 513.0);
+        lo = lo + width * (256.0 / 257.0);
       } else {
-        hi = lo + width * ((double)(f + 1) / 513.0);
-        if (f > 0) lo = lo + width * ((double)f / 513.0);
+        hi = lo + width * ((double)(f + 1) / 257.0);
+        if (f > 0) lo = lo + width * ((double)f / 257.0);
       }
     }
     if (tid == 0) {
