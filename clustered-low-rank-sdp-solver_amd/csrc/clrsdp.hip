@@ -298,9 +298,10 @@ struct TrsmPlan : PlanBase {
   std::vector<int> t2d;
   TrsmDesc<T>* d = nullptr;
   int* dt = nullptr;
-  int nmax = 0;
+  int nmax = 0, rmax = 0;
   void add(const T* L, int ldl, T* B, int ldb, int n, int nrhs) {
     if (n <= 0 || nrhs <= 0) return;
+    rmax = std::max(rmax, nrhs);
     TrsmDesc<T> t;
     t.L = L; t.B = B; t.n = n; t.nrhs = nrhs; t.ldl = ldl; t.ldb = ldb;
     t.tile0 = (int)t2d.size();
@@ -318,8 +319,15 @@ struct TrsmPlan : PlanBase {
     if (h.empty()) return;
     const size_t lds = sizeof(T) * ((size_t)NB * NB + (size_t)NB * NC + (size_t)NB * nmax);
     const unsigned grid = (unsigned)t2d.size();
-    if (trans) trsm_batched<T, true, NB, NC><<<grid, 256, lds, s>>>(d, dt);
-    else trsm_batched<T, false, NB, NC><<<grid, 256, lds, s>>>(d, dt);
+    // multi-word solves with many right-hand sides (W = L^-1 B): 1024 threads, four waves per
+    // SIMD for the VALU-bound panel update; vector solves keep 256
+    if (!std::is_same<T, double>::value && rmax >= 32) {
+      if (trans) trsm_batched<T, true, NB, NC, 1024><<<grid, 1024, lds, s>>>(d, dt);
+      else trsm_batched<T, false, NB, NC, 1024><<<grid, 1024, lds, s>>>(d, dt);
+    } else {
+      if (trans) trsm_batched<T, true, NB, NC><<<grid, 256, lds, s>>>(d, dt);
+      else trsm_batched<T, false, NB, NC><<<grid, 256, lds, s>>>(d, dt);
+    }
     HIPCHK(hipGetLastError());
   }
 };

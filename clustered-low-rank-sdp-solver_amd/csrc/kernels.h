@@ -752,8 +752,8 @@ __global__ __launch_bounds__(NT) void potrf_batched(const MatDesc<T>* __restrict
 // diagonal enters as reciprocals (one division per row, not per right-hand side: a multi-word
 // division is an order of magnitude dearer than a product).
 // ------------------------------------------------------------------------------------------
-template <class T, bool TRANS, int NB, int NC>
-__global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restrict__ descs,
+template <class T, bool TRANS, int NB, int NC, int NT = 256>
+__global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict__ descs,
                                                     const int* __restrict__ t2d) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   T* D = reinterpret_cast<T*>(smem_raw);  // NB x NB diagonal block of L (column-major)
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(256) void trsm_batched(const TrsmDesc<T>* __restric
     // by a shuffle and rows beyond it subtract l_rq x_q -- 16 short steps instead of one
     // thread's serial chain of nb(nb+1)/2 multi-word products per column (forward: the same
     // operation order per row as the row-oriented form)
-    for (int cb = 0; cb < nc; cb += 16) {  // uniform: 16 right-hand sides per pass
+    for (int cb = 0; cb < nc; cb += NT / 16) {  // uniform: NT/16 right-hand sides per pass
       const int r = tid & 15, c = cb + (tid >> 4), base = tid & 48;
       const bool act = r < nb && c < nc;
       T v = act ? B[(i0 + r) + (size_t)c * d.ldb] : T(0.0);
