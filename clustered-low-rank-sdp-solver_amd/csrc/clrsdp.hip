@@ -173,7 +173,7 @@ struct GemmPlan : PlanBase {
   GemmDesc<T>* d = nullptr;
   TileRef* dt = nullptr;
   // gemm_f64_lds (fp64) and gemm_valu (multi-word) output tiles
-  static constexpr int TILE = std::is_same<T, double>::value ? 64 : 32;
+  static constexpr int TILE = std::is_same<T, double>::value ? 64 : 16;
 
   void add(const T* A, int lda, const T* B, int ldb, const T* Cin, int ldcin, T* C, int ldc, int M,
            int N, int K) {

@@ -285,13 +285,17 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_dyn(const GemmDesc<double>* 
 }
 
 // ------------------------------------------------------------------------------------------
-// GEMM on the VALU for multi-word T: 32x32 tile, 256 threads, 2x2 outputs per thread.
+// GEMM on the VALU for multi-word T: 16x16 tile, 256 threads, one output per thread.
 // ------------------------------------------------------------------------------------------
 template <class T, bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__ descs,
                                                  const TileRef* __restrict__ t2d, double alpha,
                                                  double beta) {
-  constexpr int BM = 32, BN = 32, BK = 8;
+  // 16x16 output tile, one output per thread with two accumulation chains (even / odd k): the
+  // multi-word FMA is a long dependent sequence, so the tile is small enough for a batch of
+  // 64x64 blocks to put two workgroups on every CU (the 32x32 tile with 2x2 outputs per thread
+  // left half the CUs idle at one wave per SIMD)
+  constexpr int BM = 16, BN = 16, BK = 16;
   __shared__ T As[BK][BM + 1];
   __shared__ T Bs[BK][BN + 1];
   const TileRef tr = t2d[blockIdx.x];
@@ -299,20 +303,18 @@ __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__
   const int t = tr.t;
   const int m0 = (t / d.tn) * BM, n0 = (t % d.tn) * BN;
   const int tid = threadIdx.x;
-  const int ti = (tid & 15) * 2, tj = (tid >> 4) * 2;
-  T acc[2][2];
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b) acc[a][b] = T(0.0);
+  const int ti = tid & 15, tj = tid >> 4;
+  T acc0 = T(0.0), acc1 = T(0.0);
   for (int k0 = 0; k0 < d.K; k0 += BK) {
-    {  // A tile 32 x 8 = 256 elements
-      const int i = TA ? (tid >> 3) : (tid & 31), k = TA ? (tid & 7) : (tid >> 5);
+    {  // A tile 16 x 16: i contiguous in memory unless TA
+      const int i = TA ? (tid >> 4) : (tid & 15), k = TA ? (tid & 15) : (tid >> 4);
       const int gi = m0 + i, gk = k0 + k;
       T v = T(0.0);
       if (gi < d.M && gk < d.K) v = TA ? d.A[gk + (size_t)gi * d.lda] : d.A[gi + (size_t)gk * d.lda];
       As[k][i] = v;
     }
-    {  // B tile 8 x 32
-      const int j = TB ? (tid & 31) : (tid >> 3), k = TB ? (tid >> 5) : (tid & 7);
+    {  // B tile 16 x 16: j contiguous in memory iff TB
+      const int j = TB ? (tid & 15) : (tid >> 4), k = TB ? (tid >> 4) : (tid & 15);
       const int gj = n0 + j, gk = k0 + k;
       T v = T(0.0);
       if (gj < d.N && gk < d.K) v = TB ? d.B[gj + (size_t)gk * d.ldb] : d.B[gk + (size_t)gj * d.ldb];
@@ -320,24 +322,18 @@ __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < BK; ++k) {
-      const T a0 = As[k][ti], a1 = As[k][ti + 1], b0 = Bs[k][tj], b1 = Bs[k][tj + 1];
-      acc[0][0] += a0 * b0;
-      acc[0][1] += a0 * b1;
-      acc[1][0] += a1 * b0;
-      acc[1][1] += a1 * b1;
+    for (int k = 0; k < BK; k += 2) {
+      acc0 += As[k][ti] * Bs[k][tj];
+      acc1 += As[k + 1][ti] * Bs[k + 1][tj];
     }
     __syncthreads();
   }
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b) {
-      const int row = m0 + ti + a, col = n0 + tj + b;
-      if (row < d.M && col < d.N) {
-        T v = acc[a][b] * T(alpha);
-        if (beta != 0.0) v += d.Cin[row + (size_t)col * d.ldcin] * T(beta);
-        d.C[row + (size_t)col * d.ldc] = v;
-      }
-    }
+  const int row = m0 + ti, col = n0 + tj;
+  if (row < d.M && col < d.N) {
+    T v = (acc0 + acc1) * T(alpha);
+    if (beta != 0.0) v += d.Cin[row + (size_t)col * d.ldcin] * T(beta);
+    d.C[row + (size_t)col * d.ldc] = v;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
