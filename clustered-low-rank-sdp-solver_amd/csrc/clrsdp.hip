@@ -126,7 +126,7 @@ inline void lds_attr_once(std::atomic<unsigned long long>& seen, const void* fn,
 // register-tile shapes of chol_inv_reg per word type (NMAX = TR * GR)
 template <class T> struct RegCfg { static constexpr int TR = 4, TC = 8, GR = 32, GC = 16; };
 template <> struct RegCfg<dd> { static constexpr int TR = 1, TC = 4, GR = 64, GC = 16; };  // 1024 threads
-template <> struct RegCfg<qd> { static constexpr int TR = 1, TC = 2, GR = 32, GC = 16; };
+template <> struct RegCfg<qd> { static constexpr int TR = 1, TC = 1, GR = 32, GC = 32; };  // 1024 threads
 template <class T> constexpr int reg_nmax() { return std::is_same<T, double>::value ? 128 : RegCfg<T>::TR * RegCfg<T>::GR; }
 // eigmin_lds: A (n^2), v, NC = 8 (n <= 64) or 4 partial vectors, dg, e2, w, scalars
 template <class T> size_t eig_lds_bytes(int n) {
