@@ -657,6 +657,25 @@ __device__ T block_max(T v, T* red) {
 // memory (L2-resident at the sizes of this solver).  info[b] = 0 on success, else the 1-based
 // column at which a non-positive pivot appeared (the reference's status 0 of spd_inv!/cho!).
 // ------------------------------------------------------------------------------------------
+// sqrt(d) and 1/sqrt(d) of a positive pivot.  Double-double: the hardware reciprocal square root
+// refined by two fp64 Newton steps and one double-double Newton step, then s = d r -- no IEEE
+// division or square-root sequence on the factorisations' serial pivot chain.
+template <class T>
+__device__ inline void pivot_sqrt(const T& d, T& s, T& r) {
+  s = Num<T>::sqrt_(d);
+  r = T(1.0) / s;
+}
+template <>
+__device__ inline void pivot_sqrt<mw::dd>(const mw::dd& d, mw::dd& s, mw::dd& r) {
+  double r0 = __builtin_amdgcn_rsq(d.hi);
+  r0 = r0 * fma(-0.5 * d.hi, r0 * r0, 1.5);
+  r0 = r0 * fma(-0.5 * d.hi, r0 * r0, 1.5);
+  const mw::dd rr(r0);
+  const mw::dd e = mw::dd(1.0) - d * (rr * rr);
+  r = rr + (rr * e) * 0.5;
+  s = d * r;
+}
+
 template <class T, int NB, int NT = 256>
 __global__ __launch_bounds__(NT) void potrf_batched(const MatDesc<T>* __restrict__ descs,
                                                      int* __restrict__ info) {
@@ -683,9 +702,10 @@ __global__ __launch_bounds__(NT) void potrf_batched(const MatDesc<T>* __restrict
         if (!(djj > T(0.0))) {
           fail = k0 + j + 1;
         } else {
-          const T sj = Num<T>::sqrt_(djj);
+          T sj, rj;
+          pivot_sqrt(djj, sj, rj);
           D[j + j * NB] = sj;
-          rdg[j] = T(1.0) / sj;
+          rdg[j] = rj;
         }
       }
       __syncthreads();

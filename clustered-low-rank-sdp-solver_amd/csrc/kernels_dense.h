@@ -77,8 +77,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
     fail = 0;
     const T d0 = d.A[0];
     if (!(d0 > T(0.0))) fail = 1;
-    sd = Num<T>::sqrt_(d0);
-    rsd = T(1.0) / sd;
+    pivot_sqrt(d0, sd, rsd);
   }
   __syncthreads();
   for (int j = 0; j < n; ++j) {
@@ -151,8 +150,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
         for (int c = 0; c < TC; ++c)
           if (i == jn % TR && c == jn % TC) dn = a[i][c];
       if (!(dn > T(0.0))) fail = jn + 1;
-      sd = Num<T>::sqrt_(dn);
-      rsd = T(1.0) / sd;
+      pivot_sqrt(dn, sd, rsd);
     }
     __syncthreads();
   }
