@@ -676,6 +676,20 @@ __device__ inline void pivot_sqrt<mw::dd>(const mw::dd& d, mw::dd& s, mw::dd& r)
   s = d * r;
 }
 
+// 1/q: double-double from the hardware reciprocal (two fp64 Newton steps) and one
+// double-double Newton step
+template <class T>
+__device__ inline T recip_fast(const T& q) { return T(1.0) / q; }
+template <>
+__device__ inline mw::dd recip_fast<mw::dd>(const mw::dd& q) {
+  double r0 = __builtin_amdgcn_rcp(q.hi);
+  r0 = fma(fma(-q.hi, r0, 1.0), r0, r0);
+  r0 = fma(fma(-q.hi, r0, 1.0), r0, r0);
+  const mw::dd rr(r0);
+  const mw::dd e = mw::dd(1.0) - q * rr;
+  return rr + rr * e;
+}
+
 template <class T, int NB, int NT = 256>
 __global__ __launch_bounds__(NT) void potrf_batched(const MatDesc<T>* __restrict__ descs,
                                                      int* __restrict__ info) {

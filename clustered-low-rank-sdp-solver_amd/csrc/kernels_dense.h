@@ -838,12 +838,13 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
           e2[k] = x0 * x0;
           scal[0] = T(0.0);  // beta = 0: no reflection
         } else {
-          const T nrm = Num<T>::sqrt_(s);
+          T nrm, rnrm;
+          pivot_sqrt(s, nrm, rnrm);  // (dd: off the IEEE sqrt/division sequences)
           const T alpha = (x0 > T(0.0)) ? -nrm : nrm;
           const T v0 = x0 - alpha;
           e2[k] = alpha * alpha;
           v[0] = v0;
-          scal[0] = T(2.0) / (tail + v0 * v0);
+          scal[0] = recip_fast(tail + v0 * v0) * T(2.0);
         }
       }
     }
