@@ -676,6 +676,15 @@ __device__ inline void pivot_sqrt<mw::dd>(const mw::dd& d, mw::dd& s, mw::dd& r)
   s = d * r;
 }
 
+template <>
+__device__ inline void pivot_sqrt<mw::qd>(const mw::qd& d, mw::qd& s, mw::qd& r) {
+  // sqrt_qd's Newton iteration on 1/sqrt(d) (three steps from the fp64 value), kept: r itself
+  // is the reciprocal, so no quad-double division follows
+  const mw::qd h = d * 0.5;
+  r = mw::qd(1.0 / sqrt(d.x[0]));
+  for (int it = 0; it < 3; ++it) r = r + r * (mw::qd(0.5) - h * (r * r));
+  s = d * r;
+}
 // 1/q: double-double from the hardware reciprocal (two fp64 Newton steps) and one
 // double-double Newton step
 template <class T>
