@@ -45,14 +45,31 @@ struct ClrsdpError {
       throw ClrsdpError{CLRSDP_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)}; \
   } while (0)
 
+// zero-filled device allocation; the fill is complete on return (null stream, synchronised:
+// no caller has to order it against its own non-blocking streams)
 template <class X>
 X* dmalloc(size_t n) {
   if (n == 0) n = 1;
   void* p = nullptr;
   HIPCHK(hipMalloc(&p, n * sizeof(X)));
-  HIPCHK(hipMemset(p, 0, n * sizeof(X)));
+  HIPCHK(hipMemsetAsync(p, 0, n * sizeof(X), nullptr));
+  HIPCHK(hipStreamSynchronize(nullptr));
   return reinterpret_cast<X*>(p);
 }
+
+// the calling thread's current device, set for the scope and restored after (the C ABI's calls
+// are made from threads that may drive other devices)
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) HIPCHK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
 
 // ---------------- RCCL, loaded at run time (the library itself has no link dependency on it,
 // so a single-GPU or CPU-side user never needs librccl).  Only the five entry points the
@@ -220,6 +237,10 @@ struct GemmPlan : PlanBase {
       throw ClrsdpError{CLRSDP_E_ARG, "scaled-A GEMM: fp64 A B^T only"};
     gemv = !dyn && !sca;  // (a mixed or scaled batch always takes the tiled kernel)
     for (const auto& g : h) gemv = gemv && g.N == 1;
+    // op(B) = B^T of a 1 x K row is the gemv vector only for K = 1 (e.g. all blocks 1 x 1)
+    if (gemv && tb)
+      for (const auto& g : h) gemv = gemv && g.K == 1;
+    if (gemv) sym = false;  // a product with one column is 1 x 1 when square: trivially symmetric
     if (gemv)  // one workgroup per 64 outputs
       for (size_t q = 0; q < h.size(); ++q) ntiles[q] = (int)cdiv(h[q].M, 64);
     if (dyn && (gemv || sym || !std::is_same<T, double>::value))
@@ -248,8 +269,7 @@ struct GemmPlan : PlanBase {
     if (dscal && !std::is_same<T, double>::value)
       throw ClrsdpError{CLRSDP_E_ARG, "fused diagonal epilogue is fp64 only"};
     const unsigned grid = (unsigned)t2d.size();
-    if (gemv) {
-      if (tb) throw ClrsdpError{CLRSDP_E_ARG, "gemv with transposed vector"};
+    if (gemv) {  // (tb only with K = 1: B[0] is the vector either way)
       if (ta) gemv_batched<T, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else gemv_batched<T, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       HIPCHK(hipGetLastError());
@@ -315,10 +335,25 @@ struct TrsmPlan : PlanBase {
     d = own(h);
     dt = own(t2d);
   }
+  // mode (the LU fallback's factors): 0 = potrf's L; 1 = unit lower L of getrf; 2 = getrf's U,
+  // read transposed (forward: U^T x = b; trans: U x = b)
+  int mode = 0;
   void launch(hipStream_t s, bool trans) const {
     if (h.empty()) return;
     const size_t lds = sizeof(T) * ((size_t)NB * NB + (size_t)NB * NC + (size_t)NB * nmax);
     const unsigned grid = (unsigned)t2d.size();
+    if (mode == 1 && !trans) {
+      trsm_batched<T, false, NB, NC, 256, true, false><<<grid, 256, lds, s>>>(d, dt);
+      HIPCHK(hipGetLastError());
+      return;
+    }
+    if (mode == 2) {
+      if (trans) trsm_batched<T, true, NB, NC, 256, false, true><<<grid, 256, lds, s>>>(d, dt);
+      else trsm_batched<T, false, NB, NC, 256, false, true><<<grid, 256, lds, s>>>(d, dt);
+      HIPCHK(hipGetLastError());
+      return;
+    }
+    if (mode != 0) throw ClrsdpError{CLRSDP_E_ARG, "unsupported triangular solve mode"};
     // multi-word solves with many right-hand sides (W = L^-1 B): 1024 threads, four waves per
     // SIMD for the VALU-bound panel update; vector solves keep 256
     if (!std::is_same<T, double>::value && rmax >= 32) {
@@ -386,6 +421,52 @@ struct MatPlan : PlanBase {  // potrf / eigmin
 };
 
 
+// pivoted LU in place (the approx_lu! / approx_inv! fallback, getrf_batched)
+template <class T>
+struct LuPlan : PlanBase {
+  static constexpr int NB = 16;
+  std::vector<LuDesc<T>> h;
+  LuDesc<T>* d = nullptr;
+  int nmax = 0;
+  void add(T* A, int* perm, int n, int lda) {
+    h.push_back(LuDesc<T>{A, perm, n, lda});
+    nmax = std::max(nmax, n);
+  }
+  void finalize() {
+    if (!h.empty()) d = own(h);
+  }
+  void launch(hipStream_t s, int* info) const {
+    if (h.empty()) return;
+    const size_t lds = getrf_lds_bytes<T, NB>(nmax);
+    if (lds > LDS_MAX) throw ClrsdpError{CLRSDP_E_ARG, "LU fallback: matrix too large for the on-chip panel"};
+    static std::atomic<unsigned long long> attr{0};
+    lds_attr_once(attr, (const void*)getrf_batched<T, NB, 256>, (int)LDS_MAX);
+    getrf_batched<T, NB, 256><<<(unsigned)h.size(), 256, lds, s>>>(d, info);
+    HIPCHK(hipGetLastError());
+  }
+};
+
+// row gathers out = in[perm, :] (or P I with ident)
+template <class T>
+struct PermPlan : PlanBase {
+  std::vector<PermDesc<T>> h;
+  PermDesc<T>* d = nullptr;
+  long long emax = 0;
+  void add(const T* in, int ldi, T* out, int ldo, const int* perm, int n, int ncol) {
+    h.push_back(PermDesc<T>{in, out, perm, n, ncol, ldi, ldo});
+    emax = std::max(emax, (long long)n * ncol);
+  }
+  void finalize() {
+    if (!h.empty()) d = own(h);
+  }
+  void launch(hipStream_t s, bool ident = false) const {
+    if (h.empty()) return;
+    dim3 g(std::min<unsigned>(cdiv(emax, 256), 64), (unsigned)h.size());
+    perm_rows<T><<<g, 256, 0, s>>>(d, ident ? 1 : 0);
+    HIPCHK(hipGetLastError());
+  }
+};
+
 template <class T>
 struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
   std::vector<MatDesc<T>> hin, hout, hl;
@@ -427,6 +508,7 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
 
 struct HandleBase {
   std::string err;
+  int dev = 0;  // the handle's HIP device (every C-ABI call on the handle runs with it current)
   virtual ~HandleBase() {}
   virtual void upload(const double* V, const double* lam, const double* B, const double* c,
                       const double* b, const double* C) = 0;
@@ -448,6 +530,8 @@ struct HandleBase {
   virtual void set_timing(int on) = 0;
   virtual void save_state() = 0;
   virtual void restore_state() = 0;
+  virtual void set_factorization(int flags) = 0;
+  virtual int get_factorization() const = 0;
 };
 
 template <class T>
@@ -492,6 +576,18 @@ struct Solver final : HandleBase {
   int device = 0;
   bool uploaded = false;
   int info_count = 0, info_S0 = 0, info_Q0 = 0, info_Y0 = 0, info_H = 0;
+  int info_L0 = 0;  // status words of X^-1 by LU (one per block)
+  int info_G = 0;   // world > 1: the failure bits of every rank, OR-ed (STEP's exchange)
+  // ---------------- the LU fallback (approx_lu! / approx_inv!, MPMP.jl:774-786, 1436, 1501):
+  // Cholesky first; when a Cholesky status word fires, the loop body is re-run with pivoted LU
+  // for S_j and Q (or for X^-1), and LU stays on for the rest of the solve, as the reference
+  // switches spd_inv! off.  CLRSDP_FACT_LU_SQ from the start is the reference's own choice.
+  int fact_flags = CLRSDP_FACT_FALLBACK;
+  bool lu_built = false;
+  int* lperm = nullptr;  // row permutations: S_j (at the cluster's x offset), Q, X blocks
+  T* W2m = nullptr;      // U_j^-T B_j  (the transposed B_j^T U_j^-1, MPMP.jl:1457-1460)
+  bool lu_sq() const { return (fact_flags & CLRSDP_FACT_LU_SQ) != 0; }
+  bool lu_x() const { return (fact_flags & CLRSDP_FACT_LU_X) != 0; }
   // pipelined loop (iterate_async / iterate_wait): device-side loop control and results copy
   T gap_thr{}, p_thr{}, d_thr{};
   int need_p = 0, need_d = 0;
@@ -524,6 +620,11 @@ struct Solver final : HandleBase {
   bool pending_x21 = false;  // the solves wait for X21 (side stream, iterate)
   hipEvent_t ev_x2 = nullptr, ev_x21 = nullptr;
   MatPlan<T> e_XY;                        // both step-length eigenproblems in one launch
+  // LU fallback plans (built on the first switch)
+  LuPlan<T> lu_S, lu_Q, lu_X;
+  PermPlan<T> pm_B, pm_rhs, pm_r, pm_I;
+  TrsmPlan<T> tl_W1, tl_W2, tl_t, tl_dx, tl_Q1, tl_Q2, tl_X1, tl_X2;
+  GemmPlan<T> lq_slab, lq_Wt;
   BlkDesc* d_blk = nullptr;      // all local blocks
   BlkDesc* d_blk_m = nullptr;    // local blocks with m > 1
   int n_blk_m = 0;
@@ -565,7 +666,8 @@ struct Solver final : HandleBase {
     world = std::max(1, (int)cfg->world_size);
     timing = cfg->timing;
     device = cfg->device;
-    HIPCHK(hipSetDevice(cfg->device));
+    dev = cfg->device;
+    HIPCHK(hipSetDevice(cfg->device));  // (clrsdp_create restores the caller's device)
     J = desc->J;
     n_y = desc->n_y;
     if (J <= 0 || n_y <= 0) throw ClrsdpError{CLRSDP_E_ARG, "J and n_y must be positive"};
@@ -666,7 +768,8 @@ struct Solver final : HandleBase {
     // device memory is released with the process / hipDeviceReset; free what we own explicitly
     T* bufs[] = {X, Y, Xinv, LX, LY, R, P, dX, dY, Z, tA, tB, Cm, V, lam, TX, TY, TU, TW, BX, BY, AY,
                  tval, S, Wm, Bm, Qslab, Q, Qf, Qinv, cvec, x, dx, dvec, rhs, tvec, tmpv, pslab, y,
-                 bvec, dyv, pvec, uvec, bpart, upart, eigX, tmpsc, tC, Stmp, B2p, own_send, Vt, Pres, pres, dres};
+                 bvec, dyv, pvec, uvec, bpart, upart, eigX, tmpsc, tC, Stmp, B2p, own_send, Vt, Pres, pres, dres,
+                 W2m};
     for (T* p : bufs)
       if (p) (void)hipFree(p);
     if (comm) {
@@ -677,6 +780,7 @@ struct Solver final : HandleBase {
     if (snap) (void)hipFree(snap);
     (void)hipFree(ksamp);
     (void)hipFree(rsums);
+    if (lperm) (void)hipFree(lperm);
     if (stat_dev) (void)hipFree(stat_dev);
     if (stat_host) (void)hipHostFree(stat_host);
     for (char* r : ring_host)
@@ -734,12 +838,15 @@ struct Solver final : HandleBase {
     ksamp = dmalloc<int>(nK);
     rsums = dmalloc<int>(nRS);
     if (fast_schur) Vt = dmalloc<T>(std::max<int64_t>(nV, 1));
-    // info layout: [X: nb][Y: nb][S: nc single + nc2 second blocks][Q: 1]
-    info_count = 2 * nb() + nc() + nc2 + 1 + 1;   // + the halt word (last; not zeroed)
+    // info layout: [X: nb][Y: nb][S: nc single + nc2 second blocks][Q: 1][X by LU: nb]
+    // [gathered failure bits: 1][halt: 1 (last; not zeroed)]
+    info_count = 3 * nb() + nc() + nc2 + 1 + 1 + 1;
     info_H = info_count - 1;
     info_Y0 = nb();
     info_S0 = 2 * nb();
     info_Q0 = 2 * nb() + nc() + nc2;
+    info_L0 = info_Q0 + 1;
+    info_G = info_L0 + nb();
     stat_alloc();
     xcap = n_y * n_y + n_y + 16;
     own_send = dmalloc<T>(xcap);
@@ -1081,6 +1188,70 @@ struct Solver final : HandleBase {
     }
   }
 
+  // The LU fallback's buffers and launch plans (first switch, or set_factorization).
+  //   FACTOR:  S_j[perm_j] = L_j U_j (getrf); W1_j = L_j^-1 B_j[perm_j]; W2_j = U_j^-T B_j;
+  //            slab_j = W2_j^T W1_j; Q = sum_j slab_j; Q[perm] = L_Q U_Q     (MPMP.jl:1429-1505)
+  //   solves:  t_j = L_j^-1 rhs_j[perm_j]; u = sum_j W2_j^T t_j; dy = U_Q^-1 L_Q^-1 (p - u)[perm];
+  //            dx_j = U_j^-1 (t_j + W1_j dy)                                  (MPMP.jl:1743-1776)
+  //   X^-1:    X_b[perm_b] = L_b U_b; X_b^-1 = U_b^-1 L_b^-1 (P_b I)          (approx_inv!, 781)
+  void build_lu_plans() {
+    if (lu_built) return;
+    int64_t np = nx + n_y;
+    for (const LBlk& b : lb) np += b.n;
+    lperm = dmalloc<int>(std::max<int64_t>(np, 1));
+    W2m = dmalloc<T>(std::max<int64_t>(nB, 1));
+    const int ny = (int)n_y;
+    for (int c = 0; c < nc(); ++c) {
+      const int D = (int)Ds[oc[c]];
+      T* Sc = S + c_Soff[c];
+      T* Wc = Wm + c_Boff[c];
+      T* W2c = W2m + c_Boff[c];
+      const T* Bc = Bm + c_Boff[c];
+      int* pc = lperm + c_xoff[c];
+      const int64_t xo = c_xoff[c];
+      lu_S.add(Sc, pc, D, D);
+      pm_B.add(Bc, D, Wc, D, pc, D, ny);                                          // B_j[perm_j]
+      tl_W1.add(Sc, D, Wc, D, D, ny);                                             // L_j^-1 (.)
+      tl_W2.add(Sc, D, W2c, D, D, ny);                                            // U_j^-T B_j
+      lq_slab.add(W2c, D, Wc, D, nullptr, 0, Qslab + (int64_t)c * n_y * n_y, ny, ny, ny, D);
+      pm_rhs.add(rhs + xo, D, tvec + xo, D, pc, D, 1);                            // rhs_j[perm_j]
+      tl_t.add(Sc, D, tvec + xo, D, D, 1);
+      lq_Wt.add(W2c, D, tvec + xo, D, nullptr, 0, pslab + (int64_t)c * n_y, ny, ny, 1, D);
+      tl_dx.add(Sc, D, dx + xo, D, D, 1);                                         // U_j^-1 (.)
+    }
+    int* qp = lperm + nx;
+    lu_Q.add(Qf, qp, ny, ny);
+    pm_r.add(uvec, ny, dyv, ny, qp, ny, 1);
+    tl_Q1.add(Qf, ny, dyv, ny, ny, 1);
+    tl_Q2.add(Qf, ny, dyv, ny, ny, 1);
+    int* xp = qp + n_y;
+    for (const LBlk& b : lb) {
+      lu_X.add(tA + b.off, xp, b.n, b.n);
+      pm_I.add(nullptr, 0, Xinv + b.off, b.n, xp, b.n, b.n);
+      tl_X1.add(tA + b.off, b.n, Xinv + b.off, b.n, b.n, b.n);
+      tl_X2.add(tA + b.off, b.n, Xinv + b.off, b.n, b.n, b.n);
+      xp += b.n;
+    }
+    lq_slab.ta = lq_Wt.ta = true;
+    for (TrsmPlan<T>* t : {&tl_W1, &tl_t, &tl_Q1, &tl_X1}) t->mode = 1;
+    for (TrsmPlan<T>* t : {&tl_W2, &tl_dx, &tl_Q2, &tl_X2}) t->mode = 2;
+    for (LuPlan<T>* l : {&lu_S, &lu_Q, &lu_X}) l->finalize();
+    for (PermPlan<T>* q : {&pm_B, &pm_rhs, &pm_r, &pm_I}) q->finalize();
+    for (TrsmPlan<T>* t : {&tl_W1, &tl_W2, &tl_t, &tl_dx, &tl_Q1, &tl_Q2, &tl_X1, &tl_X2}) t->finalize();
+    lq_slab.finalize();
+    lq_Wt.finalize();
+    lu_built = true;
+  }
+  void set_factorization(int flags) override {
+    if (inflight) throw ClrsdpError{CLRSDP_E_STATE, "set_factorization with loop bodies in flight"};
+    if (flags & ~(CLRSDP_FACT_FALLBACK | CLRSDP_FACT_LU_SQ | CLRSDP_FACT_LU_X))
+      throw ClrsdpError{CLRSDP_E_ARG, "unknown factorization flags"};
+    if (flags & (CLRSDP_FACT_LU_SQ | CLRSDP_FACT_LU_X)) build_lu_plans();
+    if (flags != fact_flags) drop_graphs();
+    fact_flags = flags;
+  }
+  int get_factorization() const override { return fact_flags; }
+
   // ---------------- host <-> device conversion
   void put(T* dst, const double* planes, int64_t nplane, int64_t first, int64_t count) {
     if (count <= 0) return;
@@ -1257,6 +1428,8 @@ struct Solver final : HandleBase {
     p.zero_ptr = info;
     p.halt_ptr = zero_info ? info + info_H : nullptr;  // which == 0 at the start of a loop body
     p.stamps = zero_info ? stamps : nullptr;
+    p.guard = info;
+    p.nguard = info_count;
     zero_info = false;
     size_t q = 0;
     while (q < pend.size() || q == 0) {  // at most 6 folded reductions per launch
@@ -1351,14 +1524,28 @@ struct Solver final : HandleBase {
   void st_xinv() {
     if (reg_blk) {  // L_X^-1 and L_Y^-1 on chip in one launch, X^-1 = L^-T L^-1 on MFMA
       ci_XY.launch(stream, info);
-      q_xinv.launch(stream, 1.0, 0.0);
+      if (lu_x()) xinv_lu();
+      else q_xinv.launch(stream, 1.0, 0.0);
       return;
     }
     blk_lin(LX, X, 1.0, nullptr, 0.0);
     f_X.potrf(stream, info);
+    if (lu_x()) {
+      xinv_lu();
+      return;
+    }
     if (nb()) blk_identity<T><<<nb(), 256, 0, stream>>>(d_blk, tA);
     t_Linv.launch(stream, false);             // tA = L^-1
     p_xinv.launch(stream, 1.0, 0.0);          // X^-1 = L^-T L^-1
+  }
+  // approx_inv! (MPMP.jl:781, 788): X_b^-1 = U_b^-1 L_b^-1 P_b by pivoted LU (the Cholesky factor
+  // above stays: the step length needs it, cho! MPMP.jl:1846)
+  void xinv_lu() {
+    blk_lin(tA, X, 1.0, nullptr, 0.0);
+    lu_X.launch(stream, info + info_L0);
+    pm_I.launch(stream, true);                // Xinv = P I
+    tl_X1.launch(stream, false);              // L^-1 (P I)
+    tl_X2.launch(stream, true);               // U^-1 (L^-1 P I)
   }
   void st_schur() {
     if constexpr (std::is_same<T, double>::value) {
@@ -1394,6 +1581,16 @@ struct Solver final : HandleBase {
   }
   // side_x21: X21 on the side stream (the loop body), joined before the first solve
   void factor_local(bool side_x21 = false) {
+    if (lu_sq()) {                            // approx_lu! (MPMP.jl:1433-1494)
+      lu_S.launch(stream, info + info_S0);
+      pm_B.launch(stream);
+      tl_W1.launch(stream, false);            // W1_j = L_j^-1 B_j[perm_j]
+      vlin(W2m, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
+      tl_W2.launch(stream, false);            // W2_j = U_j^-T B_j
+      lq_slab.launch(stream, 1.0, 0.0);       // slab_j = W2_j^T W1_j
+      sum_q_slabs();
+      return;
+    }
     if (fac2) {                               // fp64: S_j <- L_j^-1 in place, W_j and Q's slabs
       ci_S.launch(stream, info + info_S0);    // S (dim_S <= 128) and S11 blocks
       f_a.launch(stream, 1.0, 0.0);
@@ -1443,6 +1640,11 @@ struct Solver final : HandleBase {
   }
   void factor_q() {
     const int64_t q2 = n_y * n_y;
+    if (lu_sq()) {                            // approx_lu!(perm, Q) (MPMP.jl:1499-1505)
+      vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
+      lu_Q.launch(stream, info + info_Q0);
+      return;
+    }
     if (reg_Q) {
       ci_Q.launch(stream, info + info_Q0);    // Qf = L_Q^-1
       q_qinv.launch(stream, 1.0, 0.0);        // Q^-1 = L_Q^-T L_Q^-1
@@ -1543,6 +1745,10 @@ struct Solver final : HandleBase {
       HIPCHK(hipStreamWaitEvent(stream, ev_x21, 0));
       pending_x21 = false;
     }
+    if (lu_sq()) {
+      direction_solves_lu(tag);
+      return;
+    }
     if (reg_S) {
       q_t.launch(stream, 1.0, 0.0);
     } else {
@@ -1578,6 +1784,30 @@ struct Solver final : HandleBase {
       p_Wdy.launch(stream, 1.0, 1.0);
       t_dx.launch(stream, true);
     }
+  }
+  // the same with the LU factors (approx_solve_tril!/approx_solve_lu_precomp!/approx_solve_triu!,
+  // MPMP.jl:1751-1773)
+  void direction_solves_lu(int tag) {
+    pm_rhs.launch(stream);                    // t_j = rhs_j[perm_j]
+    tl_t.launch(stream, false);               // t_j = L_j^-1 t_j
+    lq_Wt.launch(stream, 1.0, 0.0);           // slab_j = W2_j^T t_j  (B_j^T U_j^-1 t_j)
+    if (world == 1 && nc()) {
+      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, uvec, pvec, 1.0, -1.0);
+    } else {
+      if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+      else fill(xsend, 0.0, n_y);
+      exchange(tag, n_y);
+      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec, pvec, 1.0, -1.0);
+    }
+    if (pending_q) {
+      HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
+      pending_q = false;
+    }
+    pm_r.launch(stream);                      // dy = (p - u)[perm_Q]
+    tl_Q1.launch(stream, false);              // L_Q^-1
+    tl_Q2.launch(stream, true);               // U_Q^-1
+    p_Wdy.launch(stream, 1.0, 1.0);           // dx_j = t_j + W1_j dy
+    tl_dx.launch(stream, true);               // dx_j = U_j^-1 (.)
   }
   void st_corrector_r(const clrsdp_params* prm, int pd_feas) {
     blk_dot(X, Y, dX, dY, 1, SC_DOT_XDY, 5);
@@ -1623,9 +1853,13 @@ struct Solver final : HandleBase {
       } else {
         fill(xsend, 1e300, 2);  // no local blocks: neutral element of min
       }
-      exchange(8, 2);
-      reduce_ranks(2, 0, 3, SC_MINEIG_X);
-      reduce_ranks(2, 1, 3, SC_MINEIG_Y);
+      // + this rank's failure bits: every rank guards its update and reports (and falls back)
+      // on the OR over all ranks, so the ranks stay in step
+      status_bits<T><<<1, 256, 0, stream>>>(info, nb(), nc() + nc2, info_S0, info_Q0, info_L0, xsend + 2);
+      exchange(8, 3);
+      status_gather<T><<<1, 64, 0, stream>>>(xrecv, world, 3, 2, info + info_G);
+      reduce_ranks(3, 0, 3, SC_MINEIG_X);
+      reduce_ranks(3, 1, 3, SC_MINEIG_Y);
     }
     scalars(prm, pd_feas, 2);
   }
@@ -1688,18 +1922,53 @@ struct Solver final : HandleBase {
     HIPCHK(hipGetLastError());
   }
 
-  // both parse the host mirror filled by stat_fetch()
+  // both parse the host mirror filled by stat_fetch().  Failure bits: 1 S_j, 2 Q, 4 X
+  // (Cholesky), 8 X^-1 by LU, 16 Y (step length); with world > 1 the OR over all ranks
+  // (info_G, STEP's exchange), so every rank returns the same code
+  int fail_bits(const int* h) const {
+    int b = 0;
+    for (int i = 0; i < nb(); ++i) {
+      if (h[i]) b |= 4;
+      if (h[info_Y0 + i]) b |= 16;
+      if (h[info_L0 + i]) b |= 8;
+    }
+    for (int i = 0; i < nc() + nc2; ++i)
+      if (h[info_S0 + i]) b |= 1;
+    if (h[info_Q0]) b |= 2;
+    return b;
+  }
   int check_info(const char* blk = nullptr) {
     const int* h = reinterpret_cast<const int*>((blk ? blk : stat_host) + stat_info_off);
-    for (int i = 0; i < nb(); ++i)
-      if (h[i]) { err = "X block not positive definite (spd_inv! failed)"; return CLRSDP_E_NOT_PD_X; }
-    for (int i = 0; i < nc() + nc2; ++i)
-      if (h[info_S0 + i]) { err = "S was not decomposed succesfully, try again with higher precision"; return CLRSDP_E_NOT_PD_S; }
-    if (h[info_Q0]) { err = "Q was not decomposed correctly. Try restarting with a higher precision."; return CLRSDP_E_NOT_PD_Q; }
-    for (int i = 0; i < nb(); ++i)
-      if (h[info_Y0 + i]) { err = "The step length could not be calculated correctly (Y not PD)."; return CLRSDP_E_STEP; }
+    const int b = (world > 1 && (comm || xfn)) ? h[info_G] : fail_bits(h);
+    if (b & 4) {
+      if (lu_x()) {  // X^-1 came from LU; cho!(X) of the step length failed (MPMP.jl:1846-1882)
+        err = "The step length could not be calculated correctly (X not PD).";
+        return CLRSDP_E_STEP;
+      }
+      err = "X block not positive definite (spd_inv! failed)";
+      return CLRSDP_E_NOT_PD_X;
+    }
+    if (b & 8) { err = "The inverse was not computed correctly. Try again with higher precision"; return CLRSDP_E_NOT_PD_X; }
+    if (b & 1) { err = "S was not decomposed succesfully, try again with higher precision"; return CLRSDP_E_NOT_PD_S; }
+    if (b & 2) { err = "Q was not decomposed correctly. Try restarting with a higher precision."; return CLRSDP_E_NOT_PD_Q; }
+    if (b & 16) { err = "The step length could not be calculated correctly (Y not PD)."; return CLRSDP_E_STEP; }
     return CLRSDP_OK;
   }
+  // A Cholesky failure the LU fallback covers: switch (for the rest of the solve) and report
+  // true, so the caller re-runs the loop body (its update was skipped, the state is unchanged)
+  bool fallback(int rc) {
+    if (!(fact_flags & CLRSDP_FACT_FALLBACK)) return false;
+    int add = 0;
+    if ((rc == CLRSDP_E_NOT_PD_S || rc == CLRSDP_E_NOT_PD_Q) && !lu_sq()) add = CLRSDP_FACT_LU_SQ;
+    else if (rc == CLRSDP_E_NOT_PD_X && !lu_x()) add = CLRSDP_FACT_LU_X;
+    if (!add) return false;
+    build_lu_plans();
+    fact_flags |= add;
+    drop_graphs();
+    ++fallbacks;
+    return true;
+  }
+  int fallbacks = 0;
 
   void read_stats(clrsdp_iter_stats* st, const char* blk = nullptr) {
     const T* h = reinterpret_cast<const T*>(blk ? blk : stat_host);
@@ -1857,6 +2126,12 @@ struct Solver final : HandleBase {
   int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
     if (inflight) { err = "iterate with loop bodies in flight (call iterate_wait)"; return CLRSDP_E_STATE; }
+    for (;;) {
+      const int rc = iterate_once(prm, pd_feas, st);
+      if (!fallback(rc)) return rc;
+    }
+  }
+  int iterate_once(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) {
     if (graph_ok()) launch_graph(prm, pd_feas);
     else enqueue_iteration(prm, pd_feas);
     res_from_copy = false;
@@ -1904,12 +2179,7 @@ struct Solver final : HandleBase {
                               hipMemcpyDeviceToDevice, stream));
   }
   void save_state() override {
-    if (!snap) {
-      snap = dmalloc<T>((size_t)nx + 2 * (size_t)nblk_el + (size_t)n_y + SC_COUNT);
-      // dmalloc's hipMemset runs on the null stream, which a non-blocking handle stream does
-      // not order against: without this the zero fill can land after the first copy below
-      HIPCHK(hipDeviceSynchronize());
-    }
+    if (!snap) snap = dmalloc<T>((size_t)nx + 2 * (size_t)nblk_el + (size_t)n_y + SC_COUNT);
     snap_copy(true);
     snapped = true;
   }
@@ -1926,8 +2196,10 @@ struct Solver final : HandleBase {
   char* ring_host[2] = {nullptr, nullptr};
   hipEvent_t ring_ev[2] = {nullptr, nullptr};
   int ring_head = 0, inflight = 0;
+  clrsdp_params last_prm{};
   int iterate_async(const clrsdp_params* prm) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
+    last_prm = *prm;
     if (inflight >= 2) { err = "two loop bodies already in flight (call iterate_wait)"; return CLRSDP_E_STATE; }
     if (!ring_host[0]) {
       for (int i = 0; i < 2; ++i) {
@@ -1958,6 +2230,19 @@ struct Solver final : HandleBase {
     if (halted) return CLRSDP_OK;   // skipped body: its factorisations may fail, nothing applied
     const int rc = check_info(ring_host[slot]);
     st->status = rc;
+    if (fallback(rc)) {
+      // the bodies behind this one ran on the same (unchanged) state and failed alike: wait for
+      // them, then re-enqueue this body and those behind it with the LU factorisations
+      const int behind = inflight;
+      for (int q = 0; q < behind; ++q) HIPCHK(hipEventSynchronize(ring_ev[(ring_head + q) % 2]));
+      inflight = 0;
+      const clrsdp_params prm = last_prm;
+      for (int q = 0; q <= behind; ++q) {
+        const int r2 = iterate_async(&prm);
+        if (r2) return r2;
+      }
+      return iterate_wait(st, ran);
+    }
     return rc;
   }
 
@@ -2054,7 +2339,7 @@ struct DevBuf {
 
 int step_length_f64(int device, int64_t nblk, const int64_t* n, const double* Mh, const double* dMh,
                     double gamma, double* alpha, double* min_eig, std::string& err) {
-  HIPCHK(hipSetDevice(device));
+  DeviceGuard dg(device);
   std::vector<int64_t> off(nblk + 1, 0);
   int nmax = 0;
   for (int64_t b = 0; b < nblk; ++b) {
@@ -2071,7 +2356,6 @@ int step_length_f64(int device, int64_t nblk, const int64_t* n, const double* Mh
   double* t2 = mem.alloc<double>(tot);
   double* eig = mem.alloc<double>(nblk);
   int* info = mem.alloc<int>(nblk);
-  HIPCHK(hipDeviceSynchronize());  // the zero fills (null stream) before the copies below
   HIPCHK(hipMemcpy(M, Mh, tot * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dM, dMh, tot * sizeof(double), hipMemcpyHostToDevice));
   CholInvPlan<double> ci;
@@ -2148,6 +2432,7 @@ struct clrsdp_handle {
 
 #define GUARD(h, body)                                          \
   try {                                                         \
+    DeviceGuard dg_(guard_dev(h));                              \
     body                                                        \
   } catch (const ClrsdpError& e) {                              \
     g_last_error = e.msg;                                       \
@@ -2158,6 +2443,13 @@ struct clrsdp_handle {
     if (h) (h)->impl->err = e.what();                           \
     return CLRSDP_E_HIP;                                        \
   }
+
+static int guard_dev(const clrsdp_handle* h) {
+  if (h) return h->impl->dev;
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d;
+}
 
 extern "C" {
 
@@ -2172,6 +2464,7 @@ int32_t clrsdp_create(const clrsdp_desc* desc, const clrsdp_config* cfg, clrsdp_
   clrsdp_handle* h = nullptr;
   if (!desc || !cfg || !out) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
   GUARD(h, {
+    DeviceGuard dg(cfg->device);
     auto* hh = new clrsdp_handle();
     if (cfg->precision_words == 1) hh->impl.reset(new Solver<double>(desc, cfg));
     else if (cfg->precision_words == 2) hh->impl.reset(new Solver<dd>(desc, cfg));
@@ -2314,6 +2607,17 @@ int32_t clrsdp_step_length(int32_t device, int64_t nblocks, const int64_t* n, co
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on) {
   if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
   GUARD(h, { h->impl->set_timing(on); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_set_factorization(clrsdp_handle* h, int32_t flags) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->set_factorization(flags); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_get_factorization(const clrsdp_handle* h, int32_t* flags) {
+  if (!h || !flags) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  *flags = h->impl->get_factorization();
+  return CLRSDP_OK;
 }
 
 int32_t clrsdp_destroy(clrsdp_handle* h) {

@@ -784,14 +784,18 @@ __global__ __launch_bounds__(NT) void potrf_batched(const MatDesc<T>* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// Triangular solves with L from potrf (lower, non-unit), in place on B:
+// Triangular solves with a lower triangular L (potrf's, non-unit), in place on B:
 //   TRANS = false:  B <- L^-1 B     (forward substitution)
 //   TRANS = true :  B <- L^-T B     (backward substitution)
+// UNIT: L has a unit diagonal (the L factor of getrf_batched, approx_solve_tril!(.., 1)).
+// STORE_T: L is read transposed from upper storage, L(i, j) = A[j + i*ld] -- with the U factor
+// of getrf_batched: forward U^T x = b (B^T U^-1, MPMP.jl:1457-1460) and, with TRANS, backward
+// U x = b (approx_solve_triu!, MPMP.jl:1772).
 // One workgroup per (matrix, NC-column tile of B); NB-row blocks; L panel staged in LDS.  The
 // diagonal enters as reciprocals (one division per row, not per right-hand side: a multi-word
 // division is an order of magnitude dearer than a product).
 // ------------------------------------------------------------------------------------------
-template <class T, bool TRANS, int NB, int NC, int NT = 256>
+template <class T, bool TRANS, int NB, int NC, int NT = 256, bool UNIT = false, bool STORE_T = false>
 __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict__ descs,
                                                     const int* __restrict__ t2d) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -804,6 +808,8 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
   const int nc = min(NC, d.nrhs - c0);
   const int n = d.n, tid = threadIdx.x;
   const T* L = d.L;
+  const size_t ldl = d.ldl;
+  auto lat = [&](int i, int j) -> T { return STORE_T ? L[j + (size_t)i * ldl] : L[i + (size_t)j * ldl]; };
   T* B = d.B + (size_t)c0 * d.ldb;
   const int nblk = (n + NB - 1) / NB;
   for (int bi = 0; bi < nblk; ++bi) {
@@ -811,16 +817,16 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
     const int nb = min(NB, n - i0);
     for (int e = tid; e < nb * nb; e += blockDim.x) {
       const int i = e % nb, j = e / nb;
-      D[i + j * NB] = L[(i0 + i) + (size_t)(i0 + j) * d.ldl];
+      D[i + j * NB] = lat(i0 + i, i0 + j);
     }
-    if (tid < nb) rdg[tid] = T(1.0) / L[(i0 + tid) + (size_t)(i0 + tid) * d.ldl];
+    if (tid < nb) rdg[tid] = UNIT ? T(1.0) : T(1.0) / lat(i0 + tid, i0 + tid);
     // panel of the rows still to be updated
     const int pr0 = TRANS ? 0 : i0 + nb;
     const int pm = TRANS ? i0 : n - i0 - nb;
     for (int e = tid; e < nb * pm; e += blockDim.x) {
       const int i = e % pm, q = e / pm;
       // non-trans: P[q][i] = L[pr0 + i, i0 + q];  trans: P[q][i] = L[i0 + q, i]
-      P[q * pm + i] = TRANS ? L[(i0 + q) + (size_t)i * d.ldl] : L[(pr0 + i) + (size_t)(i0 + q) * d.ldl];
+      P[q * pm + i] = TRANS ? lat(i0 + q, i) : lat(pr0 + i, i0 + q);
     }
     __syncthreads();
     // the diagonal block, column-oriented: lane r of a 16-lane group holds row r of one
@@ -837,7 +843,7 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
           if (q < nb) {
-            if (r == q) xr = v * rdg[q];
+            if (r == q) xr = UNIT ? v : v * rdg[q];
             const T xq = shfl_t(xr, base + q);
             if (r > q) v = v - D[r + q * NB] * xq;
           }
@@ -846,7 +852,7 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
 #pragma unroll
         for (int q = NB - 1; q >= 0; --q) {
           if (q < nb) {
-            if (r == q) xr = v * rdg[q];
+            if (r == q) xr = UNIT ? v : v * rdg[q];
             const T xq = shfl_t(xr, base + q);
             if (r < q) v = v - D[q + r * NB] * xq;
           }
@@ -866,6 +872,173 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
       *bp = *bp - s;
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// LU with partial pivoting in place, A[perm] = L U (L unit lower, U upper): approx_lu!
+// (MPMP.jl:1436, 1501) on midpoints, and the factor of approx_inv! (MPMP.jl:781, 788).  The
+// fallback of the Cholesky-based factorisations: taken once a Cholesky status
+// word fires, then for the rest of the solve, as the reference switches spd_inv! off.
+// One NT-thread workgroup per matrix, right-looking with NB-column panels.  The panel (rows
+// k0..n-1) is factorised in LDS column by column; the pivot is the first row of maximal |a_ik|
+// (approx_lu!'s and LAPACK's choice), found by a wave shuffle reduction and one LDS step.  The
+// panel's interchanges are then applied to the other columns, U12 = L11^-1 A12 is solved into
+// LDS and the trailing matrix is updated in global memory (L2-resident at these sizes).
+// perm[k] is the original row at position k (the reference's 1-based perms minus one);
+// info[b] = 0, or the 1-based column of a zero pivot (approx_lu!'s status 0).
+// ------------------------------------------------------------------------------------------
+template <class T> struct LuDesc {
+  T* A;
+  int* perm;
+  int n, lda;
+};
+template <class T, int NB> constexpr size_t getrf_lds_bytes(int n) { return 2 * sizeof(T) * (size_t)NB * n; }
+
+template <class T, int NB, int NT = 256>
+__global__ __launch_bounds__(NT) void getrf_batched(const LuDesc<T>* __restrict__ descs,
+                                                     int* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  constexpr int NWV = NT / 64;
+  const LuDesc<T> d = descs[blockIdx.x];
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const size_t lda = d.lda;
+  T* A = d.A;
+  T* P = reinterpret_cast<T*>(smem_raw);  // panel, P[q * pm + i]                 (NB x pm)
+  T* U = P + (size_t)NB * n;                // U12 of the panel, U[c * NB + q]     (NB x (n - k1))
+  __shared__ T wbest[NWV];
+  __shared__ int wrow[NWV];
+  __shared__ int piv[NB];
+  __shared__ T rpv;
+  __shared__ int fail;
+  if (tid == 0) fail = 0;
+  for (int i = tid; i < n; i += NT) d.perm[i] = i;
+  __syncthreads();
+  for (int k0 = 0; k0 < n; k0 += NB) {
+    const int nb = min(NB, n - k0), pm = n - k0, k1 = k0 + nb;
+    for (int e = tid; e < nb * pm; e += NT) {
+      const int i = e % pm, q = e / pm;
+      P[q * pm + i] = A[(k0 + i) + (size_t)(k0 + q) * lda];
+    }
+    __syncthreads();
+    for (int j = 0; j < nb; ++j) {
+      // pivot: first row i >= j of maximal |P(i, j)| (ties to the smaller row)
+      T best = T(-1.0);
+      int brow = pm;
+      for (int i = j + tid; i < pm; i += NT) {
+        const T a = Num<T>::abs_(P[j * pm + i]);
+        if (a > best) { best = a; brow = i; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const T ob = shfl_xor_t(best, o);
+        const int orow = __shfl_xor(brow, o);
+        if (ob > best || (!(ob < best) && orow < brow)) { best = ob; brow = orow; }
+      }
+      if (lane == 0) { wbest[wv] = best; wrow[wv] = brow; }
+      __syncthreads();
+      if (tid == 0) {
+        T b = wbest[0];
+        int r = wrow[0];
+        for (int w = 1; w < NWV; ++w)
+          if (wbest[w] > b || (!(wbest[w] < b) && wrow[w] < r)) { b = wbest[w]; r = wrow[w]; }
+        if (!(b > T(0.0))) {
+          fail = k0 + j + 1;
+        } else {
+          piv[j] = k0 + r;
+          if (r != j) {  // interchange rows j and r of the panel, and of perm
+            for (int q = 0; q < nb; ++q) {
+              const T t = P[q * pm + j];
+              P[q * pm + j] = P[q * pm + r];
+              P[q * pm + r] = t;
+            }
+            const int t = d.perm[k0 + j];
+            d.perm[k0 + j] = d.perm[k0 + r];
+            d.perm[k0 + r] = t;
+          }
+          rpv = recip_fast(P[j * pm + j]);
+        }
+      }
+      __syncthreads();
+      if (fail) break;
+      const T rp = rpv;
+      for (int i = j + 1 + tid; i < pm; i += NT) P[j * pm + i] = P[j * pm + i] * rp;
+      __syncthreads();
+      const int r = pm - j - 1;
+      for (int e = tid; e < r * (nb - j - 1); e += NT) {
+        const int i = j + 1 + e % r, c = j + 1 + e / r;
+        P[c * pm + i] = P[c * pm + i] - P[j * pm + i] * P[c * pm + j];
+      }
+      __syncthreads();
+    }
+    if (fail) break;
+    for (int e = tid; e < nb * pm; e += NT) {
+      const int i = e % pm, q = e / pm;
+      A[(k0 + i) + (size_t)(k0 + q) * lda] = P[q * pm + i];
+    }
+    // the panel's interchanges on the columns left and right of it (sequential per column)
+    for (int c = tid; c < n - nb; c += NT) {
+      const int col = c < k0 ? c : c + nb;
+      for (int j = 0; j < nb; ++j) {
+        const int r = piv[j];
+        if (r != k0 + j) {
+          T* a0 = A + (k0 + j) + (size_t)col * lda;
+          T* a1 = A + r + (size_t)col * lda;
+          const T t = *a0;
+          *a0 = *a1;
+          *a1 = t;
+        }
+      }
+    }
+    __syncthreads();
+    const int nr = n - k1;
+    if (nr <= 0) break;
+    // U12 = L11^-1 A12 (unit lower), one column per thread (compile-time indexed: registers)
+    for (int c = tid; c < nr; c += NT) {
+      T x[NB];
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        if (q < nb) {
+          T v = A[(k0 + q) + (size_t)(k1 + c) * lda];
+#pragma unroll
+          for (int p = 0; p < q; ++p) v = v - P[p * pm + q] * x[p];
+          x[q] = v;
+          U[c * NB + q] = v;
+          A[(k0 + q) + (size_t)(k1 + c) * lda] = v;
+        }
+      }
+    }
+    __syncthreads();
+    // trailing update A22 -= L21 U12
+    for (int e = tid; e < nr * nr; e += NT) {
+      const int i = e % nr, c = e / nr;
+      T s = T(0.0);
+      for (int q = 0; q < nb; ++q) s += P[q * pm + nb + i] * U[c * NB + q];
+      T* a = A + (k1 + i) + (size_t)(k1 + c) * lda;
+      *a = *a - s;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) info[blockIdx.x] = fail;
+}
+
+// out = rows perm of in (out[i, c] = in[perm[i], c]): B_j[perms[j], :] (MPMP.jl:1463) and
+// rhs[perm] (MPMP.jl:1752, 1764).  grid (chunks, problems).  ident: in is the identity
+// (approx_inv!'s right-hand side P I).
+template <class T> struct PermDesc {
+  const T* in;
+  T* out;
+  const int* perm;
+  int n, ncol, ldi, ldo;
+};
+template <class T>
+__global__ __launch_bounds__(256) void perm_rows(const PermDesc<T>* __restrict__ descs, int ident) {
+  const PermDesc<T> d = descs[blockIdx.y];
+  const long long tot = (long long)d.n * d.ncol;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < tot; e += 256LL * gridDim.x) {
+    const int i = (int)(e % d.n), c = (int)(e / d.n);
+    const int pi = d.perm[i];
+    d.out[i + (size_t)c * d.ldo] = ident ? (pi == c ? T(1.0) : T(0.0)) : d.in[pi + (size_t)c * d.ldi];
   }
 }
 
@@ -1756,8 +1929,44 @@ template <class T> struct ScalarParams {
   int* zero_ptr;
   int* halt_ptr;  // which == 0: status word "skip this loop body" (device-decided termination)
   unsigned long long* stamps;  // which == 0: reset the SCHUR-stage clock pair (min start, max end)
+  // which == 3: the loop control (gap, pd_feas, halt) is left as the last body that ran decided
+  // it when a status word guard[0..nguard) is set: the body failed and applied nothing (the LU
+  // fallback re-runs it with the control of the body before)
+  const int* guard;
+  int nguard;
   FoldRed<T> red[6];
 };
+
+// This rank's failure bits (1 S_j, 2 Q, 4 X, 8 X^-1 by LU, 16 Y; the layout of the Solver's
+// status words) as a value of T for STEP's all-gather, and their OR over the gathered ranks
+// into one status word (so every rank skips its update and reports alike).
+template <class T>
+__global__ __launch_bounds__(256) void status_bits(const int* __restrict__ info, int nb, int nS,
+                                                   int s0, int q0, int l0, T* out) {
+  __shared__ int bits;
+  if (threadIdx.x == 0) bits = 0;
+  __syncthreads();
+  int v = 0;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    if (info[i]) v |= 4;
+    if (info[nb + i]) v |= 16;
+    if (info[l0 + i]) v |= 8;
+  }
+  for (int i = threadIdx.x; i < nS; i += 256)
+    if (info[s0 + i]) v |= 1;
+  if (threadIdx.x == 0 && info[q0]) v |= 2;
+  if (v) atomicOr(&bits, v);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = T((double)bits);
+}
+template <class T>
+__global__ void status_gather(const T* __restrict__ recv, int world, long long stride, int slot,
+                              int* dst) {
+  if (threadIdx.x != 0) return;
+  int b = 0;
+  for (int r = 0; r < world; ++r) b |= (int)Num<T>::hi(recv[(size_t)r * stride + slot]);
+  *dst = b;
+}
 
 template <class T>
 __device__ inline bool pd_feasible(const T* sc, const ScalarParams<T>& p) {
@@ -1860,7 +2069,9 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     if (p.zero_cy) sc[SC_DOT_CY] = T(0.0);
     sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;
     sc[SC_DOBJ] = sc[SC_DOT_CY] + sc[SC_DOT_BY] + p.b0;
-    control_update(sc, p, false);
+    bool failed = false;
+    for (int e = 0; e < p.nguard; ++e) failed = failed || p.guard[e] != 0;
+    if (!failed) control_update(sc, p, false);
   } else if (which == 4) {  // objectives + control of the initial point (MPMP.jl:723-736)
     if (p.zero_cy) sc[SC_DOT_CY] = T(0.0);
     sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;

@@ -759,7 +759,11 @@ __device__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const T pn = dv[u] * pc - fv[u] * pm;
+      T pn = dv[u] * pc - fv[u] * pm;
+      // a zero minor followed by e2_i = 0 (a decoupled tridiagonal) would keep the recurrence
+      // at zero and hide every later sign change: count it as negative (LAPACK's -pivmin),
+      // as the fp64 count floors e2 at 2^-900
+      if (Num<T>::hi(pn) == 0.0) pn = T(-__builtin_ldexp(fabs(Num<T>::hi(pc)), -300));
       neg = neg || (pn < T(0.0));
       pm = pc;
       pc = pn;
@@ -772,7 +776,8 @@ __device__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict
     }
   }
   for (; i < n; ++i) {
-    const T pn = (dg[i] - sigma) * pc - (i > 0 ? e2[i - 1] : T(0.0)) * pm;
+    T pn = (dg[i] - sigma) * pc - (i > 0 ? e2[i - 1] : T(0.0)) * pm;
+    if (Num<T>::hi(pn) == 0.0) pn = T(-__builtin_ldexp(fabs(Num<T>::hi(pc)), -300));
     neg = neg || (pn < T(0.0));
     pm = pc;
     pc = pn;

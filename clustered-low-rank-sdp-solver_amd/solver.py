@@ -236,6 +236,18 @@ class DeviceSolver:
         """Restore the last snapshot, stream-ordered after the work already enqueued."""
         self.check(self.L.clrsdp_restore_state(self.h))
 
+    def set_factorization(self, flags: int):
+        """clrsdp_set_factorization: FACT_FALLBACK (default: pivoted LU once a Cholesky fails),
+        FACT_LU_SQ (S_j and Q by pivoted LU, the reference's approx_lu!), FACT_LU_X (X^-1 by
+        approx_inv!)."""
+        self.check(self.L.clrsdp_set_factorization(self.h, int(flags)))
+
+    @property
+    def factorization(self) -> int:
+        f = C.c_int32(0)
+        self.check(self.L.clrsdp_get_factorization(self.h, C.byref(f)))
+        return f.value
+
     def set_stream(self, stream_ptr: int):
         self.check(self.L.clrsdp_set_stream(self.h, C.c_void_p(stream_ptr)))
 
@@ -383,7 +395,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
                   dual_error_threshold=None, need_primal_feasible=False, need_dual_feasible=False,
                   testing=True, initial_solutions=(), precision_words=1, device=0, verbose=True,
                   solver: Optional[DeviceSolver] = None, return_info=False, record_exact=False,
-                  pipelined: Optional[bool] = None):
+                  pipelined: Optional[bool] = None, factorization: Optional[int] = None):
     """Solve the clustered low-rank SDP on the GPU; same signature/semantics as MPMP.jl:595-614.
 
     Returns ``(x, X, y, Y, P, p, d, duality_gap, primal_objective, dual_objective, time)``
@@ -393,6 +405,11 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     the device (clrsdp_iterate_async / _wait) and pd_feas / terminate() are evaluated on the
     device with the same thresholds, so no host round trip separates two loop bodies.  The
     iterates, the log and the returned values are the same as the synchronous loop's.
+
+    ``factorization``: clrsdp_set_factorization flags (default FACT_FALLBACK: Cholesky, and the
+    reference's pivoted LU once a Cholesky fails, announced like MPMP.jl:776-778).  At
+    double-double and quad-double the returned gap and objectives are mpmath numbers at the
+    state's full precision (MPMP.jl:1021-1023), not leading limbs.
     """
     kw = dict(beta_infeasible=beta_infeasible, beta_feasible=beta_feasible, gamma=gamma,
               omega_p=omega_p, omega_d=omega_d, duality_gap_threshold=duality_gap_threshold,
@@ -412,6 +429,9 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     else:
         x, X, y, Y = initial_point(bi, float(prm_v["omega_p"]), float(prm_v["omega_d"]))
     dev.set_state(x, X, y, Y)
+    if factorization is not None:
+        dev.set_factorization(factorization)
+    fact_seen = dev.factorization
     b0f = float(b0)
     if pipelined is None:
         # one GPU: the hipGraph replay leaves only a short host round trip between bodies and
@@ -440,7 +460,16 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     timed = bool(getattr(dev, "timing", False))
 
     def record(st):
-        nonlocal p_obj, d_obj, dual_gap, perr, derr, pd_feas, it
+        nonlocal p_obj, d_obj, dual_gap, perr, derr, pd_feas, it, fact_seen
+        f = dev.factorization
+        if f != fact_seen:   # the device switched to LU for the rest of the solve
+            if (f & ~fact_seen) & _lib.FACT_LU_X:
+                out("The inverse of X could not be computed with the cholesky factorization. We "
+                    "switch to using the LU decomposition.")
+            if (f & ~fact_seen) & _lib.FACT_LU_SQ:
+                out("The Cholesky factorization of S or Q failed. We switch to the pivoted LU "
+                    "decomposition (approx_lu!) for S and Q.")
+            fact_seen = f
         if it > 2:
             phase[:] += np.array(st.phase_ms[:])
         elif testing and timed:  # MPMP.jl:899-920: the times of the first iterations
@@ -515,7 +544,18 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     P, d = dev.global_P_d()
     p = dev.buffer(_lib.BUF_PVEC)
     gap_nob0 = abs((p_obj - b0f) - (d_obj - b0f)) / max(1.0, abs((p_obj - b0f) + (d_obj - b0f)))
-    res = (xf, Xf, yf, Yf, P, p, d, gap_nob0, p_obj, d_obj, t_total)
+    ret_p, ret_d = p_obj, d_obj
+    if dev.w > 1:
+        # MPMP.jl:1021-1023 at the state's precision: the device's objectives of the final state
+        # (all limbs) and the gap without b0 from them
+        import mpmath
+        with mpmath.workprec(64 * dev.w + 64):
+            sc = dev.buffer(_lib.BUF_SCALARS, exact=True)
+            ret_p, ret_d = +sc[_lib.SC["p_obj"]], +sc[_lib.SC["d_obj"]]
+            b0m = mpmath.mpf(b0)
+            pp, dd_ = ret_p - b0m, ret_d - b0m
+            gap_nob0 = abs(pp - dd_) / max(mpmath.mpf(1), abs(pp + dd_))
+    res = (xf, Xf, yf, Yf, P, p, d, gap_nob0, ret_p, ret_d, t_total)
     if return_info:
         res = res + (RunInfo(it - 1, log, phase, t_total,
                              (time.time() - t_after2) if t_after2 else 0.0, status, exact),)

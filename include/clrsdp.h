@@ -255,6 +255,21 @@ int32_t clrsdp_synchronize(clrsdp_handle* h);
  * native RCCL communicator), clrsdp_iterate replays a captured hipGraph of the loop body. */
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on);
 
+/* Factorisations of S_j, Q and X (flags, default CLRSDP_FACT_FALLBACK).  The device factorises
+ * S_j and Q by Cholesky (they are SPD) and X^-1 by the Cholesky inverse (spd_inv!).  The
+ * reference factorises S_j and Q by partially pivoted LU (approx_lu!, MPMP.jl:1433-1442,
+ * 1499-1505) and switches X^-1 to LU when spd_inv! fails (approx_inv!, MPMP.jl:774-786):
+ *   CLRSDP_FACT_FALLBACK  when a Cholesky fails, set the matching LU flag and re-run the loop
+ *                         body (its update was not applied); LU then stays on for the solve
+ *   CLRSDP_FACT_LU_SQ     S_j and Q by pivoted LU now (the reference's own factorisation)
+ *   CLRSDP_FACT_LU_X      X^-1 by pivoted LU now (approx_inv!)
+ * clrsdp_get_factorization reports the current flags (a fallback adds its LU flag).
+ * A failed LU is the reference's error (CLRSDP_E_NOT_PD_S / _Q / _X). */
+#define CLRSDP_FACT_FALLBACK 1
+#define CLRSDP_FACT_LU_SQ 2
+#define CLRSDP_FACT_LU_X 4
+int32_t clrsdp_set_factorization(clrsdp_handle* h, int32_t flags);
+int32_t clrsdp_get_factorization(const clrsdp_handle* h, int32_t* flags);
 int32_t clrsdp_destroy(clrsdp_handle* h);
 
 /* Stand-alone step length of a block-diagonal pair, fp64 (replaces compute_step_length,

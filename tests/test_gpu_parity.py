@@ -12,7 +12,8 @@ import os
 import numpy as np
 import pytest
 
-from helpers import CONFIGS_SMALL, poly_min_instance, rel_err
+from helpers import (CONFIGS_SMALL, compare_summary, poly_min_instance, rel_err, residual_scales,
+                     stage_device, stage_reference)
 
 pytestmark = pytest.mark.gpu
 
@@ -35,63 +36,50 @@ def _oracle_states(oracle, cons, bi, b, iters_before, ar=None, omega=10.0):
 
 
 def _stage_compare(pk, oracle, cons, b, iters_before=2, words=1, ar=None, tol=TOL64):
-    from clrsdp_amd import _lib as L
-    from clrsdp_amd import instance as inst
     bi = oracle.get_block_info(cons)
     state, nxt, it = _oracle_states(oracle, cons, bi, b, iters_before, ar)
     dev = pk.DeviceSolver(cons, b, pk.get_block_info(cons), precision_words=words)
     try:
-        x, X, y, Y = state
-        dev.set_state(x, X, y, Y)
-        P = pk.make_params("0.3", "0.1", "0.7", 0)
-        exact = words > 1
-        fl = lambda blocks: _blocks(inst, blocks)
-        buf = lambda k: np.array(dev.buffer(k, exact), dtype=float if not exact else object)
-        e = {}
-        dev.run_stage(L.STAGE_MU_R, P, False)
-        e["mu"] = rel_err([dev.scalar("mu", exact)], [it["mu"]])
-        e["R"] = rel_err(buf(L.BUF_R), fl(it["R"]))
-        dev.run_stage(L.STAGE_XINV, P, False)
-        e["Xinv"] = rel_err(buf(L.BUF_XINV), fl(it["X_inv"]))
-        dev.run_stage(L.STAGE_SCHUR, P, False)
-        e["S"] = rel_err(buf(L.BUF_S), np.concatenate([s.reshape(-1, order="F") for s in it["dec"].S_raw]))
-        ay = [it["A_Y"][j][l][r][s] for j in range(bi.J) for l in range(bi.L[j])
-              for r in range(bi.m[j]) for s in range(r + 1)]
-        e["A_Y"] = rel_err(buf(L.BUF_AY), np.concatenate(ay))
-        dev.run_stage(L.STAGE_FACTOR, P, False)
-        e["Q"] = rel_err(buf(L.BUF_Q), it["dec"].Q_raw.reshape(-1, order="F"))
-        dev.run_stage(L.STAGE_RESIDUALS, P, False)
-        Xscale = float(np.max(np.abs(np.array(fl(X), dtype=float))))
-        e["P"] = rel_err(buf(L.BUF_P), fl(it["P"]), Xscale)
-        e["p"] = rel_err(buf(L.BUF_PVEC), it["p"], float(np.max(np.abs(np.array(b, dtype=float)))))
-        # d is also a residual that reaches round-off once the dual is feasible
-        cscale = float(max(np.max(np.abs(np.array(c.c, dtype=float))) for c in cons))
-        e["d"] = rel_err(buf(L.BUF_DVEC), it["d"], cscale)
-        for stage, key, Rk in ((L.STAGE_PREDICTOR, "pred", None), (L.STAGE_CORRECTOR, "corr", "R2")):
-            if Rk:
-                dev.run_stage(L.STAGE_CORRECTOR_R, P, False)
-                e["beta_c"] = rel_err([dev.scalar("beta_c", exact)], [it["beta_c"]])
-                e["R2"] = rel_err(buf(L.BUF_R), fl(it["R2"]))
-            dev.run_stage(stage, P, False)
-            dx, dX, dy, dY = it[key]
-            e[key + "_dx"] = rel_err(buf(L.BUF_DX), dx)
-            e[key + "_dy"] = rel_err(buf(L.BUF_DY), dy)
-            e[key + "_dX"] = rel_err(buf(L.BUF_DXMAT), fl(dX))
-            e[key + "_dY"] = rel_err(buf(L.BUF_DYMAT), fl(dY))
-        dev.run_stage(L.STAGE_STEP, P, False)
-        e["alpha_p"] = rel_err([dev.scalar("alpha_p", exact)], [it["alpha_p"]])
-        e["alpha_d"] = rel_err([dev.scalar("alpha_d", exact)], [it["alpha_d"]])
-        dev.run_stage(L.STAGE_UPDATE, P, False)
-        xg, Xg, yg, Yg = dev.get_state(exact)
-        e["x+"] = rel_err(xg, nxt[0])
-        e["X+"] = rel_err(fl(Xg), fl(nxt[1]))
-        e["y+"] = rel_err(yg, nxt[2])
-        e["Y+"] = rel_err(fl(Yg), fl(nxt[3]))
-        bad = {k: v for k, v in e.items() if not v <= tol}
-        assert not bad, f"stage parity failures: {bad}"
-        return e
+        dev.set_state(*state)
+        got = stage_device(dev, words > 1)
     finally:
         dev.close()
+    ref = stage_reference(it, nxt, bi)
+    sc = residual_scales(cons, b, state[1])
+    e = {k: rel_err(got[k], ref[k], sc.get(k, 0.0)) for k in ref}
+    bad = {k: v for k, v in e.items() if not v <= tol}
+    assert not bad, f"stage parity failures: {bad}"
+    return e
+
+
+def _stage_compare_fixture(pk, name, words, tol, bits=256):
+    """Stage parity against a precomputed multi-precision oracle fixture
+    (tests/golden/make_stage_fixtures.py): sampled entries and linear sketches of every stage
+    buffer, scale-aware relative error <= tol."""
+    import gzip
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_stage_fixtures",
+                                                  os.path.join(GOLDEN, "make_stage_fixtures.py"))
+    M = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(M)
+    sf = os.path.join(GOLDEN, f"stage_{name}.npz")
+    cons, b = M.instance(name, sf)
+    bi = pk.get_block_info(cons)
+    state = M.load_state(sf, bi)
+    with gzip.open(os.path.join(GOLDEN, f"stage_{name}_mp{bits}.json.gz"), "rt") as f:
+        fx = json.load(f)
+    dev = pk.DeviceSolver(cons, b, bi, precision_words=words)
+    try:
+        dev.set_state(*state)
+        got = stage_device(dev, True)
+    finally:
+        dev.close()
+    sc = residual_scales(cons, b, state[1])
+    e = {k: compare_summary(got[k], rec, sc.get(k, 0.0)) for k, rec in fx["buffers"].items()}
+    print(name, words, bits, " ".join(f"{k}={v:.1e}" for k, v in e.items()))
+    bad = {k: v for k, v in e.items() if not v <= tol}
+    assert not bad, f"stage parity failures vs mp{bits}: {bad}"
+    return e
 
 
 CONFIGS_GPU = CONFIGS_SMALL + [
@@ -151,6 +139,23 @@ def test_stage_parity_sphere_packing_shape_qd(pk, oracle):
                         ar.asarray(cl.B), ar.asarray(cl.c),
                         [[[ar.num(x) for x in hk] for hk in Hl] for Hl in cl.H]) for cl in cons]
     _stage_compare(pk, oracle, consm, ar.asarray(b), iters_before=3, words=4, ar=ar, tol=1e-45)
+
+
+@pytest.mark.parametrize("bits", [128, 256])
+def test_stage_parity_dd_c4_shape(pk, bits):
+    """Config 4 at its own cluster shape (J = 2, delta = 64, rank 2, n_y = 64, dim_S = 127,
+    blocks of 64) at double-double against the 128- and 256-bit oracle: drives
+    potrf_batched<dd> / trsm_batched<dd> (dim_S > 64), chol_inv_reg<dd> and eigmin_lds<dd> at
+    n = 64 (MPMP.jl:1433-1465, 762-801, 1829-1898).  dd carries ~106 bits; 1e-25 relative
+    (scale-aware) leaves ~6 orders for the conditioning of S_j at this state."""
+    _stage_compare_fixture(pk, "c4dd", 2, 1e-25, bits)
+
+
+def test_stage_parity_qd_twin(pk):
+    """Quad-double twin (J = 2, delta = 32, rank 2, n_y = 32, dim_S = 63): chol_inv_reg<qd> at
+    n = 32, potrf_batched<qd> / trsm_batched<qd> at dim_S > 32, eigmin_lds<qd> at n = 32,
+    against the 256-bit oracle at 1e-50 relative (qd carries ~212 bits)."""
+    _stage_compare_fixture(pk, "qd32", 4, 1e-50, 256)
 
 
 def _golden(name):

@@ -170,3 +170,37 @@ def test_golden_vectors(pk, oracle, name):
         for key in ("mu", "alpha_p", "alpha_d", "beta"):
             assert abs(float(getattr(row, key)) - float(ref[key])) <= tol * max(1.0, abs(float(ref[key]))), key
     assert rel_err(res.x, np.array([float(v) for v in g["x"]])) < tol
+
+
+@pytest.mark.parametrize("name,bits", [("c4dd", 128), ("c4dd", 256), ("qd32", 256)])
+def test_stage_fixtures_agree_with_fp64_oracle(pk, oracle, name, bits):
+    """The precomputed multi-precision stage fixtures (tests/golden/make_stage_fixtures.py) are
+    consistent with the fp64 oracle run on the same stored state: every sampled entry and
+    sketch within fp64 round-off times the conditioning of this mid-run state."""
+    import gzip
+    import importlib.util
+    import json
+    import os
+
+    from helpers import compare_summary, residual_scales, stage_reference
+    gdir = os.path.join(os.path.dirname(__file__), "golden")
+    spec = importlib.util.spec_from_file_location("make_stage_fixtures",
+                                                  os.path.join(gdir, "make_stage_fixtures.py"))
+    M = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(M)
+    sf = os.path.join(gdir, f"stage_{name}.npz")
+    if not os.path.exists(os.path.join(gdir, f"stage_{name}_mp{bits}.json.gz")):
+        pytest.skip("fixture not generated")
+    cons, b = M.instance(name, sf)
+    bi = oracle.get_block_info(cons)
+    state = M.load_state(sf, bi)
+    ar = oracle.Fp64()
+    prm = {k: oracle._param(ar, v) for k, v in oracle.DEFAULTS.items()}
+    nxt, it = oracle.iteration(ar, cons, bi, b, None, 0.0, state, False, prm)
+    ref = stage_reference(it, nxt, bi)
+    with gzip.open(os.path.join(gdir, f"stage_{name}_mp{bits}.json.gz"), "rt") as f:
+        fx = json.load(f)
+    assert set(fx["buffers"]) == set(ref)
+    sc = residual_scales(cons, b, state[1])
+    e = {k: compare_summary(ref[k], rec, sc.get(k, 0.0)) for k, rec in fx["buffers"].items()}
+    assert max(e.values()) < 1e-9, e
