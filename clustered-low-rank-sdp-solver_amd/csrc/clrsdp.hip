@@ -432,15 +432,20 @@ struct LuPlan : PlanBase {
     h.push_back(LuDesc<T>{A, perm, n, lda});
     nmax = std::max(nmax, n);
   }
+  size_t lds = 0;
+  // (outside any graph capture: the LDS attribute is set here, not at launch)
   void finalize() {
-    if (!h.empty()) d = own(h);
+    if (h.empty()) return;
+    d = own(h);
+    lds = getrf_lds_bytes<T, NB>(nmax);
+    // the static LDS of the kernel (pivot search, pivots) comes on top of the dynamic panel
+    if (lds > LDS_MAX - 4096) throw ClrsdpError{CLRSDP_E_ARG, "LU fallback: matrix too large for the on-chip panel"};
+    if (lds > 64 * 1024)
+      HIPCHK(hipFuncSetAttribute((const void*)getrf_batched<T, NB, 256>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
   void launch(hipStream_t s, int* info) const {
     if (h.empty()) return;
-    const size_t lds = getrf_lds_bytes<T, NB>(nmax);
-    if (lds > LDS_MAX) throw ClrsdpError{CLRSDP_E_ARG, "LU fallback: matrix too large for the on-chip panel"};
-    static std::atomic<unsigned long long> attr{0};
-    lds_attr_once(attr, (const void*)getrf_batched<T, NB, 256>, (int)LDS_MAX);
     getrf_batched<T, NB, 256><<<(unsigned)h.size(), 256, lds, s>>>(d, info);
     HIPCHK(hipGetLastError());
   }
@@ -654,7 +659,7 @@ struct Solver final : HandleBase {
   // first part of the predictor (iterate only; run_stage stays serial)
   hipStream_t aux = nullptr;
   hipEvent_t ev_m = nullptr, ev_x = nullptr, ev_s = nullptr, ev_r = nullptr, ev_qa = nullptr,
-             ev_q = nullptr;
+             ev_q = nullptr, ev_join = nullptr;
   bool pending_q = false;
   float phase_ms[CLRSDP_NUM_STAGES];
 
@@ -758,7 +763,7 @@ struct Solver final : HandleBase {
     // graph-boundary and join idle time against the lost overlap)
     if (std::getenv("CLRSDP_ONE_STREAM")) aux = own_stream;
     else HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21, &ev_ty})
+    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21, &ev_ty, &ev_join})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
     build_plans();
@@ -786,7 +791,7 @@ struct Solver final : HandleBase {
     for (char* r : ring_host)
       if (r) (void)hipHostFree(r);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ev_ty, ring_ev[0], ring_ev[1]})
+    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ev_ty, ev_join, ring_ev[0], ring_ev[1]})
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
       if (g) (void)hipGraphExecDestroy(g);
@@ -2111,8 +2116,13 @@ struct Solver final : HandleBase {
       try {
         enqueue_iteration(prm, pd_feas);
       } catch (...) {
+        // join the side stream (it may have been forked into the capture) so that the capture
+        // ends cleanly and the streams stay usable
+        if (aux != stream && hipEventRecord(ev_join, aux) == hipSuccess)
+          (void)hipStreamWaitEvent(stream, ev_join, 0);
         (void)hipStreamEndCapture(stream, &graph);
         if (graph) (void)hipGraphDestroy(graph);
+        (void)hipGetLastError();
         throw;
       }
       HIPCHK(hipStreamEndCapture(stream, &graph));

@@ -76,6 +76,16 @@ def test_lu_stage_parity_multiword(pk, oracle, words, tol):
                       words=words, ar=ar, tol=tol)
 
 
+def _run(dev, stage, P, L):
+    """run_stage, tolerating the Y status (the step length's cho!(Y), reported from XINV on:
+    Y is indefinite in these states on purpose)."""
+    try:
+        dev.run_stage(stage, P, False)
+    except L.ClrsdpError as e:
+        if e.code != L.E_STEP:
+            raise
+
+
 def _indefinite_Y_state(oracle, cons, b, bi):
     """A mid-run state whose Y blocks are shifted to be indefinite: S_j = (V^T X^-1 V) o (V^T Y V)
     is then indefinite (but well conditioned), so its Cholesky fails while pivoted LU does not."""
@@ -112,7 +122,7 @@ def test_cholesky_fails_lu_matches_oracle(pk, oracle, cfg):
         dev.set_factorization(0)
         dev.set_state(x, X, y, Y)
         for s in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR):
-            dev.run_stage(s, P, False)
+            _run(dev, s, P, L)
         with pytest.raises(L.ClrsdpError) as ei:
             dev.run_stage(L.STAGE_FACTOR, P, False)
         assert ei.value.code == L.E_NOT_PD_S
@@ -131,7 +141,7 @@ def test_cholesky_fails_lu_matches_oracle(pk, oracle, cfg):
         dev.set_state(x, X, y, Y)
         for s in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR, L.STAGE_FACTOR, L.STAGE_RESIDUALS,
                   L.STAGE_PREDICTOR):
-            dev.run_stage(s, P, False)
+            _run(dev, s, P, L)
         from clrsdp_amd import instance as inst
         e = {"Q": rel_err(dev.buffer(L.BUF_Q), dec.Q_raw.reshape(-1, order="F")),
              "dx": rel_err(dev.buffer(L.BUF_DX), dx), "dy": rel_err(dev.buffer(L.BUF_DY), dy),
