@@ -253,17 +253,24 @@ def test_live_schur_timing_keeps_iterates_bitwise(pk):
         assert np.array_equal(a[3][j], c[3][j])
 
 
-def test_not_positive_definite_reports_error(pk):
+@pytest.mark.parametrize("fallback", [False, True])
+def test_not_positive_definite_reports_error(pk, fallback):
+    """X not PD: spd_inv! fails (CLRSDP_E_NOT_PD_X, MPMP.jl:774-797).  With the default LU
+    fallback X^-1 comes from approx_inv! instead and the step length's cho!(X) fails, as in the
+    reference (CLRSDP_E_STEP, MPMP.jl:1846-1882)."""
     from clrsdp_amd import _lib as L
     cons, b = pk.synth(seed=9, J=2, delta=4, rank=1, n_y=3)
     bi = pk.get_block_info(cons)
     x, X, y, Y = pk.initial_point(bi, 10.0, 10.0)
     X[1][0][2, 2] = -5.0
     dev = pk.DeviceSolver(cons, b, bi)
+    if not fallback:
+        dev.set_factorization(0)
     dev.set_state(x, X, y, Y)
     with pytest.raises(L.ClrsdpError) as ei:
         dev.iterate(pk.make_params("0.3", "0.1", "0.7", 0), False)
-    assert ei.value.code == L.E_NOT_PD_X
+    assert ei.value.code == (L.E_STEP if fallback else L.E_NOT_PD_X)
+    assert dev.factorization == (L.FACT_FALLBACK | L.FACT_LU_X if fallback else 0)
     dev.close()
 
 
