@@ -17,14 +17,20 @@ if which in ("all", "poly"):
     from oracle import mpmp_oracle as O
     cons, b, pmin = poly_min_instance(pk)
     bi = pk.get_block_info(cons)
-    for fact in (1, 2):
-        res = pk.solverank1sdp(cons, b, bi, omega_p=10.0, omega_d=10.0, maxiterations=100,
-                               verbose=False, return_info=True, factorization=fact)
-        info = res[-1]
-        print("poly fp64 GPU fact=%d: status %s after %d it, gap %.3e, p_obj-pmin %.3e d_obj-pmin %.3e"
-              % (fact, info.status, info.iterations, res[7], res[8] - pmin, res[9] - pmin), flush=True)
+    for fact in (0, 1, 2, 3):
+        print("=== poly fp64 GPU factorization flags", fact, flush=True)
+        try:
+            res = pk.solverank1sdp(cons, b, bi, omega_p=10.0, omega_d=10.0, maxiterations=100,
+                                   verbose=True, return_info=True, factorization=fact)
+            info = res[-1]
+            print("poly fp64 GPU fact=%d: status %s after %d it, gap %.3e, p_obj-pmin %.3e d_obj-pmin %.3e"
+                  % (fact, info.status, info.iterations, res[7], res[8] - pmin, res[9] - pmin), flush=True)
+        except Exception as e:
+            print("poly fp64 GPU fact=%d raised: %s" % (fact, e), flush=True)
+    print("=== poly fp64 oracle", flush=True)
     try:
-        r = O.solverank1sdp(cons, b, O.get_block_info(cons), maxiterations=100, omega_p=10.0, omega_d=10.0)
+        r = O.solverank1sdp(cons, b, O.get_block_info(cons), maxiterations=100, omega_p=10.0,
+                            omega_d=10.0, verbose=True)
         print("poly fp64 oracle: status %s after %d it, gap %.3e, p-pmin %.3e" %
               (r.status, len(r.log), r.gap, r.p_obj - pmin), flush=True)
     except Exception as e:
