@@ -354,6 +354,8 @@ class RunInfo:
     time_loop_after2: float
     status: str
     exact: list = None   # per iteration, the device scalar slots at full precision (record_exact)
+    factorization: int = 1  # clrsdp_get_factorization at the end (an LU fallback adds its flag)
+    lu_switch: int = 0      # iteration whose loop body switched to LU (0: none)
 
 
 def _stage_groups(ph):
@@ -456,6 +458,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     t_after2 = None
     status = "maxiterations"
     exact = []
+    lu_switch = [0]
 
     timed = bool(getattr(dev, "timing", False))
 
@@ -470,6 +473,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
                 out("The Cholesky factorization of S or Q failed. We switch to the pivoted LU "
                     "decomposition (approx_lu!) for S and Q.")
             fact_seen = f
+            lu_switch[0] = lu_switch[0] or it
         if it > 2:
             phase[:] += np.array(st.phase_ms[:])
         elif testing and timed:  # MPMP.jl:899-920: the times of the first iterations
@@ -558,7 +562,8 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     res = (xf, Xf, yf, Yf, P, p, d, gap_nob0, ret_p, ret_d, t_total)
     if return_info:
         res = res + (RunInfo(it - 1, log, phase, t_total,
-                             (time.time() - t_after2) if t_after2 else 0.0, status, exact),)
+                             (time.time() - t_after2) if t_after2 else 0.0, status, exact,
+                             dev.factorization, lu_switch[0]),)
     if solver is None:
         dev.close()
     return res

@@ -64,6 +64,8 @@ def run(name, inst, iters, prec=None, tol=1e-9, params=None):
         "log": [{k: fmt(getattr(r, k)) for k in ("mu", "p_obj", "d_obj", "gap", "P_err", "p_err",
                                                   "d_err", "alpha_p", "alpha_d", "beta")}
                 for r in res.log],
+        "status": res.status,
+        "final": {"gap": fmt(res.gap), "p_obj": fmt(res.p_obj), "d_obj": fmt(res.d_obj)},
         "x": [fmt(v) for v in res.x],
         "y": [fmt(v) for v in res.y],
     }
@@ -76,6 +78,12 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "sp_real":  # real sphere-packing instance (~15 min)
         run("sp_real_d8_mp256", dict(kind="sphere_packing", n=3, d=8), 40, prec=256,
             params=dict(omega_p=100.0, omega_d=100.0, duality_gap_threshold=1e-30))
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "sp_real_full":  # to the reference's defaults (~40 min)
+        # SP.jl:110 passes no thresholds: solverank1sdp's defaults gap 1e-15, errors 1e-30
+        run("sp_real_d8_mp256_full", dict(kind="sphere_packing", n=3, d=8), 120, prec=256,
+            params=dict(omega_p=100.0, omega_d=100.0, duality_gap_threshold=1e-15,
+                        primal_error_threshold=1e-30, dual_error_threshold=1e-30))
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "sp":  # only the config-5-shape vector (~40 s)
         run("sp_mp256_seed1", dict(kind="sphere_packing_shape", seed=1), 12, prec=256)
