@@ -6,15 +6,15 @@ cluster, n_y = 128, fp64 -- SURVEY.md §8d "C3".  One step = one full predictor-
 iteration (MPMP.jl:755-887) on device-resident data.
 
 With --gpus N (one process per GPU, clusters balanced as MPMP.jl:425-465, the cross-cluster
-partials all-gathered over RCCL) the default is WEAK scaling: every GPU keeps one C3 shard of
-64 clusters, so the instance has J = 64 N clusters (n_y = 128 couples all of them) and `value` is
-N x its iterations/s, i.e. C3-shard iterations/s summed over the GPUs (at N = 1 exactly the C3
-iterations/s).  --scaling strong keeps J = 64 and shards it (8 clusters per GPU at N = 8); that
-regime is latency-bound by the per-block chains, so it is not the default.
+partials all-gathered over RCCL) the default is the configuration as BASELINE.json states it:
+the 64-cluster instance sharded over the N GPUs (STRONG scaling, 8 clusters per GPU at N = 8);
+`value` is the instance's iterations/s, the whole job's throughput.  --scaling weak gives every
+GPU a C3-sized shard (J = 64 N clusters coupled by n_y = 128); `value` is then that instance's
+iterations/s and `shard_iterations_per_s_summed` = N x value.
 
-Also reported: the Schur-assembly roofline (its kernels timed with HIP events on the library's
-stream over the timed region) and a CPU baseline (the numpy restatement of the reference
-algorithm in oracle/, one iteration of the same instance, rank 0 at N = 1 only).
+Also reported: the Schur-assembly roofline (its kernels timed on the device clock inside the
+timed region), and a CPU baseline: the C++/OpenMP restatement of the reference algorithm
+(oracle/cpu_restatement.cpp) at the bench's word type on the host's cores, rank 0 at N = 1.
 """
 from __future__ import annotations
 
@@ -65,9 +65,10 @@ def schur_flops_bytes(bi, word=8):
 
 
 def schur_pmc_traffic(config, precision, world):
-    """HBM bytes per iteration of the Schur stage (FETCH_SIZE + WRITE_SIZE of its two launches)
-    from the newest committed PMC summary, profiles/rNN_schur_pmc.json, written by
-    tools/profile_round.sh for the default C3 fp64 1-GPU run.  None for other runs."""
+    """HBM bytes per iteration of the Schur stage (FETCH_SIZE + WRITE_SIZE of its launches) from
+    the newest committed PMC summary, profiles/rNN_schur_pmc.json (tools/profile_round.sh, the
+    default C3 fp64 1-GPU run), used only when it was taken on this very build (its
+    source_hash); otherwise None and the source says why.  None for other runs."""
     import glob
     if config != "c3" or precision != 1 or world != 1:
         return None, None
@@ -76,46 +77,38 @@ def schur_pmc_traffic(config, precision, world):
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    return d.get("traffic_bytes_per_iteration"), os.path.relpath(files[-1], ROOT)
+    import _clrsdp_pkg
+    cur = _clrsdp_pkg.load_build().source_hash()
+    src = os.path.relpath(files[-1], ROOT)
+    if d.get("source_hash") != cur:
+        return None, (f"stale: {src} was counted on build {d.get('source_hash')}, this is build "
+                      f"{cur} (run tools/profile_round.sh)")
+    return d.get("traffic_bytes_per_iteration"), f"{src} (build {cur})"
 
 
-MP_BITS = {2: 106, 4: 212}   # significand bits of dd / qd, for the multi-precision CPU baseline
-MP_BASELINE_MAX_ELEMS = 20000  # mpmath is ~1 us per operation: small instances only (config 5)
-
-
-def cpu_baseline(cons, b, bi, precision=1, budget_s=20.0):
-    """Time the oracle on this instance: the numpy fp64 restatement of MPMP.jl, or for a
-    multi-word run on a small instance (config 5) the mpmath restatement at the significand
-    width of the device words (single-threaded, as mpmath is)."""
-    from oracle import mpmp_oracle as O
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
-    except Exception:
-        cores = 1
-    label = "numpy/scipy fp64 restatement (oracle/mpmp_oracle.py), BLAS threads=%d" % cores
-    ar = O.Fp64()
-    elems = sum(n * n for bl in bi.Y_blocksizes for n in bl) + sum(d * d for d in bi.dim_S)
-    if precision > 1 and elems <= MP_BASELINE_MAX_ELEMS:
-        ar = O.Mp(MP_BITS[precision])
-        cons = [O.Cluster([[[ar.asarray(v) for v in vk] for vk in Al] for Al in cl.A],
-                          ar.asarray(cl.B), ar.asarray(cl.c),
-                          [[[ar.num(x) for x in hk] for hk in Hl] for Hl in cl.H]) for cl in cons]
-        b = ar.asarray(b)
-        cores = 1
-        label = "mpmath restatement at %d bits (oracle/mpmp_oracle.py), 1 thread" % MP_BITS[precision]
-    prm = {k: O._param(ar, v) for k, v in O.DEFAULTS.items()}
-    state = O.initial_point(ar, bi, 100.0, 100.0)
-    t0 = time.time()
-    n = 0
-    while True:
-        state, _ = O.iteration(ar, cons, bi, b, None, ar.num(0), state, False, prm)
-        n += 1
-        if time.time() - t0 > budget_s * 0.5 or n >= 3:
-            break
-    dt = time.time() - t0
-    return {"value": n / dt, "unit": "iterations/s", "cores": int(cores), "kind": "port",
-            "sample": f"{n} loop bodies of the same instance from the initial point, {label}"}
+def cpu_baseline(pk, cons, b, bi, precision=1, budget_s=15.0):
+    """Time the C++/OpenMP restatement of the reference algorithm (oracle/cpu_restatement.cpp:
+    the same loop body as MPMP.jl:755-887 with approx_lu! for S_j and Q, threaded over the
+    reference's (j,l) and cluster partitions) on this instance at the bench's word type
+    (double, double-double, quad-double), on all the host threads OpenMP is given
+    (OMP_NUM_THREADS), from the reference's initial point: one calibration body, then as many
+    as fit in ~budget_s."""
+    from oracle import cpurest
+    cpurest.build()
+    threads = cpurest.max_threads()
+    st = pk.initial_point(bi, 100.0, 100.0)
+    rc, _, s1, st1 = cpurest.run(pk, cons, b, bi, precision, st, 1)
+    if rc != 1:
+        return {"value": None, "unit": "iterations/s", "cores": threads, "kind": "port",
+                "sample": f"the C++ restatement failed in its first loop body (code {rc})"}
+    n = int(max(1, min(30, budget_s / max(s1, 1e-3))))
+    rc, _, secs, _ = cpurest.run(pk, cons, b, bi, precision, st1, n)
+    n = max(rc, 0)
+    return {"value": n / secs if n else None, "unit": "iterations/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"{n} loop bodies (iterations 2..{n + 1}) of the same instance from the "
+                       f"reference's initial point; C++/OpenMP restatement of MPMP.jl's loop body "
+                       f"(oracle/cpu_restatement.cpp) at {DTYPES[precision]}, {threads} OpenMP threads")}
 
 
 def main():
@@ -133,9 +126,10 @@ def main():
                          "(pipelined; auto = pipelined when the clusters are sharded)")
     ap.add_argument("--clusters", type=int, default=0,
                     help="override J of the config (per-rank sizing experiments; not a bench line)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="N > 1: weak = one config-sized shard per GPU (J x N clusters), strong = "
-                         "the config's J sharded over the GPUs")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="N > 1: strong = the config's J sharded over the GPUs (BASELINE.json "
+                         "configs[2], the default), weak = one config-sized shard per GPU (J x N "
+                         "clusters)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -280,7 +274,7 @@ def main():
         dist.close()
         return
     its = args.steps / dt
-    value = its * world if weak else its
+    value = its   # the instance's loop bodies per second: the whole job's throughput
     fl, by = schur_flops_bytes(bi, 8 * args.precision)
     if world > 1:
         fl /= world   # per-rank share of the Schur work (the roofline is per GPU)
@@ -300,12 +294,13 @@ def main():
         "value": value,
         "unit": "iterations/s",
         "instance_iterations_per_s": its,
+        "shard_iterations_per_s_summed": its * world if weak else None,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak" if (weak or world == 1) else "strong",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": DTYPES[args.precision],
         "data": "synthetic (seeded splitmix64 instance, SURVEY.md §8d)",
@@ -314,9 +309,10 @@ def main():
                                if "J" in cfg else
                                f"{args.config}: sphere-packing shape, J={bi.J} clusters, blocks "
                                f"{bi.Y_blocksizes}, dim_S {bi.dim_S}, n_y={bi.n_y}",
-                   "parallelism": (f"{cfg['J'] // world} clusters per GPU on {world} GPUs (weak: "
-                                   f"value = {world} x instance iterations/s)" if weak else
-                                   f"clusters sharded over {world} GPU(s)") if world > 1 else "1 GPU"},
+                   "parallelism": (f"{cfg['J'] // world} clusters per GPU on {world} GPUs (weak: one "
+                                   f"C3-sized shard per GPU)" if weak else
+                                   f"{cfg['J']} clusters sharded over {world} GPUs (strong)")
+                                  if world > 1 else "1 GPU"},
         "roofline": {"bound": "mfma" if args.precision == 1 else "valu",
                      "kernel": "Schur assembly (stage SCHUR)",
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -337,7 +333,7 @@ def main():
                      if pipelined else "synchronous (one hipGraph replay per loop body)",
     }
     if world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(cons, b, bi, args.precision)
+        res["cpu_baseline"] = cpu_baseline(pk, cons, b, bi, args.precision)
     print(json.dumps(res), flush=True)
     dev.close()
     if dist is not None:

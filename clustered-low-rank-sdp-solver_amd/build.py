@@ -18,6 +18,17 @@ HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-mllvm", "-amdgpu-mfma-vgpr-form", "-ldl"]
 
 
+def source_hash() -> str:
+    """sha256 over the library's sources (csrc + the C ABI header): names the build a profile or
+    counter pass was taken on, so results of another build are recognised as stale."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in DEPS:
+        with open(d, "rb") as f:
+            h.update(os.path.basename(d).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and os.path.exists(OUT):
         t = os.path.getmtime(OUT)

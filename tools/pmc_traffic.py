@@ -43,6 +43,10 @@ def main():
         "kernels": {k: {"fetch_bytes": fetch.get(k), "fetch_bytes_x2": 2 * fetch.get(k, 0.0),
                         "write_bytes": write.get(k), "dispatches": nf.get(k)} for k in KERNELS},
     }
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import _clrsdp_pkg
+    res["source_hash"] = _clrsdp_pkg.load_build().source_hash()   # the build the counters saw
     res["traffic_bytes_per_iteration"] = sum(fetch.values()) + sum(write.values())
     res["traffic_bytes_per_iteration_fetch_x2"] = 2 * sum(fetch.values()) + sum(write.values())
     res["note"] = ("FETCH_SIZE at 8 B/lane is uncalibrated on gfx950 (MI355X_MICROARCH.md §HBM); "
