@@ -2028,6 +2028,11 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     const T v = fold_wave(p.red[q], lane);
     if (lane == 0) sc[p.red[q].dst] = v;
   }
+  // any status word set (which == 3): the wave reads them strided, one ballot
+  bool fl = false;
+  if (which == 3)
+    for (int e = lane; e < p.nguard; e += 64) fl = fl || p.guard[e] != 0;
+  const bool failed = __any(fl);
   if (lane != 0) return;
   const T dim = T(p.dim);
   if (which == 0) {  // mu, mu_p
@@ -2069,8 +2074,6 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     if (p.zero_cy) sc[SC_DOT_CY] = T(0.0);
     sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;
     sc[SC_DOBJ] = sc[SC_DOT_CY] + sc[SC_DOT_BY] + p.b0;
-    bool failed = false;
-    for (int e = 0; e < p.nguard; ++e) failed = failed || p.guard[e] != 0;
     if (!failed) control_update(sc, p, false);
   } else if (which == 4) {  // objectives + control of the initial point (MPMP.jl:723-736)
     if (p.zero_cy) sc[SC_DOT_CY] = T(0.0);
