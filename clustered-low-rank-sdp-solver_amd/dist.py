@@ -86,6 +86,34 @@ class TorchExchange:
             self.dist.destroy_process_group()
 
 
+class _Watchdog:
+    """Ends the process (exit status 3, with a message) if the guarded block has not finished in
+    `seconds` -- a communicator set-up whose peer never arrives blocks inside RCCL forever, and a
+    multi-GPU job must fail loudly instead of hanging (CLRSDP_COMM_TIMEOUT, default 180 s)."""
+
+    def __init__(self, what: str, rank: int, seconds: float = None):
+        self.what, self.rank = what, rank
+        self.seconds = float(os.environ.get("CLRSDP_COMM_TIMEOUT", "180")) if seconds is None else seconds
+
+    def __enter__(self):
+        import threading
+        self._done = threading.Event()
+
+        def watch():
+            if not self._done.wait(self.seconds):
+                import sys
+                print(f"[clrsdp rank {self.rank}] {self.what} did not finish within "
+                      f"{self.seconds:.0f} s: exiting", file=sys.stderr, flush=True)
+                os._exit(3)
+        self._t = threading.Thread(target=watch, daemon=True)
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._done.set()
+        return False
+
+
 class RcclExchange:
     """The default multi-GPU path: the library's own RCCL communicator (clrsdp_comm_init).
 
@@ -127,7 +155,8 @@ class RcclExchange:
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
         try:
-            dev.comm_init(bytes(t.tolist()))
+            with _Watchdog("RCCL communicator set-up (clrsdp_comm_init)", self.rank):
+                dev.comm_init(bytes(t.tolist()))
             ok = 1
         except Exception as e:   # e.g. "invalid usage": several ranks on one GPU
             print(f"[clrsdp rank {self.rank}] RCCL communicator failed: {e}", flush=True)
