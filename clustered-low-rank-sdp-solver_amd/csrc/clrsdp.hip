@@ -261,6 +261,49 @@ struct GemmPlan : PlanBase {
     }
     d = own(h);
     dt = own(t2d);
+    detect_uniform();
+  }
+  // fp64 batches of one shape at constant operand strides take gemm_f64_uni (no descriptor
+  // chain before the first operand load); CLRSDP_NO_UNI_GEMM keeps the descriptor kernels
+  bool uni = false;
+  UniGemm ug{};
+  void detect_uniform() {
+    if constexpr (std::is_same<T, double>::value) {
+      static const bool off = std::getenv("CLRSDP_NO_UNI_GEMM") != nullptr;
+      if (off || gemv || dyn || h.empty()) return;
+      const GemmDesc<T>& g0 = h[0];
+      auto stride = [&](auto get, long long& st) {
+        st = h.size() > 1 ? (long long)(get(h[1]) - get(h[0])) : 0;
+        for (size_t p = 1; p < h.size(); ++p)
+          if ((long long)(get(h[p]) - get(h[p - 1])) != st) return false;
+        return true;
+      };
+      for (const auto& g : h)
+        if (g.M != g0.M || g.N != g0.N || g.K != g0.K || g.lda != g0.lda || g.ldb != g0.ldb ||
+            g.ldc != g0.ldc || g.ldcin != g0.ldcin || (g.Cin == nullptr) != (g0.Cin == nullptr) ||
+            (g.sa == nullptr) != (g0.sa == nullptr))
+          return;
+      UniGemm u{};
+      bool ok = stride([](const GemmDesc<T>& g) { return g.A; }, u.sA) &&
+                stride([](const GemmDesc<T>& g) { return g.B; }, u.sB) &&
+                stride([](const GemmDesc<T>& g) { return (const T*)g.C; }, u.sC);
+      if (g0.Cin) ok = ok && stride([](const GemmDesc<T>& g) { return g.Cin; }, u.sCin);
+      if (g0.sa) ok = ok && stride([](const GemmDesc<T>& g) { return g.sa; }, u.sSa) &&
+                      stride([](const GemmDesc<T>& g) { return g.sl; }, u.sSl);
+      if (!ok) return;
+      u.A = g0.A; u.B = g0.B; u.Cin = g0.Cin; u.C = g0.C; u.sa = g0.sa; u.sl = g0.sl;
+      u.M = g0.M; u.N = g0.N; u.K = g0.K; u.lda = g0.lda; u.ldb = g0.ldb; u.ldcin = g0.ldcin;
+      u.ldc = g0.ldc; u.tn = g0.tn; u.P = (int)h.size();
+      const int tm = (int)cdiv(g0.M, TILE);
+      u.tsym = tm * (tm + 1) / 2;
+      ug = u;
+      uni = true;
+    }
+  }
+  template <class U = T>
+  void launch_uni_impl(hipStream_t s, double alpha, double beta, const double* ds, double dmult) const;
+  void launch_uni(hipStream_t s, double alpha, double beta, const double* ds, double dmult) const {
+    launch_uni_impl<T>(s, alpha, beta, ds, dmult);
   }
   // C = alpha op(A) op(B) + beta Cin (+ dmult * *dscal on the diagonal of square problems)
   void launch(hipStream_t s, double alpha, double beta, const T* dscal = nullptr,
@@ -277,6 +320,10 @@ struct GemmPlan : PlanBase {
     }
     if constexpr (std::is_same<T, double>::value) {
       const double* ds = reinterpret_cast<const double*>(dscal);
+      if (uni) {
+        launch_uni(s, alpha, beta, ds, dmult);
+        return;
+      }
       if (sca) {
         gemm_f64_lds<false, true, 0, 32, 8, false, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
         HIPCHK(hipGetLastError());
@@ -310,6 +357,32 @@ struct GemmPlan : PlanBase {
     HIPCHK(hipGetLastError());
   }
 };
+
+template <class T>
+template <class U>
+void GemmPlan<T>::launch_uni_impl(hipStream_t s, double alpha, double beta, const double* ds, double dmult) const {
+  if constexpr (std::is_same<T, double>::value) {
+    const UniGemm& u = ug;
+    if (sca) {
+      gemm_f64_uni<false, true, 0, 32, 8, false, true><<<(unsigned)(u.P * (int)cdiv(u.M, 64) * u.tn), 512, 0, s>>>(u, alpha, beta, ds, dmult);
+    } else if (sym) {
+      if (beta != 0.0 || ds) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: beta = 0 only"};
+      const unsigned grid = (unsigned)(u.P * u.tsym);
+      if (!ta && tb) gemm_f64_uni<false, true, 0, 32, 8, true><<<grid, 512, 0, s>>>(u, alpha, 0.0);
+      else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, 8, true><<<grid, 512, 0, s>>>(u, alpha, 0.0);
+      else throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: op(A) = A only"};
+    } else {
+      const unsigned grid = (unsigned)(u.P * (int)cdiv(u.M, 64) * u.tn);
+      if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+      else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+      else if (!ta && !tb) gemm_f64_uni<false, false><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+      else if (ta && !tb) gemm_f64_uni<true, false><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+      else if (!ta && tb) gemm_f64_uni<false, true><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+      else gemm_f64_uni<true, true><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+    }
+    HIPCHK(hipGetLastError());
+  }
+}
 
 template <class T>
 struct TrsmPlan : PlanBase {

@@ -266,6 +266,59 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_lds(const GemmDesc<double>* 
     }
 }
 
+// Uniform batch: every problem has the same shape and leading dimensions, and problem p's
+// operands sit at a fixed stride from problem 0's (the block and cluster arenas).  The batch is
+// passed by value in the kernel arguments, and workgroup b takes tile b / P of problem b % P
+// (tile-major, problem fastest, as tile_major()), so no descriptor or tile table is read before
+// the first operand load (the t2d -> desc -> operands chain cost ~2 us per launch).
+struct UniGemm {
+  const double* A;
+  const double* B;
+  const double* Cin;
+  double* C;
+  const double* sa;
+  const double* sl;
+  long long sA, sB, sCin, sC, sSa, sSl;  // per-problem strides (elements)
+  int M, N, K, lda, ldb, ldcin, ldc, tn, P, tsym;  // tsym: SYM, lower tiles per problem
+};
+// lower tile q (row-major over the lower triangle) -> (tm, tn)
+__device__ inline void lower_tile(int q, int& tm, int& tn) {
+  tm = 0;
+  while ((tm + 1) * (tm + 2) / 2 <= q) ++tm;
+  tn = q - tm * (tm + 1) / 2;
+}
+template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false, bool SCA = false>
+__global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double alpha, double beta,
+                                                        const double* __restrict__ dscal = nullptr,
+                                                        double dmult = 0.0,
+                                                        unsigned long long* stamp = nullptr) {
+  if constexpr (TAG == 1 || TAG == 3)
+    if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  __shared__ double smem[gemm_f64_smem<BK, NW>()];
+  const int p = blockIdx.x % u.P, q = blockIdx.x / u.P;
+  GemmDesc<double> d;
+  d.A = u.A + p * u.sA;
+  d.B = u.B + p * u.sB;
+  d.Cin = u.Cin ? u.Cin + p * u.sCin : nullptr;
+  d.C = u.C + p * u.sC;
+  d.M = u.M; d.N = u.N; d.K = u.K;
+  d.lda = u.lda; d.ldb = u.ldb; d.ldcin = u.ldcin; d.ldc = u.ldc; d.tn = u.tn;
+  d.sa = SCA ? u.sa + p * u.sSa : nullptr;
+  d.sl = SCA ? u.sl + p * u.sSl : nullptr;
+  int t = q;
+  if constexpr (SYM) {
+    int tm, tc;
+    lower_tile(q, tm, tc);
+    t = tm * u.tn + tc;
+  }
+  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA>(d, t, smem, alpha, beta, dscal, dmult);
+  if constexpr (TAG == 1 || TAG == 3)
+    if (stamp) {
+      __syncthreads();
+      if (threadIdx.x == 0) atomicMax(stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+}
+
 // Mixed batch: op(A), op(B) and (flags bit 2) alpha/beta per problem, so independent products of
 // different shapes share one launch (one uniform branch per workgroup picks the instantiation).
 template <int BK = 32, int NW = 8>
