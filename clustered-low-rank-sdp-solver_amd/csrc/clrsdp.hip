@@ -358,29 +358,40 @@ struct GemmPlan : PlanBase {
   }
 };
 
+template <bool DB>
+void launch_uni_db(const UniGemm& u, hipStream_t s, bool ta, bool tb, bool sca, bool sym, int tag,
+                   unsigned long long* stamp, double alpha, double beta, const double* ds, double dmult) {
+  if (sca) {
+    gemm_f64_uni<false, true, 0, 32, 8, false, true, DB><<<(unsigned)(u.P * (int)cdiv(u.M, 64) * u.tn), 512, 0, s>>>(u, alpha, beta, ds, dmult);
+  } else if (sym) {
+    if (beta != 0.0 || ds) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: beta = 0 only"};
+    const unsigned grid = (unsigned)(u.P * u.tsym);
+    if (!ta && tb) gemm_f64_uni<false, true, 0, 32, 8, true, false, DB><<<grid, 512, 0, s>>>(u, alpha, 0.0);
+    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, 8, true, false, DB><<<grid, 512, 0, s>>>(u, alpha, 0.0);
+    else throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: op(A) = A only"};
+  } else {
+    const unsigned grid = (unsigned)(u.P * (int)cdiv(u.M, 64) * u.tn);
+    if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+    else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+    else if (ta && !tb) gemm_f64_uni<true, false, 0, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+    else if (!ta && tb) gemm_f64_uni<false, true, 0, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+    else gemm_f64_uni<true, true, 0, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+  }
+  HIPCHK(hipGetLastError());
+}
+
 template <class T>
 template <class U>
 void GemmPlan<T>::launch_uni_impl(hipStream_t s, double alpha, double beta, const double* ds, double dmult) const {
   if constexpr (std::is_same<T, double>::value) {
-    const UniGemm& u = ug;
-    if (sca) {
-      gemm_f64_uni<false, true, 0, 32, 8, false, true><<<(unsigned)(u.P * (int)cdiv(u.M, 64) * u.tn), 512, 0, s>>>(u, alpha, beta, ds, dmult);
-    } else if (sym) {
-      if (beta != 0.0 || ds) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: beta = 0 only"};
-      const unsigned grid = (unsigned)(u.P * u.tsym);
-      if (!ta && tb) gemm_f64_uni<false, true, 0, 32, 8, true><<<grid, 512, 0, s>>>(u, alpha, 0.0);
-      else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, 8, true><<<grid, 512, 0, s>>>(u, alpha, 0.0);
-      else throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: op(A) = A only"};
-    } else {
-      const unsigned grid = (unsigned)(u.P * (int)cdiv(u.M, 64) * u.tn);
-      if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
-      else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
-      else if (!ta && !tb) gemm_f64_uni<false, false><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
-      else if (ta && !tb) gemm_f64_uni<true, false><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
-      else if (!ta && tb) gemm_f64_uni<false, true><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
-      else gemm_f64_uni<true, true><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
-    }
-    HIPCHK(hipGetLastError());
+    // CLRSDP_UNI_DB=0: single-buffered slabs (two barriers per k-step), for A/B timing
+    static const bool db = [] {
+      const char* e = std::getenv("CLRSDP_UNI_DB");
+      return !(e && e[0] == '0');
+    }();
+    if (db) launch_uni_db<true>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
+    else launch_uni_db<false>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
   }
 }
 

@@ -121,15 +121,18 @@ __device__ inline int acc_col(int wn, int ni, int lr, int wcols = 32) { return w
 // SYM: square problems whose product is symmetric in exact arithmetic (L^-1 dM L^-T): the launch
 // covers the lower tiles only, each writes its tile and the mirror image, and a diagonal tile
 // mirrors its lower triangle -- the result is exactly symmetric (beta = 0, no diagonal term).
-template <int BK, int NW>
+template <int BK, int NW, bool DB = false>
 constexpr int gemm_f64_smem() {
-  return 2 * lds_gemm::Slab<BK, 64 * NW>::SZ > 64 * lds_gemm::TP ? 2 * lds_gemm::Slab<BK, 64 * NW>::SZ
-                                                                 : 64 * lds_gemm::TP;
+  return (DB ? 4 : 2) * lds_gemm::Slab<BK, 64 * NW>::SZ > 64 * lds_gemm::TP
+             ? (DB ? 4 : 2) * lds_gemm::Slab<BK, 64 * NW>::SZ
+             : 64 * lds_gemm::TP;
 }
 // one 64x64 output tile t of problem d (the body of every fp64 GEMM launch)
 // SCA (op(A) = A only): A(i, k) * (sa[k] * sl[k]) -- compute_weighted_A's V diag(x lambda)
 // (MPMP.jl:1659) formed while the slab is staged, with scale_cols's operation order
-template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false>
+// DB: double-buffered slabs (two LDS images per operand): the next slab is stored into the
+// other image while no wave reads it, so each k-step needs one barrier instead of two
+template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false, bool DB = false>
 __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, double* smem,
                                               double alpha, double beta,
                                               const double* __restrict__ dscal, double dmult) {
@@ -178,6 +181,7 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
   SL::template store<AK>(ra, As, tid, 0, K);
   SL::template store<BKc>(rb, Bs, tid, 0, K);
   __syncthreads();
+  int cur = 0;
   for (int k0 = 0; k0 < K; k0 += BK) {
     const bool more = k0 + BK < K;
     if (more) {
@@ -185,13 +189,15 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
       SL::template load<BKc>(rb, d.B, d.ldb, n0, N, k0 + BK, K, tid);
       load_w(k0 + BK);
     }
+    const double* Ac = DB ? smem + cur * 2 * SL::SZ : As;
+    const double* Bc = DB ? smem + cur * 2 * SL::SZ + SL::SZ : Bs;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       double af[2], bf[NI];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) af[mi] = SL::template frag<AK>(As, wm * 32 + mi * 16 + lr, kk + lk);
+      for (int mi = 0; mi < 2; ++mi) af[mi] = SL::template frag<AK>(Ac, wm * 32 + mi * 16 + lr, kk + lk);
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) bf[ni] = SL::template frag<BKc>(Bs, wn * WC + ni * 16 + lr, kk + lk);
+      for (int ni = 0; ni < NI; ++ni) bf[ni] = SL::template frag<BKc>(Bc, wn * WC + ni * 16 + lr, kk + lk);
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -199,11 +205,20 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
           acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
     }
     if (!more) break;
-    __syncthreads();
-    scale_a();
-    SL::template store<AK>(ra, As, tid, k0 + BK, K);
-    SL::template store<BKc>(rb, Bs, tid, k0 + BK, K);
-    __syncthreads();
+    if constexpr (DB) {
+      // the other image was last read before the previous barrier
+      cur ^= 1;
+      scale_a();
+      SL::template store<AK>(ra, smem + cur * 2 * SL::SZ, tid, k0 + BK, K);
+      SL::template store<BKc>(rb, smem + cur * 2 * SL::SZ + SL::SZ, tid, k0 + BK, K);
+      __syncthreads();
+    } else {
+      __syncthreads();
+      scale_a();
+      SL::template store<AK>(ra, As, tid, k0 + BK, K);
+      SL::template store<BKc>(rb, Bs, tid, k0 + BK, K);
+      __syncthreads();
+    }
   }
   __syncthreads();  // LDS slabs -> output tile
 #pragma unroll
@@ -287,14 +302,15 @@ __device__ inline void lower_tile(int q, int& tm, int& tn) {
   while ((tm + 1) * (tm + 2) / 2 <= q) ++tm;
   tn = q - tm * (tm + 1) / 2;
 }
-template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false, bool SCA = false>
+template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false, bool SCA = false,
+          bool DB = true>
 __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double alpha, double beta,
                                                         const double* __restrict__ dscal = nullptr,
                                                         double dmult = 0.0,
                                                         unsigned long long* stamp = nullptr) {
   if constexpr (TAG == 1 || TAG == 3)
     if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-  __shared__ double smem[gemm_f64_smem<BK, NW>()];
+  __shared__ double smem[gemm_f64_smem<BK, NW, DB>()];
   const int p = blockIdx.x % u.P, q = blockIdx.x / u.P;
   GemmDesc<double> d;
   d.A = u.A + p * u.sA;
@@ -311,7 +327,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double 
     lower_tile(q, tm, tc);
     t = tm * u.tn + tc;
   }
-  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA>(d, t, smem, alpha, beta, dscal, dmult);
+  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA, DB>(d, t, smem, alpha, beta, dscal, dmult);
   if constexpr (TAG == 1 || TAG == 3)
     if (stamp) {
       __syncthreads();
