@@ -188,6 +188,20 @@ def test_full_run_matches_golden(pk, name, words, tol):
             r = mpmath.mpf(ref[key])
             v = mpmath.mpf(sc[slot])
             assert abs(v - r) <= tol * max(1, abs(r)), (it + 1, key, float(v), float(r))
+        # the objectives after this iteration's update are the next log row's (MPMP.jl:940-941)
+        if it + 1 < len(g["log"]):
+            for key in ("p_obj", "d_obj"):
+                r = mpmath.mpf(g["log"][it + 1][key])
+                v = mpmath.mpf(sc[key])
+                assert abs(v - r) <= tol * max(1, abs(r)), (it + 1, key, float(v), float(r))
+    # the returned gap and objectives of the final state (MPMP.jl:1021-1023), at the state's
+    # precision when words > 1 (mpmath numbers, not leading limbs)
+    if "final" in g and len(info.exact) == len(g["log"]):
+        if words > 1:
+            assert all(isinstance(v, mpmath.mpf) for v in res[7:10])
+        for v, key in zip(res[7:10], ("gap", "p_obj", "d_obj")):
+            r = mpmath.mpf(g["final"][key])
+            assert abs(mpmath.mpf(v) - r) <= tol * max(1, abs(r)), (key, float(v), float(r))
 
 
 def test_known_answer_polynomial_minimum_gpu(pk):
