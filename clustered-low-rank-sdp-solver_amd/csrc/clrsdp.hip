@@ -463,11 +463,43 @@ struct MatPlan : PlanBase {  // potrf / eigmin
     h.push_back(m);
     nmax = std::max(nmax, n);
   }
+  // multi-word Cholesky factors of blocks with n <= 64: the register-resident chol_inv_reg
+  // (1024 threads, the whole block on chip, two barriers per column) writes L in place, its
+  // L^-1 goes to scratch -- against potrf_batched's 16-column panels with a serial pivot chain
+  // (C5: 600 us per launch for dim 51/52 at quad-double).  Set before finalize().
+  bool reg_potrf = false;
+  MatDesc<T>* d_scr = nullptr;
   void finalize() {
-    if (!h.empty()) d = own(h);
+    if (h.empty()) return;
+    d = own(h);
+    if constexpr (!std::is_same<T, double>::value) {
+      reg_potrf = reg_potrf && nmax <= 64 && !std::getenv("CLRSDP_NO_REG_POTRF");
+      if (reg_potrf) {
+        size_t tot = 0;
+        for (const auto& m : h) tot += (size_t)m.n * m.n;
+        T* scr = dmalloc<T>(tot);
+        owned_dev.push_back(scr);
+        std::vector<MatDesc<T>> sd;
+        size_t off = 0;
+        for (const auto& m : h) {
+          sd.push_back(MatDesc<T>{scr + off, m.n, m.n});
+          off += (size_t)m.n * m.n;
+        }
+        d_scr = own(sd);
+      }
+    } else {
+      reg_potrf = false;
+    }
   }
   void potrf(hipStream_t s, int* info) const {
     if (h.empty()) return;
+    if constexpr (!std::is_same<T, double>::value) {
+      if (reg_potrf) {
+        chol_inv_reg<T, 1, 4, 64, 16><<<(unsigned)h.size(), 1024, 0, s>>>(d, d_scr, d, info);
+        HIPCHK(hipGetLastError());
+        return;
+      }
+    }
     const size_t lds = sizeof(T) * ((size_t)NB * NB + (size_t)NB * nmax);
     // double-double: 1024 threads, so the trailing update (VALU bound) has four waves per SIMD
     // (C4 factor stage 806 -> 724 us); quad-double keeps 256 (its registers, 3 % slower at 1024)
@@ -1212,6 +1244,7 @@ struct Solver final : HandleBase {
     e_XY.finalize();
     for (TrsmPlan<T>* t : {&t_Linv, &t_W, &t_t, &t_Q, &t_sX1, &t_sX2, &t_sY1, &t_sY2, &t_dx})
       t->finalize();
+    for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q}) f->reg_potrf = true;
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q, &e_X, &e_Y}) f->finalize();
   }
 
