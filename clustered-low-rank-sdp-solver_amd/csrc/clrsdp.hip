@@ -464,38 +464,21 @@ struct MatPlan : PlanBase {  // potrf / eigmin
     nmax = std::max(nmax, n);
   }
   // multi-word Cholesky factors of blocks with n <= 64: the register-resident chol_inv_reg
-  // (1024 threads, the whole block on chip, two barriers per column) writes L in place, its
-  // L^-1 goes to scratch -- against potrf_batched's 16-column panels with a serial pivot chain
-  // (C5: 600 us per launch for dim 51/52 at quad-double).  Set before finalize().
+  // without the inverse (1024 threads, the whole block on chip, two barriers per column) writes
+  // L in place -- against potrf_batched's 16-column panels with a serial pivot chain.  Set
+  // before finalize(); CLRSDP_REG_POTRF=0 keeps potrf_batched.
   bool reg_potrf = false;
-  MatDesc<T>* d_scr = nullptr;
   void finalize() {
     if (h.empty()) return;
     d = own(h);
-    if constexpr (!std::is_same<T, double>::value) {
-      reg_potrf = reg_potrf && nmax <= 64 && !std::getenv("CLRSDP_NO_REG_POTRF");
-      if (reg_potrf) {
-        size_t tot = 0;
-        for (const auto& m : h) tot += (size_t)m.n * m.n;
-        T* scr = dmalloc<T>(tot);
-        owned_dev.push_back(scr);
-        std::vector<MatDesc<T>> sd;
-        size_t off = 0;
-        for (const auto& m : h) {
-          sd.push_back(MatDesc<T>{scr + off, m.n, m.n});
-          off += (size_t)m.n * m.n;
-        }
-        d_scr = own(sd);
-      }
-    } else {
-      reg_potrf = false;
-    }
+    const char* e = std::getenv("CLRSDP_REG_POTRF");
+    reg_potrf = reg_potrf && !std::is_same<T, double>::value && nmax <= 64 && !(e && e[0] == '0');
   }
   void potrf(hipStream_t s, int* info) const {
     if (h.empty()) return;
     if constexpr (!std::is_same<T, double>::value) {
       if (reg_potrf) {
-        chol_inv_reg<T, 1, 4, 64, 16><<<(unsigned)h.size(), 1024, 0, s>>>(d, d_scr, d, info);
+        chol_inv_reg<T, 1, 4, 64, 16, false><<<(unsigned)h.size(), 1024, 0, s>>>(d, d, d, info);
         HIPCHK(hipGetLastError());
         return;
       }

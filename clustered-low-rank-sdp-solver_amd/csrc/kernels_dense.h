@@ -49,7 +49,8 @@ __device__ T block_sum_w(T v, T* red) {
 // column is scaled by the reciprocal of the pivot, formed once by the pivot's owner.
 // In-place safe (out == A): every thread reads its own tile before anything is written.
 // ------------------------------------------------------------------------------------------
-template <class T, int TR, int TC, int GR, int GC>
+// INV = false: the Cholesky factor only (out_l, in place allowed; out_inv unused)
+template <class T, int TR, int TC, int GR, int GC, bool INV = true>
 __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __restrict__ in,
                                                         const MatDesc<T>* __restrict__ out_inv,
                                                         const MatDesc<T>* __restrict__ out_l,
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
         }
       }
     }
-    if (tr == j / TR) {
+    if (INV && tr == j / TR) {
 #pragma unroll
       for (int i = 0; i < TR; ++i) {
         if (i == jr) {
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
           }
         }
       }
-      if (c0 <= j) {
+      if (INV && c0 <= j) {
 #pragma unroll
         for (int c = 0; c < TC; ++c) {
           const T rc = row[c0 + c];
@@ -155,14 +156,16 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
     __syncthreads();
   }
   if (t == 0 && info) info[blockIdx.x] = fail;
-  const MatDesc<T> o = out_inv[blockIdx.x];
+  if (INV) {
+    const MatDesc<T> o = out_inv[blockIdx.x];
 #pragma unroll
-  for (int i = 0; i < TR; ++i)
+    for (int i = 0; i < TR; ++i)
 #pragma unroll
-    for (int c = 0; c < TC; ++c) {
-      const int gi = r0 + i, gc = c0 + c;
-      if (gi < n && gc < n) o.A[gi + (size_t)gc * o.lda] = x[i][c];
-    }
+      for (int c = 0; c < TC; ++c) {
+        const int gi = r0 + i, gc = c0 + c;
+        if (gi < n && gc < n) o.A[gi + (size_t)gc * o.lda] = x[i][c];
+      }
+  }
   if (out_l) {
     const MatDesc<T> ol = out_l[blockIdx.x];
 #pragma unroll
