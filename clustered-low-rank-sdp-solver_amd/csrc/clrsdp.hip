@@ -499,6 +499,15 @@ struct MatPlan : PlanBase {  // potrf / eigmin
         return;
       }
     }
+    // multi-word: eigmin_lds2 (two barriers per column) unless CLRSDP_EIG_LDS1=1
+    static const bool lds1 = std::getenv("CLRSDP_EIG_LDS1") != nullptr;
+    if (!std::is_same<T, double>::value && !lds1 && eig2_lds_bytes<T>(nmax) <= LDS_MAX) {
+      static std::atomic<unsigned long long> attr2{0};
+      lds_attr_once(attr2, (const void*)eigmin_lds2<T, true>, (int)LDS_MAX);
+      eigmin_lds2<T, true><<<(unsigned)h.size(), 512, eig2_lds_bytes<T>(nmax), s>>>(d, out);
+      HIPCHK(hipGetLastError());
+      return;
+    }
     if (eig_lds_bytes<T>(nmax) <= LDS_MAX) {
       const size_t lds = eig_lds_bytes<T>(nmax);
       static std::atomic<unsigned long long> attr_t{0}, attr_f{0};

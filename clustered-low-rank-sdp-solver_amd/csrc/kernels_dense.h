@@ -788,6 +788,190 @@ __device__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict
   return neg;
 }
 
+// the multi-word count >= 1 tests (CLRSDP_EIG_PIVOT_COUNT: the pivot form, for A/B timing)
+#ifdef CLRSDP_EIG_PIVOT_COUNT
+#define ANY_BELOW(sg) (sturm_count(dg, e2, n, (sg)) >= 1)
+#else
+#define ANY_BELOW(sg) sturm_any_below_mw(dg, e2, n, (sg))
+#endif
+// The multisection phase of eigmin_lds / eigmin_lds2 (512 threads): lambda_min of the
+// tridiagonal (dg, e2 = squared off-diagonals) in LDS to the word's precision, into
+// out[blockIdx.x].  A is LDS scratch (>= 2n + 14 doubles), Wv one word of LDS scratch.
+template <class T, bool NEWTON>
+__device__ void eig_multisection(const T* __restrict__ dg, const T* __restrict__ e2, int n,
+                                 T* __restrict__ A, T* __restrict__ Wv, T* __restrict__ out) {
+  constexpr int NT = 512, NW = 8;
+  const int tid = threadIdx.x;
+  if (n == 1) {
+    if (tid == 0) out[blockIdx.x] = dg[0];
+    return;
+  }
+  // ---- multisection, 256-way on waves 0-3 (8 bits per round), in two phases:
+  //  (1) fp64 on the leading limbs of the tridiagonal: Gershgorin bracket, 8 rounds;
+  //  (2) multi-word, started from the fp64 eigenvalue +- delta, where delta bounds the effect of
+  //      the rounding to fp64 (Weyl: |dlambda| <= ||dT|| <= ~3 eps64 ||T||) and of the fp64 Sturm
+  //      counts (exact for a matrix perturbed by a few eps64 relative), with a wide margin.  The
+  //      bracket is checked with two multi-word counts (no eigenvalue below it, one below its top)
+  //      and replaced by the Gershgorin bracket if the check fails.  About half the multi-word
+  //      rounds of a multisection from the Gershgorin bracket.
+  // The matrix image in LDS is no longer needed: it holds the fp64 copy and the round masks.
+  double* dgh = reinterpret_cast<double*>(A);
+  double* e2h = dgh + n;
+  double* bnd = e2h + n;  // [0,1] Gershgorin bracket, [2,3] multi-word start bracket, [4] ok
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(bnd + 6);
+  for (int i = tid; i < n; i += NT) {
+    dgh[i] = Num<T>::hi(dg[i]);
+    e2h[i] = Num<T>::hi(e2[i]);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double glo = 0.0, ghi = 0.0;
+    for (int i = 0; i < n; ++i) {
+      double r = 0.0;
+      if (i > 0) r += sqrt(e2h[i - 1]);
+      if (i + 1 < n) r += sqrt(e2h[i]);
+      const double a = dgh[i] - r, b = dgh[i] + r;
+      if (i == 0 || a < glo) glo = a;
+      if (i == 0 || b > ghi) ghi = b;
+    }
+    // the leading limbs and the fp64 sqrt differ from the exact bounds by ~eps64 relative
+    const double span = ghi - glo, mag = fmax(fabs(glo), fabs(ghi));
+    bnd[0] = glo - span * 1e-3 - mag * 1e-12 - 1e-300;
+    bnd[1] = ghi + span * 1e-3 + mag * 1e-12 + 1e-300;
+  }
+  __syncthreads();
+  const int w = tid >> 6, lane = tid & 63;
+  // one 512-way round: the first of the 512 interior points with a count >= 1 (every thread
+  // gets the same answer); returns its index, or -1 if none
+  auto first_hit = [&](bool hit) -> int {
+    const unsigned long long mk = __ballot(hit);
+    if (lane == 0) masks[w] = mk;
+    __syncthreads();
+    int f = -1;
+    for (int q = 0; q < NW && f < 0; ++q)
+      if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
+    __syncthreads();
+    return f;
+  };
+  {
+    // 8 rounds of 256 division-free counts on waves 0-3 (64 bits of the Gershgorin span)
+    double lo = bnd[0], hi = bnd[1];
+    for (int it = 0; it < 8; ++it) {
+      const double width = hi - lo;
+      bool hit = false;
+      if (tid < 256) hit = sturm_any_below_mw(dgh, e2h, n, lo + width * ((double)(tid + 1) / 257.0));
+      const int f = first_hit(hit);
+      if (f < 0) {
+        lo = lo + width * (256.0 / 257.0);
+      } else {
+        hi = lo + width * ((double)(f + 1) / 257.0);
+        if (f > 0) lo = lo + width * ((double)f / 257.0);
+      }
+    }
+    if (tid == 0) {
+      const double c = 0.5 * (lo + hi);
+      const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
+      const double delta = 64.0 * (double)n * 2.3e-16 * mag + (hi - lo) + 1e-300;
+      bnd[2] = c - delta;
+      bnd[3] = c + delta;
+    }
+  }
+  __syncthreads();
+  if constexpr (NEWTON && Num<T>::BITS > 120) {
+    // (2') quad-double: Newton on det(T - sigma I) from the fp64 centre (at dd the 11 parallel
+    // multisection rounds are as fast as the sequential Newton chain, so dd keeps them).  With the pivots of
+    // T - sigma I = L D L^T, q_i = (d_i - sigma) - e2_{i-1} / q_{i-1}, and s_i = dq_i/dsigma =
+    // -1 + e2_{i-1} s_{i-1} / q_{i-1}^2, the Newton step is 1 / sum_i s_i / q_i.  It converges
+    // quadratically from the fp64 estimate (3 steps for a simple eigenvalue, a 4th confirms).
+    // The result is accepted only if it converged AND two multi-word Sturm counts bracket it
+    // (no eigenvalue below sigma - delta, one at most sigma + delta, delta = 2^(12-BITS)
+    // magnitudes); otherwise the multisection below runs as before.
+    T* nres = Wv;  // free after the reduction: [0] = sigma
+    const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
+    if (tid == 0) {
+      T s = T(0.5 * (bnd[2] + bnd[3]));
+      const double tol = ldexp(mag, -(Num<T>::BITS + 2)) + 1e-300;
+      int conv = 0;
+      for (int it = 0; it < 4; ++it) {
+        T q = dg[0] - s;
+        if (q == T(0.0)) q = T(1e-300);
+        T r = T(1.0) / q, sd = T(-1.0), g = -r;
+        for (int i = 1; i < n; ++i) {
+          const T t = e2[i - 1] * r;
+          sd = (t * r) * sd - T(1.0);
+          q = (dg[i] - s) - t;
+          if (q == T(0.0)) q = T(1e-300);
+          r = T(1.0) / q;
+          g = g + sd * r;
+        }
+        const T step = T(1.0) / g;
+        s = s - step;
+        const double as = fabs(Num<T>::hi(step));
+        if (!(as == as)) break;  // NaN: leave conv = 0
+        if (as <= tol) { conv = 1; break; }
+      }
+      nres[0] = s;
+      masks[2] = (unsigned long long)conv;
+    }
+    __syncthreads();
+    const T s = nres[0];
+    const T dl = T(ldexp(mag, 12 - Num<T>::BITS) + 1e-300);
+    int c = 0;
+    if (tid == 0) c = masks[2] && !ANY_BELOW(s - dl);
+    if (tid == 64) c = ANY_BELOW(s + dl);
+    __syncthreads();
+    if (tid == 0 || tid == 64) masks[tid >> 6] = (unsigned long long)c;
+    __syncthreads();
+    const bool ok = masks[0] && masks[1];
+    __syncthreads();
+    if (ok) {
+      if (tid == 0) out[blockIdx.x] = s;
+      return;
+    }
+  }
+  T lo = T(bnd[2]), hi = T(bnd[3]);
+  // check the start bracket at full width: count(lo) == 0 and count(hi) >= 1
+  {
+    int c = 0;
+    if (tid == 0) c = !ANY_BELOW(lo);
+    if (tid == 64) c = ANY_BELOW(hi);
+    if (tid == 0 || tid == 64) masks[tid >> 6] = (unsigned long long)c;
+    __syncthreads();
+    const bool ok = masks[0] && masks[1];
+    __syncthreads();
+    if (!ok) {
+      lo = T(bnd[0]);
+      hi = T(bnd[1]);
+    }
+    // rounds to shrink the bracket to ~2^-BITS of the spectrum's magnitude.  The multi-word
+    // counts are VALU-issue bound, so they run 256-way on waves 0-3 (one wave per SIMD: 8 bits
+    // per round) rather than 512-way on two waves per SIMD (9 bits per round at twice the issue)
+#ifdef CLRSDP_EIG_MW512
+    constexpr int MS = 512, MB = 9;
+#else
+    constexpr int MS = 256, MB = 8;
+#endif
+    constexpr double MD = MS + 1.0;
+    const int rounds = ok ? (Num<T>::BITS - 25) / MB + 2 : Num<T>::BITS / MB + 3;
+    for (int it = 0; it < rounds; ++it) {
+      const T width = hi - lo;
+      bool hit = false;
+      if (tid < MS) {  // wave-uniform
+        const T sigma = lo + width * T((double)(tid + 1) / MD);
+        hit = ANY_BELOW(sigma);
+      }
+      const int f = first_hit(hit);
+      if (f < 0) {
+        lo = lo + width * T((double)MS / MD);
+      } else {
+        hi = lo + width * T((double)(f + 1) / MD);
+        if (f > 0) lo = lo + width * T((double)f / MD);
+      }
+    }
+  }
+  if (tid == 0) out[blockIdx.x] = (lo + hi) * T(0.5);
+}
+
 template <class T, bool NEWTON = true>
 __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__ descs,
                                                   T* __restrict__ out) {
@@ -795,12 +979,6 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
   constexpr int NT = 512, NW = 8;
-  // the multi-word count >= 1 tests (CLRSDP_EIG_PIVOT_COUNT: the pivot form, for A/B timing)
-#ifdef CLRSDP_EIG_PIVOT_COUNT
-#define ANY_BELOW(sg) (sturm_count(dg, e2, n, (sg)) >= 1)
-#else
-#define ANY_BELOW(sg) sturm_any_below_mw(dg, e2, n, (sg))
-#endif
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const MatDesc<T> d = descs[blockIdx.x];
   const int n = d.n, tid = threadIdx.x;
@@ -926,177 +1104,174 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
     }
   }
   __syncthreads();
+  eig_multisection<T, NEWTON>(dg, e2, n, A, Wv, out);
+  EIG_STAMP(6)
+}
+
+// ------------------------------------------------------------------------------------------
+// eigmin_lds2: the Householder tridiagonalisation of eigmin_lds with two barriers per column
+// instead of four, and the next reflector off the critical path.  The matrix is in LDS with a
+// padded leading dimension (ld = 16 ceil(n/16) + 8, so the 16 lanes of an LDS pass hit distinct
+// banks); thread (wave w, lane r + 8 c) owns row 64 q + 8 w + r (every pass q) and the column
+// class j = c mod 8.  Per column k (trailing block k+1.., reflector v, beta):
+//   (B) p_i = (A v)_i: the row's 8 class partials summed by DPP / permlane swaps inside the wave,
+//       p -> LDS, the per-wave parts of v^T p -> LDS                              -- barrier
+//   (D) with K = beta^2 v^T p / 2, g_i = beta p_i - 2K v_i and h_i = beta v_i (the row's own
+//       values): a_ij -= h_i p_j + g_i v_j for every j > k of the thread's class (LDS reads of
+//       p_j, v_j only; no w vector, no third barrier).  Column k+1 is skipped there: wave 0
+//       forms its updated entries in registers and builds the next reflector from them (multi-
+//       word norm, rsqrt pivot, reciprocal) while the other waves update     -- barrier
+// The rows/columns <= k+1 are never read again, so column k+1 is not written back.
+// ------------------------------------------------------------------------------------------
+template <class T> __host__ __device__ constexpr int eig2_ld(int n) { return ((n + 15) / 16) * 16 + 8; }
+template <class T> size_t eig2_lds_bytes(int n) {
+  // A (n x ld), v (2 x ld), p (ld), dg, e2, scal (4), redw (2 x 8), + the tail's fp64 scratch
+  return sizeof(T) * ((size_t)n * eig2_ld<T>(n) + 3 * (size_t)eig2_ld<T>(n) + 2 * (size_t)n + 4 + 16) + 64;
+}
+template <class T, bool NEWTON = true>
+__global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict__ descs,
+                                                   T* __restrict__ out) {
+  constexpr int NT = 512;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const MatDesc<T> d = descs[blockIdx.x];
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ld = eig2_ld<T>(n);
+  T* A = reinterpret_cast<T*>(smem_raw);      // n x ld, column-major
+  T* vb = A + (size_t)n * ld;                 // 2 x ld: v of step k in vb[(k & 1) * ld]
+  T* p = vb + 2 * ld;                          // ld
+  T* dg = p + ld;                              // n
+  T* e2 = dg + n;                              // n
+  T* scal = e2 + n;                            // [0..1] beta of the two v buffers
+  T* redw = scal + 4;                          // 2 x 8 per-wave parts of v^T p
+  // coalesced load, then symmetrise: A = (A + A^T)/2
+  for (int j = tid >> 6; j < n; j += NT / 64)
+    for (int i = lane; i < n; i += 64) A[i + (size_t)j * ld] = d.A[i + (size_t)j * d.lda];
+  __syncthreads();
+  for (int j = tid >> 6; j < n; j += NT / 64)
+    for (int i = lane; i < j; i += 64) {
+      const T sv = (A[i + (size_t)j * ld] + A[j + (size_t)i * ld]) * T(0.5);
+      A[i + (size_t)j * ld] = sv;
+      A[j + (size_t)i * ld] = sv;
+    }
+  __syncthreads();
+  const int r = lane & 7, cls = lane >> 3;
+  const int npass = (n + 63) / 64;
+  // reflector of column c from its entries x_i = col[i] (i > c; lane l holds rows c+1+l and
+  // c+65+l), by wave 0: v into vb[c & 1], beta into scal[c & 1], dg[c] = diag, e2[c]
+  auto reflector = [&](int c, const T (&x)[2], const T& diag) {
+    T s = T(0.0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) s += x[h] * x[h];
+    s = wave_sum_mw(s);
+    const T x0 = shfl_t(x[0], 0);  // row c+1
+    const T tail = s - x0 * x0;
+    T* v = vb + (c & 1) * ld;
+    T beta = T(0.0), v0 = x0, e2c = x0 * x0;
+    if (tail > T(0.0)) {
+      T nrm, rnrm;
+      pivot_sqrt(s, nrm, rnrm);
+      const T alpha = (x0 > T(0.0)) ? -nrm : nrm;
+      v0 = x0 - alpha;
+      e2c = alpha * alpha;
+      beta = recip_fast(tail + v0 * v0) * T(2.0);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = c + 1 + lane + 64 * h;
+      if (i < n) v[i] = (i == c + 1) ? v0 : x[h];
+    }
+    if (lane < c + 1 && lane < ld) v[lane] = T(0.0);
+    if (lane + 64 < c + 1) v[lane + 64] = T(0.0);
+    if (lane == 0) {
+      dg[c] = diag;
+      e2[c] = e2c;
+      scal[c & 1] = beta;
+    }
+  };
   if (n == 1) {
-    if (tid == 0) out[blockIdx.x] = dg[0];
+    if (tid == 0) out[blockIdx.x] = A[0];
     return;
   }
-  // ---- multisection, 256-way on waves 0-3 (8 bits per round), in two phases:
-  //  (1) fp64 on the leading limbs of the tridiagonal: Gershgorin bracket, 8 rounds;
-  //  (2) multi-word, started from the fp64 eigenvalue +- delta, where delta bounds the effect of
-  //      the rounding to fp64 (Weyl: |dlambda| <= ||dT|| <= ~3 eps64 ||T||) and of the fp64 Sturm
-  //      counts (exact for a matrix perturbed by a few eps64 relative), with a wide margin.  The
-  //      bracket is checked with two multi-word counts (no eigenvalue below it, one below its top)
-  //      and replaced by the Gershgorin bracket if the check fails.  About half the multi-word
-  //      rounds of a multisection from the Gershgorin bracket.
-  // The matrix image in LDS is no longer needed: it holds the fp64 copy and the round masks.
-  double* dgh = reinterpret_cast<double*>(A);
-  double* e2h = dgh + n;
-  double* bnd = e2h + n;  // [0,1] Gershgorin bracket, [2,3] multi-word start bracket, [4] ok
-  unsigned long long* masks = reinterpret_cast<unsigned long long*>(bnd + 6);
-  for (int i = tid; i < n; i += NT) {
-    dgh[i] = Num<T>::hi(dg[i]);
-    e2h[i] = Num<T>::hi(e2[i]);
+  if (w == 0) {  // the reflector of column 0 from the input
+    T x[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = 1 + lane + 64 * h;
+      x[h] = i < n ? A[i] : T(0.0);
+    }
+    reflector(0, x, A[0]);
   }
   __syncthreads();
-  if (tid == 0) {
-    double glo = 0.0, ghi = 0.0;
-    for (int i = 0; i < n; ++i) {
-      double r = 0.0;
-      if (i > 0) r += sqrt(e2h[i - 1]);
-      if (i + 1 < n) r += sqrt(e2h[i]);
-      const double a = dgh[i] - r, b = dgh[i] + r;
-      if (i == 0 || a < glo) glo = a;
-      if (i == 0 || b > ghi) ghi = b;
-    }
-    // the leading limbs and the fp64 sqrt differ from the exact bounds by ~eps64 relative
-    const double span = ghi - glo, mag = fmax(fabs(glo), fabs(ghi));
-    bnd[0] = glo - span * 1e-3 - mag * 1e-12 - 1e-300;
-    bnd[1] = ghi + span * 1e-3 + mag * 1e-12 + 1e-300;
-  }
-  __syncthreads();
-  const int w = tid >> 6, lane = tid & 63;
-  // one 512-way round: the first of the 512 interior points with a count >= 1 (every thread
-  // gets the same answer); returns its index, or -1 if none
-  auto first_hit = [&](bool hit) -> int {
-    const unsigned long long mk = __ballot(hit);
-    if (lane == 0) masks[w] = mk;
-    __syncthreads();
-    int f = -1;
-    for (int q = 0; q < NW && f < 0; ++q)
-      if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
-    __syncthreads();
-    return f;
-  };
-  {
-    // 8 rounds of 256 division-free counts on waves 0-3 (64 bits of the Gershgorin span)
-    double lo = bnd[0], hi = bnd[1];
-    for (int it = 0; it < 8; ++it) {
-      const double width = hi - lo;
-      bool hit = false;
-      if (tid < 256) hit = sturm_any_below_mw(dgh, e2h, n, lo + width * ((double)(tid + 1) / 257.0));
-      const int f = first_hit(hit);
-      if (f < 0) {
-        lo = lo + width * (256.0 / 257.0);
-      } else {
-        hi = lo + width * ((double)(f + 1) / 257.0);
-        if (f > 0) lo = lo + width * ((double)f / 257.0);
-      }
-    }
-    if (tid == 0) {
-      const double c = 0.5 * (lo + hi);
-      const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
-      const double delta = 64.0 * (double)n * 2.3e-16 * mag + (hi - lo) + 1e-300;
-      bnd[2] = c - delta;
-      bnd[3] = c + delta;
-    }
-  }
-  __syncthreads();
-  EIG_STAMP(7)
-  if constexpr (NEWTON && Num<T>::BITS > 120) {
-    // (2') quad-double: Newton on det(T - sigma I) from the fp64 centre (at dd the 11 parallel
-    // multisection rounds are as fast as the sequential Newton chain, so dd keeps them).  With the pivots of
-    // T - sigma I = L D L^T, q_i = (d_i - sigma) - e2_{i-1} / q_{i-1}, and s_i = dq_i/dsigma =
-    // -1 + e2_{i-1} s_{i-1} / q_{i-1}^2, the Newton step is 1 / sum_i s_i / q_i.  It converges
-    // quadratically from the fp64 estimate (3 steps for a simple eigenvalue, a 4th confirms).
-    // The result is accepted only if it converged AND two multi-word Sturm counts bracket it
-    // (no eigenvalue below sigma - delta, one at most sigma + delta, delta = 2^(12-BITS)
-    // magnitudes); otherwise the multisection below runs as before.
-    T* nres = Wv;  // free after the reduction: [0] = sigma
-    const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
-    if (tid == 0) {
-      T s = T(0.5 * (bnd[2] + bnd[3]));
-      const double tol = ldexp(mag, -(Num<T>::BITS + 2)) + 1e-300;
-      int conv = 0;
-      for (int it = 0; it < 4; ++it) {
-        T q = dg[0] - s;
-        if (q == T(0.0)) q = T(1e-300);
-        T r = T(1.0) / q, sd = T(-1.0), g = -r;
-        for (int i = 1; i < n; ++i) {
-          const T t = e2[i - 1] * r;
-          sd = (t * r) * sd - T(1.0);
-          q = (dg[i] - s) - t;
-          if (q == T(0.0)) q = T(1e-300);
-          r = T(1.0) / q;
-          g = g + sd * r;
+  for (int k = 0; k + 2 < n; ++k) {
+    const T* v = vb + (k & 1) * ld;
+    const T beta = scal[k & 1];
+    // ---- (B) p = A' v on the trailing block (rows and columns > k)
+    T vp = T(0.0);
+    for (int q = 0; q < npass; ++q) {
+      const int i = 64 * q + 8 * w + r;
+      T a0 = T(0.0), a1 = T(0.0);
+      if (i > k && i < n) {
+        int j = cls + 8 * ((k + 1) / 8);
+        if (j <= k) j += 8;
+        for (; j + 8 < n; j += 16) {
+          a0 += A[i + (size_t)j * ld] * v[j];
+          a1 += A[i + (size_t)(j + 8) * ld] * v[j + 8];
         }
-        const T step = T(1.0) / g;
-        s = s - step;
-        const double as = fabs(Num<T>::hi(step));
-        if (!(as == as)) break;  // NaN: leave conv = 0
-        if (as <= tol) { conv = 1; break; }
+        if (j < n) a0 += A[i + (size_t)j * ld] * v[j];
       }
-      nres[0] = s;
-      masks[2] = (unsigned long long)conv;
+      T pi = a0 + a1;
+      pi = pi + dpp_mw<0x128>(pi);   // row_ror:8  -> classes c, c^1
+      pi = pi + swap_mw<16>(pi);     // classes c ^ 2
+      pi = pi + swap_mw<32>(pi);     // classes c ^ 4
+      if (cls == 0 && i < n) {
+        p[i] = (i > k) ? pi : T(0.0);
+        if (i > k) vp += v[i] * pi;
+      }
+    }
+    vp = wave_sum_mw(vp);
+    if (lane == 0) redw[(k & 1) * 8 + w] = vp;
+    __syncthreads();
+    // ---- (D) A' -= v w^T + w v^T on rows/columns > k+1; wave 0: column k+1 and its reflector
+    const T* rw = redw + (k & 1) * 8;
+    const T tot = ((rw[0] + rw[1]) + (rw[2] + rw[3])) + ((rw[4] + rw[5]) + (rw[6] + rw[7]));
+    const T K2 = beta * beta * tot;  // 2K
+    const int c1 = k + 1;
+    const T pc = p[c1], vc = v[c1];
+    if (w == 0) {  // column c1 (rows > c1) and its diagonal, updated in registers
+      T x[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = c1 + 1 + lane + 64 * h;
+        x[h] = T(0.0);
+        if (i < n) {
+          const T pi = p[i], vi = v[i];
+          const T gi = beta * pi - K2 * vi, hi = beta * vi;
+          x[h] = A[i + (size_t)c1 * ld] - (hi * pc + gi * vc);
+        }
+      }
+      const T gc = beta * pc - K2 * vc, hc = beta * vc;
+      const T diag = A[c1 + (size_t)c1 * ld] - (hc * pc + gc * vc);
+      reflector(c1, x, diag);
+    }
+    for (int q = 0; q < npass; ++q) {
+      const int i = 64 * q + 8 * w + r;
+      if (i > c1 && i < n) {
+        const T pi = p[i], vi = v[i];
+        const T gi = beta * pi - K2 * vi, hi = beta * vi;
+        int j = cls + 8 * ((c1 + 1) / 8);
+        if (j <= c1) j += 8;
+        for (; j < n; j += 8) {
+          T* a = A + i + (size_t)j * ld;
+          *a = *a - (hi * p[j] + gi * v[j]);
+        }
+      }
     }
     __syncthreads();
-    const T s = nres[0];
-    const T dl = T(ldexp(mag, 12 - Num<T>::BITS) + 1e-300);
-    int c = 0;
-    if (tid == 0) c = masks[2] && !ANY_BELOW(s - dl);
-    if (tid == 64) c = ANY_BELOW(s + dl);
-    __syncthreads();
-    if (tid == 0 || tid == 64) masks[tid >> 6] = (unsigned long long)c;
-    __syncthreads();
-    const bool ok = masks[0] && masks[1];
-    __syncthreads();
-    if (ok) {
-      if (tid == 0) out[blockIdx.x] = s;
-      EIG_STAMP(6)
-      return;
-    }
   }
-  T lo = T(bnd[2]), hi = T(bnd[3]);
-  // check the start bracket at full width: count(lo) == 0 and count(hi) >= 1
-  {
-    int c = 0;
-    if (tid == 0) c = !ANY_BELOW(lo);
-    if (tid == 64) c = ANY_BELOW(hi);
-    if (tid == 0 || tid == 64) masks[tid >> 6] = (unsigned long long)c;
-    __syncthreads();
-    const bool ok = masks[0] && masks[1];
-    __syncthreads();
-    if (!ok) {
-      lo = T(bnd[0]);
-      hi = T(bnd[1]);
-    }
-    // rounds to shrink the bracket to ~2^-BITS of the spectrum's magnitude.  The multi-word
-    // counts are VALU-issue bound, so they run 256-way on waves 0-3 (one wave per SIMD: 8 bits
-    // per round) rather than 512-way on two waves per SIMD (9 bits per round at twice the issue)
-#ifdef CLRSDP_EIG_MW512
-    constexpr int MS = 512, MB = 9;
-#else
-    constexpr int MS = 256, MB = 8;
-#endif
-    constexpr double MD = MS + 1.0;
-    const int rounds = ok ? (Num<T>::BITS - 25) / MB + 2 : Num<T>::BITS / MB + 3;
-    for (int it = 0; it < rounds; ++it) {
-      const T width = hi - lo;
-      bool hit = false;
-      if (tid < MS) {  // wave-uniform
-        const T sigma = lo + width * T((double)(tid + 1) / MD);
-        hit = ANY_BELOW(sigma);
-      }
-      const int f = first_hit(hit);
-      if (f < 0) {
-        lo = lo + width * T((double)MS / MD);
-      } else {
-        hi = lo + width * T((double)(f + 1) / MD);
-        if (f > 0) lo = lo + width * T((double)f / MD);
-      }
-    }
-  }
-  if (tid == 0) out[blockIdx.x] = (lo + hi) * T(0.5);
-  EIG_STAMP(6)
+  // the last diagonal entry (updated by the last step's (D))
+  if (tid == 0) dg[n - 1] = A[(n - 1) + (size_t)(n - 1) * ld];
+  __syncthreads();
+  eig_multisection<T, NEWTON>(dg, e2, n, A, p, out);
 }
 #undef ANY_BELOW
 
