@@ -1209,17 +1209,17 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
     T vp = T(0.0);
     for (int q = 0; q < npass; ++q) {
       const int i = 64 * q + 8 * w + r;
-      T a0 = T(0.0), a1 = T(0.0);
+      // the class's columns j = cls + 8 t > k, t < 16 (n <= 128): compile-time slots, so the
+      // independent multi-word products interleave (a runtime loop serialised their chains)
+      T acc[4] = {T(0.0), T(0.0), T(0.0), T(0.0)};
       if (i > k && i < n) {
-        int j = cls + 8 * ((k + 1) / 8);
-        if (j <= k) j += 8;
-        for (; j + 8 < n; j += 16) {
-          a0 += A[i + (size_t)j * ld] * v[j];
-          a1 += A[i + (size_t)(j + 8) * ld] * v[j + 8];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const int j = cls + 8 * t;
+          if (j > k && j < n) acc[t & 3] += A[i + (size_t)j * ld] * v[j];
         }
-        if (j < n) a0 += A[i + (size_t)j * ld] * v[j];
       }
-      T pi = a0 + a1;
+      T pi = (acc[0] + acc[1]) + (acc[2] + acc[3]);
       pi = pi + dpp_mw<0x128>(pi);   // row_ror:8  -> classes c, c^1
       pi = pi + swap_mw<16>(pi);     // classes c ^ 2
       pi = pi + swap_mw<32>(pi);     // classes c ^ 4
@@ -1258,11 +1258,13 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
       if (i > c1 && i < n) {
         const T pi = p[i], vi = v[i];
         const T gi = beta * pi - K2 * vi, hi = beta * vi;
-        int j = cls + 8 * ((c1 + 1) / 8);
-        if (j <= c1) j += 8;
-        for (; j < n; j += 8) {
-          T* a = A + i + (size_t)j * ld;
-          *a = *a - (hi * p[j] + gi * v[j]);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const int j = cls + 8 * t;
+          if (j > c1 && j < n) {
+            T* a = A + i + (size_t)j * ld;
+            *a = *a - (hi * p[j] + gi * v[j]);
+          }
         }
       }
     }
