@@ -1258,12 +1258,26 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
       if (i > c1 && i < n) {
         const T pi = p[i], vi = v[i];
         const T gi = beta * pi - K2 * vi, hi = beta * vi;
+        // groups of 4 slots: all loads, then the 4 independent updates, then the stores (the
+        // stores may alias later loads of the same LDS image, which would order every chain)
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-          const int j = cls + 8 * t;
-          if (j > c1 && j < n) {
-            T* a = A + i + (size_t)j * ld;
-            *a = *a - (hi * p[j] + gi * v[j]);
+        for (int t0 = 0; t0 < 16; t0 += 4) {
+          if (cls + 8 * t0 >= n) break;  // (uniform per class group: no slot of t0.. is live)
+          T av[4], pj[4], vj[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = cls + 8 * (t0 + u);
+            const int jc = j < n ? j : n - 1;
+            av[u] = A[i + (size_t)jc * ld];
+            pj[u] = p[jc];
+            vj[u] = v[jc];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) av[u] = av[u] - (hi * pj[u] + gi * vj[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = cls + 8 * (t0 + u);
+            if (j > c1 && j < n) A[i + (size_t)j * ld] = av[u];
           }
         }
       }
