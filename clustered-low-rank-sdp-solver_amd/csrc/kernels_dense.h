@@ -1262,7 +1262,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
         // stores may alias later loads of the same LDS image, which would order every chain)
 #pragma unroll
         for (int t0 = 0; t0 < 16; t0 += 4) {
-          if (cls + 8 * t0 >= n) break;  // (uniform per class group: no slot of t0.. is live)
+          if (cls + 8 * t0 >= n) break;  // (this lane has no live slot from t0 on)
           T av[4], pj[4], vj[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
