@@ -1128,7 +1128,8 @@ template <class T> size_t eig2_lds_bytes(int n) {
   // A (n x ld), v (2 x ld), p (ld), dg, e2, scal (4), redw (2 x 8), + the tail's fp64 scratch
   return sizeof(T) * ((size_t)n * eig2_ld<T>(n) + 3 * (size_t)eig2_ld<T>(n) + 2 * (size_t)n + 4 + 16) + 64;
 }
-template <class T, bool NEWTON = true>
+// DBG (timing experiments, tools/micro/eig2_mw.hip): 1 = stop after the tridiagonalisation
+template <class T, bool NEWTON = true, int DBG = 0>
 __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict__ descs,
                                                    T* __restrict__ out) {
   constexpr int NT = 512;
@@ -1287,6 +1288,10 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
   // the last diagonal entry (updated by the last step's (D))
   if (tid == 0) dg[n - 1] = A[(n - 1) + (size_t)(n - 1) * ld];
   __syncthreads();
+  if constexpr (DBG == 1) {
+    if (tid == 0) out[blockIdx.x] = dg[n - 1] + e2[0];
+    return;
+  }
   eig_multisection<T, NEWTON>(dg, e2, n, A, p, out);
 }
 #undef ANY_BELOW
