@@ -952,7 +952,16 @@ __device__ void eig_multisection(const T* __restrict__ dg, const T* __restrict__
     constexpr int MS = 256, MB = 8;
 #endif
     constexpr double MD = MS + 1.0;
-    const int rounds = ok ? (Num<T>::BITS - 25) / MB + 2 : Num<T>::BITS / MB + 3;
+    // rounds to take the bracket below 2^-(BITS+2) of the magnitude (from its actual width:
+    // the checked fp64 start bracket is ~64 n eps64 wide, so about 40 of the bits are known)
+    int rounds = Num<T>::BITS / MB + 3;
+    {
+      const double wd = Num<T>::hi(hi - lo);
+      const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
+      const double tgt = ldexp(mag, -(Num<T>::BITS + 2)) + 1e-300;
+      if (wd > 0.0 && wd < INFINITY)
+        rounds = min(rounds, max(1, (int)ceil(log2(wd / tgt) / (double)MB) + 1));
+    }
     for (int it = 0; it < rounds; ++it) {
       const T width = hi - lo;
       bool hit = false;
