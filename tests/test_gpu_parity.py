@@ -365,7 +365,8 @@ def test_sphere_packing_bound_qd(pk):
     of S_j breaks down near iteration 43 (gap ~2e-6); the LU fallback (approx_lu!, the reference's
     factorisation) takes over and the run terminates at the optimum.  The bound lies between the
     NaCl density 0.793 and de Laat et al.'s 0.813-class value (SP.jl:124-127); the 256-bit oracle's
-    iterate at gap 1.6e-5 (iteration 40, tests/golden) brackets it."""
+    iterate at gap 1.6e-5 (iteration 40, tests/golden) brackets it, and the 256-bit oracle run to
+    termination (91 iterations, gap 2.4e-22, sp_real_d8_mp256_full) pins it to 1e-13."""
     from clrsdp_amd import _lib as L
     from clrsdp_amd import sphere_packing as S
     res = S.Nsphere_packing_2point(3, 8, precision_words=4, maxiterations=200, verbose=False,
@@ -381,6 +382,10 @@ def test_sphere_packing_bound_qd(pk):
     g = _golden("sp_real_d8_mp256")["log"][-1]
     lo, hi = sorted((-float(g["p_obj"]), -float(g["d_obj"])))
     assert lo - 1e-9 <= float(bound) <= hi + 1e-9, (float(bound), lo, hi)
+    full = _golden("sp_real_d8_mp256_full")
+    assert full["status"] == "terminated"
+    ref = -float(full["final"]["p_obj"])
+    assert abs(float(bound) - ref) < 1e-13 * ref, (float(bound), ref)
 
 
 def test_fp64_reaches_where_the_oracle_stops(pk, oracle):

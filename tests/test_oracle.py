@@ -172,6 +172,25 @@ def test_golden_vectors(pk, oracle, name):
     assert rel_err(res.x, np.array([float(v) for v in g["x"]])) < tol
 
 
+def test_sphere_packing_golden_runs_are_consistent():
+    """The two 256-bit oracle runs on the real sphere-packing instance (40 iterations, and to
+    termination at the reference's default thresholds) share their first 40 log rows exactly, and
+    the terminated run satisfies the stopping rule (MPMP.jl:734-742): gap < 1e-15 and the final
+    objectives inside the 40-iteration bracket."""
+    import mpmath
+    a = json.load(open(os.path.join(GOLDEN, "sp_real_d8_mp256.json")))
+    f = json.load(open(os.path.join(GOLDEN, "sp_real_d8_mp256_full.json")))
+    assert a["instance"] == f["instance"]
+    for ra, rf in zip(a["log"], f["log"]):
+        assert all(ra[k] == rf[k] for k in ("mu", "alpha_p", "alpha_d", "beta"))
+    assert f["status"] == "terminated" and len(f["log"]) > len(a["log"])
+    with mpmath.workprec(256):
+        fin = {k: mpmath.mpf(v) for k, v in f["final"].items()}
+        assert fin["gap"] < mpmath.mpf("1e-15")
+        lo, hi = sorted((mpmath.mpf(a["log"][-1]["p_obj"]), mpmath.mpf(a["log"][-1]["d_obj"])))
+        assert lo <= fin["p_obj"] <= hi and lo <= fin["d_obj"] <= hi
+
+
 @pytest.mark.parametrize("name,bits", [("c4dd", 128), ("c4dd", 256), ("qd32", 256)])
 def test_stage_fixtures_agree_with_fp64_oracle(pk, oracle, name, bits):
     """The precomputed multi-precision stage fixtures (tests/golden/make_stage_fixtures.py) are
