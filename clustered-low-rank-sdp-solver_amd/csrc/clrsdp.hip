@@ -266,6 +266,7 @@ struct GemmPlan : PlanBase {
   // fp64 batches of one shape at constant operand strides take gemm_f64_uni (no descriptor
   // chain before the first operand load); CLRSDP_NO_UNI_GEMM keeps the descriptor kernels
   bool uni = false;
+  int uts = 64;  // gemm_f64_uni output tile (64 or 32)
   UniGemm ug{};
   void detect_uniform() {
     if constexpr (std::is_same<T, double>::value) {
@@ -293,8 +294,19 @@ struct GemmPlan : PlanBase {
       if (!ok) return;
       u.A = g0.A; u.B = g0.B; u.Cin = g0.Cin; u.C = g0.C; u.sa = g0.sa; u.sl = g0.sl;
       u.M = g0.M; u.N = g0.N; u.K = g0.K; u.lda = g0.lda; u.ldb = g0.ldb; u.ldcin = g0.ldcin;
-      u.ldc = g0.ldc; u.tn = g0.tn; u.P = (int)h.size();
-      const int tm = (int)cdiv(g0.M, TILE);
+      u.P = (int)h.size();
+      u.ldc = g0.ldc;
+      // 32x32 tiles when the 64x64 tiles would leave most CUs idle (a small batch: one CU's
+      // tile is then latency-bound, ~9.4 us for a 128^3 product against 6.5 us split over four
+      // CUs, tools/micro/gemm_tiles.hip); CLRSDP_GEMM_TS32_BELOW sets the threshold (tiles)
+      // (read at every plan build, so a test can force either tile in one process)
+      const char* e32 = std::getenv("CLRSDP_GEMM_TS32_BELOW");
+      const long ts32_below = e32 ? std::atol(e32) : 192L;
+      const long t64m = (long)cdiv(g0.M, 64), t64n = (long)cdiv(g0.N, 64);
+      const long tiles64 = u.P * (sym ? t64m * (t64m + 1) / 2 : t64m * t64n);
+      uts = tiles64 < ts32_below ? 32 : 64;
+      u.tn = (int)cdiv(g0.N, uts);
+      const int tm = (int)cdiv(g0.M, uts);
       u.tsym = tm * (tm + 1) / 2;
       ug = u;
       uni = true;
@@ -358,25 +370,26 @@ struct GemmPlan : PlanBase {
   }
 };
 
-template <bool DB>
+template <bool DB, int TS>
 void launch_uni_db(const UniGemm& u, hipStream_t s, bool ta, bool tb, bool sca, bool sym, int tag,
                    unsigned long long* stamp, double alpha, double beta, const double* ds, double dmult) {
+  constexpr int NW = TS == 64 ? 8 : 2, NT = 64 * NW;
+  const unsigned tiles = (unsigned)(u.P * (int)cdiv(u.M, TS) * u.tn);
   if (sca) {
-    gemm_f64_uni<false, true, 0, 32, 8, false, true, DB><<<(unsigned)(u.P * (int)cdiv(u.M, 64) * u.tn), 512, 0, s>>>(u, alpha, beta, ds, dmult);
+    gemm_f64_uni<false, true, 0, 32, NW, false, true, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
   } else if (sym) {
     if (beta != 0.0 || ds) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: beta = 0 only"};
     const unsigned grid = (unsigned)(u.P * u.tsym);
-    if (!ta && tb) gemm_f64_uni<false, true, 0, 32, 8, true, false, DB><<<grid, 512, 0, s>>>(u, alpha, 0.0);
-    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, 8, true, false, DB><<<grid, 512, 0, s>>>(u, alpha, 0.0);
+    if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, true, false, DB, TS><<<grid, NT, 0, s>>>(u, alpha, 0.0);
+    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, true, false, DB, TS><<<grid, NT, 0, s>>>(u, alpha, 0.0);
     else throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: op(A) = A only"};
   } else {
-    const unsigned grid = (unsigned)(u.P * (int)cdiv(u.M, 64) * u.tn);
-    if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
-    else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
-    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
-    else if (ta && !tb) gemm_f64_uni<true, false, 0, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
-    else if (!ta && tb) gemm_f64_uni<false, true, 0, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
-    else gemm_f64_uni<true, true, 0, 32, 8, false, false, DB><<<grid, 512, 0, s>>>(u, alpha, beta, ds, dmult);
+    if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+    else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else if (ta && !tb) gemm_f64_uni<true, false, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else gemm_f64_uni<true, true, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
   }
   HIPCHK(hipGetLastError());
 }
@@ -390,8 +403,9 @@ void GemmPlan<T>::launch_uni_impl(hipStream_t s, double alpha, double beta, cons
       const char* e = std::getenv("CLRSDP_UNI_DB");
       return !(e && e[0] == '0');
     }();
-    if (db) launch_uni_db<true>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
-    else launch_uni_db<false>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
+    if (uts == 32) launch_uni_db<true, 32>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
+    else if (db) launch_uni_db<true, 64>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
+    else launch_uni_db<false, 64>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
   }
 }
 
@@ -750,6 +764,12 @@ struct Solver final : HandleBase {
   PairTileDesc* d_ptd = nullptr;
   TileRef* d_pt2d = nullptr;
   int n_ptiles = 0;
+  // schur_fused_f64 (every local block delta <= 128): V^T X^-1 formed on chip, one workgroup
+  // per 64-row block; CLRSDP_SCHUR_FUSED=0 keeps the V^T X^-1 GEMM + schur_pairs_f64 pair
+  bool schur_fused = false;
+  FusedPairDesc* d_fpd = nullptr;
+  TileRef* d_fpt2d = nullptr;
+  int n_fwg = 0;
   SchurClusterDesc* d_gcd = nullptr;  // clusters summed by schur_gsum
   int n_gsum = 0, max_gD = 0;
   SchurClusterDesc* d_scd = nullptr;
@@ -1289,6 +1309,31 @@ struct Solver final : HandleBase {
       const std::vector<TileRef> pt2d = tile_major(pnt);
       n_ptiles = (int)pt2d.size();
       if (n_ptiles) { d_ptd = descs.own(ptd); d_pt2d = descs.own(pt2d); }
+      // the fused kernel: same blocks, one workgroup per 64-row block of each
+      const char* ef = std::getenv("CLRSDP_SCHUR_FUSED");
+      schur_fused = !(ef && ef[0] == '0') && !ptd.empty();
+      for (const PairTileDesc& t : ptd) schur_fused = schur_fused && t.del <= 128;
+      if (schur_fused) {
+        std::vector<FusedPairDesc> fpd;
+        std::vector<int> fnt;
+        int q = 0;
+        for (const LBlk& b : lb) {
+          if (b.K == 0) continue;
+          const PairTileDesc& t = ptd[q++];
+          FusedPairDesc f;
+          f.Vt = t.Vt; f.Xinv = Xinv + b.off; f.TYt = t.TYt; f.lam = t.lam; f.G = t.G; f.AY = t.AY;
+          f.K = t.K; f.del = t.del; f.ldG = t.ldG; f.ldx = b.n;
+          fpd.push_back(f);
+          fnt.push_back(cdiv(b.K, 64));
+        }
+        const std::vector<TileRef> ft2d = tile_major(fnt);
+        n_fwg = (int)ft2d.size();
+        d_fpd = descs.own(fpd);
+        d_fpt2d = descs.own(ft2d);
+        HIPCHK(hipFuncSetAttribute((const void*)schur_fused_f64,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)schur_fused::LDS));
+      }
       n_gsum = (int)gcd.size();
       if (n_gsum) d_gcd = descs.own(gcd);
     }
@@ -1664,14 +1709,17 @@ struct Solver final : HandleBase {
   void st_schur() {
     if constexpr (std::is_same<T, double>::value) {
       if (fast_schur) {
-        p_txy.launch(stream, 1.0, 0.0);
+        if (!schur_fused) p_txy.launch(stream, 1.0, 0.0);
         if (ty_ahead) {  // V^T Y came from the side stream
           HIPCHK(hipStreamWaitEvent(stream, ev_ty, 0));
           ty_ahead = false;
         } else {
           p_ty.launch(stream, 1.0, 0.0);
         }
-        if (n_ptiles) schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d, stamps + 4);
+        if (schur_fused)
+          schur_fused_f64<<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4);
+        else if (n_ptiles)
+          schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d, stamps + 4);
         if (n_gsum) {
           dim3 g((unsigned)std::min<int64_t>(cdiv((int64_t)max_gD * max_gD, 256), 64), n_gsum);
           schur_gsum<T><<<g, 256, 0, stream>>>(d_gcd, d_sbd, rsums, BX, S);

@@ -63,17 +63,19 @@ typedef const __attribute__((address_space(1))) double* gdptr;
 __device__ inline double gload(const double* p) { return *(gdptr)p; }
 
 namespace lds_gemm {
-// Staging of one 64 x BK slab of an operand (256 threads, BK/4 elements per thread).
-// kcontig: element (i, k) at P[k + i*ld], kept in LDS as S[i*(BK+2) + k];
-// else at P[i + k*ld], kept as S[k*80 + i].  Rows i beyond `rows` are clamped (their products
-// are never stored); k beyond K is zeroed.
+// Staging of one R x BK slab of an operand (NTH threads, R*BK/NTH elements per thread; R = 64,
+// or 32 for the small-tile GEMM).  kcontig: element (i, k) at P[k + i*ld], kept in LDS as
+// S[i*(BK+2) + k]; else at P[i + k*ld], kept as S[k*LM + i] (LM = R + 16: the four k-rows of a
+// fragment read start 32 banks apart).  Rows i beyond `rows` are clamped (their products are
+// never stored); k beyond K is zeroed.
 constexpr int LSM = 80;
-template <int BK, int NTH = 256> struct Slab {
-  static constexpr int PER = 64 * BK / NTH, LSK = BK + 2;
-  static constexpr int SZ = 64 * LSK > BK * LSM ? 64 * LSK : BK * LSM;  // doubles per image
+template <int BK, int NTH = 256, int R = 64> struct Slab {
+  static constexpr int PER = R * BK / NTH, LSK = BK + 2, LM = R + 16;
+  static_assert(PER * NTH == R * BK, "slab split");
+  static constexpr int SZ = R * LSK > BK * LM ? R * LSK : BK * LM;  // doubles per image
   template <bool kcontig>
   __device__ static inline void kk(int tid, int q, int& i, int& k) {
-    if (!kcontig) { i = tid & 63; k = (tid >> 6) + (NTH / 64) * q; }
+    if (!kcontig) { i = tid % R; k = tid / R + (NTH / R) * q; }
     else { k = tid & (BK - 1); i = tid / BK + (NTH / BK) * q; }
   }
   // Unconditional loads from clamped addresses; the k >= K tail is zeroed in store(), after
@@ -98,14 +100,14 @@ template <int BK, int NTH = 256> struct Slab {
       int i, k;
       kk<kcontig>(tid, q, i, k);
       const double v = k0 + k < K ? r[q] : 0.0;
-      if (!kcontig) S[k * LSM + i] = v;
+      if (!kcontig) S[k * LM + i] = v;
       else S[i * LSK + k] = v;
     }
   }
   // MFMA fragment: element (i, k) of the staged image
   template <bool kcontig>
   __device__ static inline double frag(const double* __restrict__ S, int i, int k) {
-    return kcontig ? S[i * LSK + k] : S[k * LSM + i];
+    return kcontig ? S[i * LSK + k] : S[k * LM + i];
   }
 };
 // 64x64 output tile staged in LDS (pitch TP) so the global stores are coalesced: the MFMA
@@ -116,33 +118,35 @@ __device__ inline int acc_col(int wn, int ni, int lr, int wcols = 32) { return w
 }  // namespace lds_gemm
 
 // TAG only names the instantiation (a profile can tell the Schur-stage launch from the others).
-// NW = 4 (2x2 waves, 32x32 each) or 8 (2x4 waves, 32x16 each: twice the waves per tile, for
-// batches of small products that leave the CUs latency-bound).
+// TS = 64: NW = 8 (2x4 waves, 32x16 each) or 4 (2x2 waves, 32x32 each).  TS = 32 (small
+// batches, where 64x64 tiles leave most CUs idle and each CU latency-bound): NW = 2, 1x2 waves
+// of 32x16.
 // SYM: square problems whose product is symmetric in exact arithmetic (L^-1 dM L^-T): the launch
 // covers the lower tiles only, each writes its tile and the mirror image, and a diagonal tile
 // mirrors its lower triangle -- the result is exactly symmetric (beta = 0, no diagonal term).
-template <int BK, int NW, bool DB = false>
+template <int BK, int NW, bool DB = false, int TS = 64>
 constexpr int gemm_f64_smem() {
-  return (DB ? 4 : 2) * lds_gemm::Slab<BK, 64 * NW>::SZ > 64 * lds_gemm::TP
-             ? (DB ? 4 : 2) * lds_gemm::Slab<BK, 64 * NW>::SZ
-             : 64 * lds_gemm::TP;
+  return (DB ? 4 : 2) * lds_gemm::Slab<BK, 64 * NW, TS>::SZ > TS * lds_gemm::TP
+             ? (DB ? 4 : 2) * lds_gemm::Slab<BK, 64 * NW, TS>::SZ
+             : TS * lds_gemm::TP;
 }
-// one 64x64 output tile t of problem d (the body of every fp64 GEMM launch)
+// one TS x TS output tile t of problem d (the body of every fp64 GEMM launch)
 // SCA (op(A) = A only): A(i, k) * (sa[k] * sl[k]) -- compute_weighted_A's V diag(x lambda)
 // (MPMP.jl:1659) formed while the slab is staged, with scale_cols's operation order
 // DB: double-buffered slabs (two LDS images per operand): the next slab is stored into the
 // other image while no wave reads it, so each k-step needs one barrier instead of two
-template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false, bool DB = false>
+template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false, bool DB = false, int TS = 64>
 __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, double* smem,
                                               double alpha, double beta,
                                               const double* __restrict__ dscal, double dmult) {
   using namespace lds_gemm;
-  constexpr int NTH = 64 * NW, WN = NW / 2, NI = 4 / WN, WC = 64 / WN;
-  using SL = Slab<BK, NTH>;
+  constexpr int NTH = 64 * NW, WM = TS / 32, WN = NW / WM, NI = TS / (16 * WN), WC = TS / WN;
+  static_assert(WM * WN == NW && NI * 16 * WN == TS, "wave layout");
+  using SL = Slab<BK, NTH, TS>;
   constexpr int PER = SL::PER;
   double* As = smem;
   double* Bs = smem + SL::SZ;
-  const int m0 = (t / d.tn) * 64, n0 = (t % d.tn) * 64;
+  const int m0 = (t / d.tn) * TS, n0 = (t % d.tn) * TS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w % WN, lr = lane & 15, lk = lane >> 4;
   const int M = d.M, N = d.N, K = d.K;
@@ -229,28 +233,30 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
       for (int r = 0; r < 4; ++r)
         smem[acc_row(wm, mi, lk, r) * TP + acc_col(wn, ni, lr, WC)] = acc[mi][ni][r];
   __syncthreads();
-  const int row = m0 + lane;
-  constexpr int CPW = 64 / NW;  // output columns stored per wave
+  // thread -> row rl of the tile (consecutive threads, consecutive rows: coalesced), columns
+  // cl = tid / TS + (NTH / TS) c
+  const int rl = tid % TS, row = m0 + rl, c0 = tid / TS;
+  constexpr int CPT = TS * TS / NTH, CST = NTH / TS;
   if constexpr (SYM) {
 #pragma unroll 4
-    for (int c = 0; c < CPW; ++c) {
-      const int cl = w * CPW + c;
+    for (int c = 0; c < CPT; ++c) {
+      const int cl = c0 + CST * c;
       if (row < M && n0 + cl < N) {
-        const double v = (m0 != n0 || cl <= lane) ? smem[lane * TP + cl] : smem[cl * TP + lane];
+        const double v = (m0 != n0 || cl <= rl) ? smem[rl * TP + cl] : smem[cl * TP + rl];
         d.C[row + (size_t)(n0 + cl) * d.ldc] = alpha * v;
       }
-      // the mirror tile: element (m0 + cl, n0 + lane) to (n0 + lane, m0 + cl)
-      if (m0 != n0 && m0 + cl < M && n0 + lane < N)
-        d.C[(n0 + lane) + (size_t)(m0 + cl) * d.ldc] = alpha * smem[cl * TP + lane];
+      // the mirror tile: element (m0 + cl, n0 + rl) to (n0 + rl, m0 + cl)
+      if (m0 != n0 && m0 + cl < M && n0 + rl < N)
+        d.C[(n0 + rl) + (size_t)(m0 + cl) * d.ldc] = alpha * smem[cl * TP + rl];
     }
     return;
   }
   if (row < M) {
 #pragma unroll 4
-    for (int c = 0; c < CPW; ++c) {
-      const int cl = w * CPW + c, col = n0 + cl;
+    for (int c = 0; c < CPT; ++c) {
+      const int cl = c0 + CST * c, col = n0 + cl;
       if (col < N) {
-        double v = alpha * smem[lane * TP + cl];
+        double v = alpha * smem[rl * TP + cl];
         if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];
         if (dscal && row == col) v += dmult * *dscal;  // fused "+ s I" (square diagonal blocks)
         d.C[row + (size_t)col * d.ldc] = v;
@@ -303,14 +309,14 @@ __device__ inline void lower_tile(int q, int& tm, int& tn) {
   tn = q - tm * (tm + 1) / 2;
 }
 template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false, bool SCA = false,
-          bool DB = true>
+          bool DB = true, int TS = 64>
 __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double alpha, double beta,
                                                         const double* __restrict__ dscal = nullptr,
                                                         double dmult = 0.0,
                                                         unsigned long long* stamp = nullptr) {
   if constexpr (TAG == 1 || TAG == 3)
     if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-  __shared__ double smem[gemm_f64_smem<BK, NW, DB>()];
+  __shared__ double smem[gemm_f64_smem<BK, NW, DB, TS>()];
   const int p = blockIdx.x % u.P, q = blockIdx.x / u.P;
   GemmDesc<double> d;
   d.A = u.A + p * u.sA;
@@ -327,7 +333,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double 
     lower_tile(q, tm, tc);
     t = tm * u.tn + tc;
   }
-  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA, DB>(d, t, smem, alpha, beta, dscal, dmult);
+  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA, DB, TS>(d, t, smem, alpha, beta, dscal, dmult);
   if constexpr (TAG == 1 || TAG == 3)
     if (stamp) {
       __syncthreads();
@@ -1467,6 +1473,229 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
       for (int c = 0; c < 16; ++c) {
         const int pl = w * 16 + c, p = p0 + pl;
         if (p < K && (I < J || p < q)) d.G[q + (size_t)p * d.ldG] = lamS[pl] * lq * Tt[pl * TP + ql];
+      }
+    }
+  }
+  if (stamp) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// schur_fused_f64: the Schur pairing of one block (m = 1, delta <= 128) with V^T X^-1 formed on
+// chip, one 512-thread workgroup per 64-row block `a` of the K x K result.  It replaces the
+// V^T X^-1 GEMM and schur_pairs_f64: the K x delta product never goes to HBM.
+//   phase 1: C' = X^-1 V_a (delta x 64, LDS-staged MFMA GEMM).  Wave w = (nt = w & 3, h = w >> 2)
+//            keeps the 16x16 tiles (mt, nt), mt = 4h..4h+3, in its accumulators; register r of
+//            lane l of tile (mt, nt) is TXt[a-row 16nt + (l & 15)][k = 16mt + 4r + (l >> 4)],
+//            i.e. exactly the A-operand fragment of k-chunk 4mt + r of TXt_a V_b.  The two
+//            K halves are swapped once through LDS, so every wave holds all 32 chunks of its row
+//            tile; the TYt_a fragments (V^T Y, computed ahead on the side stream) come from HBM.
+//   phase 2: for each column block b of this workgroup's share of the upper triangle (b = a,
+//            a+1, .., a + floor(T/2) mod T, the pair {a, a+T/2} once when T is even: 2-3 tiles
+//            for T = 4), P_X = TXt_a V_b and P_Y = TYt_a V_b (V_b staged in LDS, prefetched into
+//            registers during the previous tile), G[p, q] = lambda_p lambda_q P_X P_Y, written
+//            to (p, q) through an LDS staging tile (coalesced) and to its mirror (q, p) straight
+//            from the accumulators; a diagonal tile takes its p <= q half for both, and writes
+//            AY[p] = P_Y[p, p].
+// MPMP.jl:1291-1330 + 1373-1398 at m = 1, as schur_pairs_f64.
+// ------------------------------------------------------------------------------------------
+struct FusedPairDesc {
+  const double* Vt;    // K x delta, ld K
+  const double* Xinv;  // delta x delta, ld ldx
+  const double* TYt;   // K x delta, ld K
+  const double* lam;   // K
+  double* G;           // K x K, ld ldG
+  double* AY;          // K
+  int K, del, ldG, ldx;
+};
+namespace schur_fused {
+constexpr int BK = 32;                   // phase-1 k-slab
+constexpr int LA = 144, LBV = 80;        // slab pitches (doubles): 32 banks apart per k-row
+constexpr int P1 = BK * LA + BK * LBV;   // phase-1 slabs
+constexpr int XCH = 8 * 16 * 64;         // phase-1 swap: 8 waves x 16 doubles x 64 lanes
+constexpr int R1 = P1 > XCH ? P1 : XCH;  // region 1 (later the output staging tile)
+constexpr int VS = 128 * LBV;            // V_b slab
+constexpr size_t LDS = sizeof(double) * (R1 + VS);
+}  // namespace schur_fused
+
+__global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __restrict__ descs,
+                                                       const TileRef* __restrict__ t2d,
+                                                       unsigned long long* stamp = nullptr) {
+  using namespace schur_fused;
+  if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  extern __shared__ __attribute__((aligned(16))) double sm_fused[];
+  double* R = sm_fused;        // phase-1 slabs / swap / output staging (pitch lds_gemm::TP)
+  double* Vs = sm_fused + R1;  // V_b: k-row pitch LBV
+  const TileRef tr = t2d[blockIdx.x];
+  const FusedPairDesc d = descs[tr.p];
+  const int a = tr.t, K = d.K, D = d.del;
+  const int T = (K + 63) / 64, a0 = 64 * a;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nt = w & 3, h = w >> 2, lr = lane & 15, lk = lane >> 4;
+  // ---------------- phase 1: C' = X^-1 V_a
+  d4 c1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c1[q] = d4{0.0, 0.0, 0.0, 0.0};
+  double ra[8], rb[4];
+  auto load1 = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // X^-1 (i, k'): i = e % 128 contiguous
+      const int e = tid + 512 * q, i = e & 127, k = k0 + (e >> 7);
+      ra[q] = gload(d.Xinv + min(i, D - 1) + (size_t)min(k, D - 1) * d.ldx);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // V_a (k', j) = Vt[a0 + j + k' K]
+      const int e = tid + 512 * q, j = e & 63, k = k0 + (e >> 6);
+      rb[q] = gload(d.Vt + min(a0 + j, K - 1) + (size_t)min(k, D - 1) * K);
+    }
+  };
+  auto store1 = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 512 * q, i = e & 127, k = e >> 7;
+      R[k * LA + i] = (i < D && k0 + k < D) ? ra[q] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 512 * q, j = e & 63, k = e >> 6;
+      R[BK * LA + k * LBV + j] = k0 + k < D ? rb[q] : 0.0;
+    }
+  };
+  load1(0);
+  store1(0);
+  __syncthreads();
+  for (int k0 = 0; k0 < D; k0 += BK) {
+    const bool more = k0 + BK < D;
+    if (more) load1(k0 + BK);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const double bf = R[BK * LA + (kk + lk) * LBV + 16 * nt + lr];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double af = R[(kk + lk) * LA + 16 * (4 * h + q) + lr];
+        c1[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, c1[q], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (!more) break;
+    store1(k0 + BK);
+    __syncthreads();
+  }
+  // swap the K halves: tf[c] = TXt fragment of k-chunk c (c = 4 mt + r)
+  double tf[32];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) R[((w * 4 + q) * 4 + r) * 64 + lane] = c1[q][r];
+  // the first V_b slab and the TYt_a fragments load meanwhile
+  const int nb = (T % 2 == 0 && a >= T / 2) ? T / 2 : T / 2 + 1;  // tiles of this workgroup
+  double rv[16];
+  auto loadv = [&](int b) {
+    const int b0 = 64 * b;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {  // V_b (k, j) = Vt[b0 + j + k K]
+      const int e = tid + 512 * q, j = e & 63, k = e >> 6;
+      rv[q] = gload(d.Vt + min(b0 + j, K - 1) + (size_t)min(k, D - 1) * K);
+    }
+  };
+  auto storev = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = tid + 512 * q, j = e & 63, k = e >> 6;
+      Vs[k * LBV + j] = k < D ? rv[q] : 0.0;
+    }
+  };
+  loadv(a);
+  double yf[32];
+  {
+    const int p = min(a0 + 16 * nt + lr, K - 1);
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      const int k = 4 * c + lk;
+      const double v = gload(d.TYt + p + (size_t)min(k, D - 1) * K);
+      yf[c] = k < D ? v : 0.0;
+    }
+  }
+  __syncthreads();
+  const int wp = w ^ 4;  // the wave with the other K half of this row tile
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      tf[4 * mt + r] = (mt >> 2) == h ? c1[mt & 3][r] : R[((wp * 4 + (mt & 3)) * 4 + r) * 64 + lane];
+  // lambda of this lane's four rows
+  double lp[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) lp[r] = d.lam[min(a0 + 16 * nt + 4 * r + lk, K - 1)];
+  // (region 1 becomes the staging tile only after the first barrier of the tile loop, which
+  // every wave reaches after reading its swap fragments)
+  storev();
+  __syncthreads();
+  double* St = R;  // 64 x 64 output staging, pitch TP
+  constexpr int TP = lds_gemm::TP;
+  for (int s = 0; s < nb; ++s) {
+    const int b = (a + s) % T, b0 = 64 * b;
+    const bool diag = s == 0;
+    // ---------------- phase 2: P_X, P_Y for the column tiles bt = 2h, 2h+1
+    d4 px[2], py[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) px[u] = py[u] = d4{0.0, 0.0, 0.0, 0.0};
+    // groups of 4 k-chunks: a group's 8 B fragments are read, then its 16 MFMAs issue; the
+    // scheduling barrier keeps later reads from being hoisted (the 64 + 64 A-fragment registers
+    // leave no room for more)
+#pragma unroll
+    for (int c0 = 0; c0 < 32; c0 += 4) {
+      double bf[4][2];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) bf[c][u] = Vs[(4 * (c0 + c) + lk) * LBV + 16 * (2 * h + u) + lr];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          px[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(tf[c0 + c], bf[c][u], px[u], 0, 0, 0);
+          py[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(yf[c0 + c], bf[c][u], py[u], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the next V_b loads in flight during the epilogue (issued after the MFMAs: the 64 + 64 A
+    // fragments are live during them)
+    if (s + 1 < nb) loadv((a + s + 1) % T);
+    // element (p, q) of register r: p = a0 + 16 nt + 4r + lk, q = b0 + 16 bt + lr
+    double g[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ql = 16 * (2 * h + u) + lr, q = b0 + ql;
+      const double lq = d.lam[min(q, K - 1)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pl = 16 * nt + 4 * r + lk, p = a0 + pl;
+        const double yv = py[u][r];
+        g[u][r] = lp[r] * lq * (px[u][r] * yv);
+        if (diag && pl == ql && p < K) d.AY[p] = yv;
+        // mirror (q, p): lanes on consecutive q, coalesced
+        if (p < K && q < K && (!diag || pl < ql)) d.G[q + (size_t)p * d.ldG] = g[u][r];
+      }
+    }
+    __syncthreads();  // all reads of Vs (this tile) and of St (previous tile) are done
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) St[(16 * nt + 4 * r + lk) * TP + 16 * (2 * h + u) + lr] = g[u][r];
+    if (s + 1 < nb) storev();
+    __syncthreads();
+    // (p, q) through the staging tile: thread -> row pl, 8 columns
+    {
+      const int pl = tid & 63, p = a0 + pl;
+      if (p < K) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int ql = (tid >> 6) + 8 * c, q = b0 + ql;
+          if (q < K && (!diag || pl <= ql)) d.G[p + (size_t)q * d.ldG] = St[pl * TP + ql];
+        }
       }
     }
   }

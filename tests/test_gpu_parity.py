@@ -96,6 +96,59 @@ def test_stage_parity_fp64(pk, oracle, cfg):
     _stage_compare(pk, oracle, cons, b)
 
 
+@pytest.mark.parametrize("cfg", CONFIGS_GPU[-3:], ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_stage_parity_fp64_64x64_tiles(pk, oracle, cfg, monkeypatch):
+    """The batches of these small instances take the 32x32-tile GEMM (gemm_f64_uni TS = 32);
+    the same stages with every uniform batch forced onto the 64x64 tiles the full-size C2/C3
+    batches use."""
+    monkeypatch.setenv("CLRSDP_GEMM_TS32_BELOW", "0")
+    cons, b = pk.synth(seed=3, **cfg)
+    _stage_compare(pk, oracle, cons, b)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS_GPU[-4:-1], ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_stage_parity_fp64_unfused_schur(pk, oracle, cfg, monkeypatch):
+    """The V^T X^-1 GEMM + schur_pairs_f64 pair that schur_fused_f64 replaces (kept behind
+    CLRSDP_SCHUR_FUSED=0 for A/B): the same stage parity."""
+    monkeypatch.setenv("CLRSDP_SCHUR_FUSED", "0")
+    cons, b = pk.synth(seed=3, **cfg)
+    _stage_compare(pk, oracle, cons, b)
+
+
+def test_schur_fused_matches_unfused(pk, monkeypatch):
+    """schur_fused_f64 against the unfused kernels on the C3 cluster shape (K = 255: four row
+    blocks, the last one ragged, and the wrapped tile assignment), on rank-2 blocks (G into the
+    BX arena, then schur_gsum) and on K = 40 (one row block): S and A_Y agree to fp64 round-off,
+    and every S_j the kernel writes directly (rank-1 samples) is exactly symmetric."""
+    from clrsdp_amd import _lib as L
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    for cfg in (dict(J=3, delta=128, rank=1, n_y=20), dict(J=2, delta=64, rank=2, n_y=16),
+                dict(J=2, delta=40, rank=1, n_y=9)):
+        cons, b = pk.synth(seed=11, **cfg)
+        bi = pk.get_block_info(cons)
+        st = pk.initial_point(bi, 10.0, 10.0)
+        out = {}
+        for fused in ("1", "0"):
+            monkeypatch.setenv("CLRSDP_SCHUR_FUSED", fused)
+            dev = pk.DeviceSolver(cons, b, bi)
+            try:
+                dev.set_state(*st)
+                for stage in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR):
+                    dev.run_stage(stage, P, False)
+                out[fused] = (np.array(dev.buffer(L.BUF_S, False), dtype=float),
+                              np.array(dev.buffer(L.BUF_AY, False), dtype=float))
+            finally:
+                dev.close()
+        for u, v in zip(out["1"], out["0"]):
+            assert rel_err(u, v) < 1e-13, (cfg, rel_err(u, v))
+        S, off = out["1"][0], 0
+        for D in bi.dim_S:
+            blk = S[off:off + D * D].reshape(D, D)
+            if cfg["rank"] == 1:
+                assert np.array_equal(blk, blk.T), cfg
+            off += D * D
+
+
 def test_stage_parity_sphere_packing_shape(pk, oracle):
     """Mixed block sizes 1..18, m = 2 and m = 1 clusters, 2 blocks per cluster (config 5 shape)."""
     cons, b = pk.synth_mixed(**pk.SPHERE_PACKING_SHAPE, seed=1)
