@@ -1491,14 +1491,17 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
 //            lane l of tile (mt, nt) is TXt[a-row 16nt + (l & 15)][k = 16mt + 4r + (l >> 4)],
 //            i.e. exactly the A-operand fragment of k-chunk 4mt + r of TXt_a V_b.  The two
 //            K halves are swapped once through LDS, so every wave holds all 32 chunks of its row
-//            tile; the TYt_a fragments (V^T Y, computed ahead on the side stream) come from HBM.
+//            tile in registers.
 //   phase 2: for each column block b of this workgroup's share of the upper triangle (b = a,
 //            a+1, .., a + floor(T/2) mod T, the pair {a, a+T/2} once when T is even: 2-3 tiles
-//            for T = 4), P_X = TXt_a V_b and P_Y = TYt_a V_b (V_b staged in LDS, prefetched into
-//            registers during the previous tile), G[p, q] = lambda_p lambda_q P_X P_Y, written
-//            to (p, q) through an LDS staging tile (coalesced) and to its mirror (q, p) straight
-//            from the accumulators; a diagonal tile takes its p <= q half for both, and writes
-//            AY[p] = P_Y[p, p].
+//            for T = 4), P_X = TXt_a V_b and P_Y = TYt_a V_b.  TYt_a (V^T Y, computed ahead on
+//            the side stream) and V_b sit in LDS in MFMA-fragment order (one 64-lane row per
+//            fragment: conflict-free, and few enough registers that the fragment reads run
+//            ahead of the MFMAs); the next V_b is loaded into registers before the MFMAs of the
+//            current one.  G[p, q] = lambda_p lambda_q P_X P_Y is staged in LDS (XOR-swizzled
+//            64 x 64) and written to (p, q) and to its mirror (q, p) as whole 64-row column
+//            segments; a diagonal tile takes its p <= q half for both, and writes AY[p] =
+//            P_Y[p, p].
 // MPMP.jl:1291-1330 + 1373-1398 at m = 1, as schur_pairs_f64.
 // ------------------------------------------------------------------------------------------
 struct FusedPairDesc {
@@ -1511,29 +1514,34 @@ struct FusedPairDesc {
   int K, del, ldG, ldx;
 };
 namespace schur_fused {
-constexpr int BK = 32;                   // phase-1 k-slab
-constexpr int LA = 144, LBV = 80;        // slab pitches (doubles): 32 banks apart per k-row
-constexpr int P1 = BK * LA + BK * LBV;   // phase-1 slabs
-constexpr int XCH = 8 * 16 * 64;         // phase-1 swap: 8 waves x 16 doubles x 64 lanes
-constexpr int R1 = P1 > XCH ? P1 : XCH;  // region 1 (later the output staging tile)
-constexpr int VS = 128 * LBV;            // V_b slab
-constexpr size_t LDS = sizeof(double) * (R1 + VS);
+constexpr int BK = 32;                  // phase-1 k-slab
+constexpr int LA = 144, LBV = 80;       // phase-1 slab pitches (doubles): 32 banks apart per k-row
+constexpr int FR = 32 * 4 * 64;         // fragment-ordered 128 x 64 operand (TYt_a or V_b)
+constexpr int YR = 0, VR = FR, SR = 2 * FR, END = 2 * FR + 64 * 64;
+static_assert(BK * LA + BK * LBV <= END - VR, "phase-1 slabs fit in the V_b + staging regions");
+constexpr size_t LDS = sizeof(double) * END;  // 160 KB
+__device__ __forceinline__ int st_idx(int row, int col) { return row * 64 + (col ^ (row & 31)); }
 }  // namespace schur_fused
 
+// DBG (timing experiments only): 1 = no phase-2 MFMAs, 2 = no phase-1 MFMAs
+template <int DBG = 0>
 __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __restrict__ descs,
                                                        const TileRef* __restrict__ t2d,
                                                        unsigned long long* stamp = nullptr) {
   using namespace schur_fused;
   if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   extern __shared__ __attribute__((aligned(16))) double sm_fused[];
-  double* R = sm_fused;        // phase-1 slabs / swap / output staging (pitch lds_gemm::TP)
-  double* Vs = sm_fused + R1;  // V_b: k-row pitch LBV
+  double* Yf = sm_fused + YR;  // TYt_a fragments: (row tile t, chunk c, lane l) at (t*32 + c)*64 + l
+  double* Vf = sm_fused + VR;  // V_b fragments: (chunk c, column tile bt, lane l) at (c*4 + bt)*64 + l
+  double* St = sm_fused + SR;  // output staging, st_idx
+  double* P1 = sm_fused + VR;  // phase-1 slabs (over V_b and the staging tile)
   const TileRef tr = t2d[blockIdx.x];
   const FusedPairDesc d = descs[tr.p];
   const int a = tr.t, K = d.K, D = d.del;
   const int T = (K + 63) / 64, a0 = 64 * a;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nt = w & 3, h = w >> 2, lr = lane & 15, lk = lane >> 4;
+  const int nb = (T % 2 == 0 && a >= T / 2) ? T / 2 : T / 2 + 1;  // tiles of this workgroup
   // ---------------- phase 1: C' = X^-1 V_a
   d4 c1[4];
 #pragma unroll
@@ -1555,12 +1563,49 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int e = tid + 512 * q, i = e & 127, k = e >> 7;
-      R[k * LA + i] = (i < D && k0 + k < D) ? ra[q] : 0.0;
+      P1[k * LA + i] = (i < D && k0 + k < D) ? ra[q] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tid + 512 * q, j = e & 63, k = e >> 6;
-      R[BK * LA + k * LBV + j] = k0 + k < D ? rb[q] : 0.0;
+      P1[BK * LA + k * LBV + j] = k0 + k < D ? rb[q] : 0.0;
+    }
+  };
+  // V_b element (k, j) = Vt[b0 + j + k K]: thread element e = tid + 512 q is (k = e >> 6,
+  // j = e & 63), kept at Vf[((k >> 2) * 4 + (j >> 4)) * 64 + (k & 3) * 16 + (j & 15)]
+  double rv[16];
+  auto loadv = [&](int b) {
+    const int b0 = 64 * b;
+    const double* src = d.Vt + min(b0 + lane, K - 1);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = w + 8 * q;
+      rv[q] = gload(src + (size_t)min(k, D - 1) * K);
+    }
+  };
+  auto storev = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = w + 8 * q;
+      Vf[((k >> 2) * 4 + (lane >> 4)) * 64 + (k & 3) * 16 + (lane & 15)] = k < D ? rv[q] : 0.0;
+    }
+  };
+  // TYt_a element (row i = 16t + (l & 15), k = 4c + (l >> 4)) for (t, c, l) = (e >> 11,
+  // (e >> 6) & 31, e & 63), kept at Yf[e]
+  double ry[16];
+  auto loady = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = tid + 512 * q, l = e & 63, c = (e >> 6) & 31, t = e >> 11;
+      const int p = min(a0 + 16 * t + (l & 15), K - 1), k = 4 * c + (l >> 4);
+      ry[q] = gload(d.TYt + p + (size_t)min(k, D - 1) * K);
+    }
+  };
+  auto storey = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = tid + 512 * q, l = e & 63, c = (e >> 6) & 31;
+      Yf[e] = 4 * c + (l >> 4) < D ? ry[q] : 0.0;
     }
   };
   load1(0);
@@ -1571,10 +1616,11 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     if (more) load1(k0 + BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      const double bf = R[BK * LA + (kk + lk) * LBV + 16 * nt + lr];
+      if (DBG == 2) break;
+      const double bf = P1[BK * LA + (kk + lk) * LBV + 16 * nt + lr];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const double af = R[(kk + lk) * LA + 16 * (4 * h + q) + lr];
+        const double af = P1[(kk + lk) * LA + 16 * (4 * h + q) + lr];
         c1[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, c1[q], 0, 0, 0);
       }
     }
@@ -1583,87 +1629,63 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     store1(k0 + BK);
     __syncthreads();
   }
-  // swap the K halves: tf[c] = TXt fragment of k-chunk c (c = 4 mt + r)
-  double tf[32];
+  // phase 2's first operands load during the swap of the K halves (through the V_b region)
+  loady();
+  loadv(a);
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) R[((w * 4 + q) * 4 + r) * 64 + lane] = c1[q][r];
-  // the first V_b slab and the TYt_a fragments load meanwhile
-  const int nb = (T % 2 == 0 && a >= T / 2) ? T / 2 : T / 2 + 1;  // tiles of this workgroup
-  double rv[16];
-  auto loadv = [&](int b) {
-    const int b0 = 64 * b;
+    for (int r = 0; r < 4; ++r) Vf[((w * 4 + q) * 4 + r) * 64 + lane] = c1[q][r];
+  double lp[4];  // lambda of this lane's four rows
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {  // V_b (k, j) = Vt[b0 + j + k K]
-      const int e = tid + 512 * q, j = e & 63, k = e >> 6;
-      rv[q] = gload(d.Vt + min(b0 + j, K - 1) + (size_t)min(k, D - 1) * K);
-    }
-  };
-  auto storev = [&]() {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = tid + 512 * q, j = e & 63, k = e >> 6;
-      Vs[k * LBV + j] = k < D ? rv[q] : 0.0;
-    }
-  };
-  loadv(a);
-  double yf[32];
-  {
-    const int p = min(a0 + 16 * nt + lr, K - 1);
-#pragma unroll
-    for (int c = 0; c < 32; ++c) {
-      const int k = 4 * c + lk;
-      const double v = gload(d.TYt + p + (size_t)min(k, D - 1) * K);
-      yf[c] = k < D ? v : 0.0;
-    }
-  }
+  for (int r = 0; r < 4; ++r) lp[r] = d.lam[min(a0 + 16 * nt + 4 * r + lk, K - 1)];
   __syncthreads();
+  double tf[32];  // TXt_a fragment of k-chunk c = 4 mt + r
   const int wp = w ^ 4;  // the wave with the other K half of this row tile
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      tf[4 * mt + r] = (mt >> 2) == h ? c1[mt & 3][r] : R[((wp * 4 + (mt & 3)) * 4 + r) * 64 + lane];
-  // lambda of this lane's four rows
-  double lp[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) lp[r] = d.lam[min(a0 + 16 * nt + 4 * r + lk, K - 1)];
-  // (region 1 becomes the staging tile only after the first barrier of the tile loop, which
-  // every wave reaches after reading its swap fragments)
+      tf[4 * mt + r] = (mt >> 2) == h ? c1[mt & 3][r] : Vf[((wp * 4 + (mt & 3)) * 4 + r) * 64 + lane];
+  __syncthreads();
+  storey();
   storev();
   __syncthreads();
-  double* St = R;  // 64 x 64 output staging, pitch TP
-  constexpr int TP = lds_gemm::TP;
+  const double* yrow = Yf + nt * 32 * 64 + lane;     // chunk c at yrow[64 c]
+  const double* vrow = Vf + 2 * h * 64 + lane;       // chunk c, tile 2h + u at vrow[256 c + 64 u]
   for (int s = 0; s < nb; ++s) {
     const int b = (a + s) % T, b0 = 64 * b;
     const bool diag = s == 0;
+    if (s + 1 < nb) loadv((a + s + 1) % T);
     // ---------------- phase 2: P_X, P_Y for the column tiles bt = 2h, 2h+1
     d4 px[2], py[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) px[u] = py[u] = d4{0.0, 0.0, 0.0, 0.0};
-    // groups of 4 k-chunks: a group's 8 B fragments are read, then its 16 MFMAs issue; the
-    // scheduling barrier keeps later reads from being hoisted (the 64 + 64 A-fragment registers
-    // leave no room for more)
+    // fragment reads two chunks ahead of their MFMAs (a read an MFMA waits on exposes its
+    // latency; the scheduling barriers keep the compiler from regrouping them)
+    constexpr int PD = 2;
+    double fy[PD + 1], f0[PD + 1], f1[PD + 1];
 #pragma unroll
-    for (int c0 = 0; c0 < 32; c0 += 4) {
-      double bf[4][2];
+    for (int c = 0; c < PD; ++c) {
+      fy[c] = yrow[64 * c];
+      f0[c] = vrow[256 * c];
+      f1[c] = vrow[256 * c + 64];
+    }
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) bf[c][u] = Vs[(4 * (c0 + c) + lk) * LBV + 16 * (2 * h + u) + lr];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          px[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(tf[c0 + c], bf[c][u], px[u], 0, 0, 0);
-          py[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(yf[c0 + c], bf[c][u], py[u], 0, 0, 0);
-        }
+    for (int c = 0; c < 32; ++c) {
+      if (DBG == 1) break;
+      if (c + PD < 32) {
+        fy[(c + PD) % (PD + 1)] = yrow[64 * (c + PD)];
+        f0[(c + PD) % (PD + 1)] = vrow[256 * (c + PD)];
+        f1[(c + PD) % (PD + 1)] = vrow[256 * (c + PD) + 64];
+      }
+      const int q = c % (PD + 1);
+      px[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(tf[c], f0[q], px[0], 0, 0, 0);
+      py[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fy[q], f0[q], py[0], 0, 0, 0);
+      px[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(tf[c], f1[q], px[1], 0, 0, 0);
+      py[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fy[q], f1[q], py[1], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // the next V_b loads in flight during the epilogue (issued after the MFMAs: the 64 + 64 A
-    // fragments are live during them)
-    if (s + 1 < nb) loadv((a + s + 1) % T);
     // element (p, q) of register r: p = a0 + 16 nt + 4r + lk, q = b0 + 16 bt + lr
     double g[2][4];
 #pragma unroll
@@ -1676,26 +1698,25 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
         const double yv = py[u][r];
         g[u][r] = lp[r] * lq * (px[u][r] * yv);
         if (diag && pl == ql && p < K) d.AY[p] = yv;
-        // mirror (q, p): lanes on consecutive q, coalesced
-        if (p < K && q < K && (!diag || pl < ql)) d.G[q + (size_t)p * d.ldG] = g[u][r];
       }
     }
-    __syncthreads();  // all reads of Vs (this tile) and of St (previous tile) are done
+    __syncthreads();  // every wave is done with this V_b and with the previous staging tile
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) St[(16 * nt + 4 * r + lk) * TP + 16 * (2 * h + u) + lr] = g[u][r];
+      for (int r = 0; r < 4; ++r) St[st_idx(16 * nt + 4 * r + lk, 16 * (2 * h + u) + lr)] = g[u][r];
     if (s + 1 < nb) storev();
     __syncthreads();
-    // (p, q) through the staging tile: thread -> row pl, 8 columns
+    // (p, q) and its mirror (q, p) from the staging tile as 64-row column segments
     {
-      const int pl = tid & 63, p = a0 + pl;
-      if (p < K) {
+      const int il = tid & 63;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const int ql = (tid >> 6) + 8 * c, q = b0 + ql;
-          if (q < K && (!diag || pl <= ql)) d.G[p + (size_t)q * d.ldG] = St[pl * TP + ql];
-        }
+      for (int c = 0; c < 8; ++c) {
+        const int jl = (tid >> 6) + 8 * c;
+        if (a0 + il < K && b0 + jl < K && (!diag || il <= jl))  // G[a0 + il][b0 + jl]
+          d.G[(a0 + il) + (size_t)(b0 + jl) * d.ldG] = St[st_idx(il, jl)];
+        if (b0 + il < K && a0 + jl < K && (!diag || jl < il))   // G[b0 + il][a0 + jl]
+          d.G[(b0 + il) + (size_t)(a0 + jl) * d.ldG] = St[st_idx(jl, il)];
       }
     }
   }
