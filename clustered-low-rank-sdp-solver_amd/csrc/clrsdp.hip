@@ -1330,7 +1330,7 @@ struct Solver final : HandleBase {
         n_fwg = (int)ft2d.size();
         d_fpd = descs.own(fpd);
         d_fpt2d = descs.own(ft2d);
-        HIPCHK(hipFuncSetAttribute((const void*)schur_fused_f64,
+        HIPCHK(hipFuncSetAttribute((const void*)schur_fused_f64<0>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)schur_fused::LDS));
       }
@@ -1717,7 +1717,7 @@ struct Solver final : HandleBase {
           p_ty.launch(stream, 1.0, 0.0);
         }
         if (schur_fused)
-          schur_fused_f64<<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4);
+          schur_fused_f64<0><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4);
         else if (n_ptiles)
           schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d, stamps + 4);
         if (n_gsum) {

@@ -1518,7 +1518,8 @@ constexpr int BK = 32;                  // phase-1 k-slab
 constexpr int LA = 144, LBV = 80;       // phase-1 slab pitches (doubles): 32 banks apart per k-row
 constexpr int FR = 32 * 4 * 64;         // fragment-ordered 128 x 64 operand (TYt_a or V_b)
 constexpr int YR = 0, VR = FR, SR = 2 * FR, END = 2 * FR + 64 * 64;
-static_assert(BK * LA + BK * LBV <= END - VR, "phase-1 slabs fit in the V_b + staging regions");
+static_assert(BK * LA + BK * LBV <= FR && BK * LA + BK * LBV <= END - VR,
+              "phase-1 images fit in the TYt_a region and in the V_b + staging regions");
 constexpr size_t LDS = sizeof(double) * END;  // 160 KB
 __device__ __forceinline__ int st_idx(int row, int col) { return row * 64 + (col ^ (row & 31)); }
 }  // namespace schur_fused
@@ -1534,7 +1535,8 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
   double* Yf = sm_fused + YR;  // TYt_a fragments: (row tile t, chunk c, lane l) at (t*32 + c)*64 + l
   double* Vf = sm_fused + VR;  // V_b fragments: (chunk c, column tile bt, lane l) at (c*4 + bt)*64 + l
   double* St = sm_fused + SR;  // output staging, st_idx
-  double* P1 = sm_fused + VR;  // phase-1 slabs (over V_b and the staging tile)
+  // phase-1 slabs, double-buffered: image 0 over the TYt_a region, image 1 over V_b + staging
+  auto P1 = [&](int img) { return sm_fused + (img ? VR : YR); };
   const TileRef tr = t2d[blockIdx.x];
   const FusedPairDesc d = descs[tr.p];
   const int a = tr.t, K = d.K, D = d.del;
@@ -1559,16 +1561,16 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
       rb[q] = gload(d.Vt + min(a0 + j, K - 1) + (size_t)min(k, D - 1) * K);
     }
   };
-  auto store1 = [&](int k0) {
+  auto store1 = [&](double* S, int k0) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int e = tid + 512 * q, i = e & 127, k = e >> 7;
-      P1[k * LA + i] = (i < D && k0 + k < D) ? ra[q] : 0.0;
+      S[k * LA + i] = (i < D && k0 + k < D) ? ra[q] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tid + 512 * q, j = e & 63, k = e >> 6;
-      P1[BK * LA + k * LBV + j] = k0 + k < D ? rb[q] : 0.0;
+      S[BK * LA + k * LBV + j] = k0 + k < D ? rb[q] : 0.0;
     }
   };
   // V_b element (k, j) = Vt[b0 + j + k K]: thread element e = tid + 512 q is (k = e >> 6,
@@ -1609,29 +1611,32 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     }
   };
   load1(0);
-  store1(0);
+  store1(P1(0), 0);
   __syncthreads();
+  int img = 0;
   for (int k0 = 0; k0 < D; k0 += BK) {
     const bool more = k0 + BK < D;
     if (more) load1(k0 + BK);
+    const double* S = P1(img);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       if (DBG == 2) break;
-      const double bf = P1[BK * LA + (kk + lk) * LBV + 16 * nt + lr];
+      const double bf = S[BK * LA + (kk + lk) * LBV + 16 * nt + lr];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const double af = P1[(kk + lk) * LA + 16 * (4 * h + q) + lr];
+        const double af = S[(kk + lk) * LA + 16 * (4 * h + q) + lr];
         c1[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, c1[q], 0, 0, 0);
       }
     }
-    __syncthreads();
     if (!more) break;
-    store1(k0 + BK);
+    img ^= 1;
+    store1(P1(img), k0 + BK);  // (the other image was last read before the previous barrier)
     __syncthreads();
   }
   // phase 2's first operands load during the swap of the K halves (through the V_b region)
   loady();
   loadv(a);
+  __syncthreads();  // every wave is done with the last phase-1 image
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
