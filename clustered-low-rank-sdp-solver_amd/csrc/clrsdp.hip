@@ -1310,9 +1310,19 @@ struct Solver final : HandleBase {
       n_ptiles = (int)pt2d.size();
       if (n_ptiles) { d_ptd = descs.own(ptd); d_pt2d = descs.own(pt2d); }
       // the fused kernel: same blocks, one workgroup per 64-row block of each
+      // Taken when it fills at least half the CUs with 64 < delta <= 128 (C3 and its 2-rank
+      // shards): with fewer row blocks (small cluster counts) or delta <= 64 (its 32 k-chunks
+      // half empty: C2) the unfused pair, with more and smaller workgroups, is faster.
+      // CLRSDP_SCHUR_FUSED=0 / 1 forces either.
       const char* ef = std::getenv("CLRSDP_SCHUR_FUSED");
       schur_fused = !(ef && ef[0] == '0') && !ptd.empty();
-      for (const PairTileDesc& t : ptd) schur_fused = schur_fused && t.del <= 128;
+      int fwg = 0;
+      for (const PairTileDesc& t : ptd) {
+        schur_fused = schur_fused && t.del <= 128;
+        fwg += cdiv(t.K, 64);
+        if (!(ef && ef[0] == '1')) schur_fused = schur_fused && t.del > 64;
+      }
+      if (!(ef && ef[0] == '1')) schur_fused = schur_fused && fwg >= 128;
       if (schur_fused) {
         std::vector<FusedPairDesc> fpd;
         std::vector<int> fnt;

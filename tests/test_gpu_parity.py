@@ -106,11 +106,13 @@ def test_stage_parity_fp64_64x64_tiles(pk, oracle, cfg, monkeypatch):
     _stage_compare(pk, oracle, cons, b)
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("cfg", CONFIGS_GPU[-4:-1], ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
-def test_stage_parity_fp64_unfused_schur(pk, oracle, cfg, monkeypatch):
-    """The V^T X^-1 GEMM + schur_pairs_f64 pair that schur_fused_f64 replaces (kept behind
-    CLRSDP_SCHUR_FUSED=0 for A/B): the same stage parity."""
-    monkeypatch.setenv("CLRSDP_SCHUR_FUSED", "0")
+def test_stage_parity_fp64_schur_paths(pk, oracle, cfg, fused, monkeypatch):
+    """Both Schur paths at every stage: schur_fused_f64 (taken by default only when it fills half
+    the CUs with 64 < delta <= 128, so these small instances force it) and the V^T X^-1 GEMM +
+    schur_pairs_f64 pair it replaces."""
+    monkeypatch.setenv("CLRSDP_SCHUR_FUSED", fused)
     cons, b = pk.synth(seed=3, **cfg)
     _stage_compare(pk, oracle, cons, b)
 
