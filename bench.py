@@ -64,13 +64,13 @@ def schur_flops_bytes(bi, word=8):
     return fl, by
 
 
-def schur_pmc_traffic(config, precision, world):
+def schur_pmc_traffic(config, precision, world, clusters=0):
     """HBM bytes per iteration of the Schur stage (FETCH_SIZE + WRITE_SIZE of its launches) from
     the newest committed PMC summary, profiles/rNN_schur_pmc.json (tools/profile_round.sh, the
     default C3 fp64 1-GPU run), used only when it was taken on this very build (its
     source_hash); otherwise None and the source says why.  None for other runs."""
     import glob
-    if config != "c3" or precision != 1 or world != 1:
+    if config != "c3" or precision != 1 or world != 1 or clusters not in (0, 64):
         return None, None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_schur_pmc.json")))
     if not files:
@@ -286,7 +286,7 @@ def main():
         schur_src = ("device clock (s_memrealtime): the sum over the SCHUR launches (V^T X^-1, "
                      "V^T Y, pairs) of first workgroup start to last workgroup end, inside the "
                      "replayed graph, averaged over the timed region")
-    traffic, traffic_src = schur_pmc_traffic(args.config, args.precision, world)
+    traffic, traffic_src = schur_pmc_traffic(args.config, args.precision, world, args.clusters)
     achieved = fl / sch_s / 1e12   # in flops of the word type (multi-word flops when w > 1)
     peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]
     res = {

@@ -1,16 +1,25 @@
 #!/bin/bash
 # Round-end measurement set on the GPU box (run through gpurun from the repo root):
-#   bench lines C3 (default, with the CPU baseline), C2, C4 (C2 shape, double-double),
-#   C5 (sphere-packing shape, quad-double), then tools/profile_round.sh (kernel trace + the
-#   FETCH_SIZE / WRITE_SIZE passes of the Schur launches).  Outputs: gpurun_out/meas_$TAG/.
+#   1. tools/profile_round.sh: kernel trace + the FETCH_SIZE / WRITE_SIZE passes of the Schur
+#      launches; its counter summary is copied to profiles/${TAG}_schur_pmc.json first, so the
+#      bench lines below carry `traffic` from a counter pass of this very build;
+#   2. bench lines C3 (default, with the CPU baseline), C2, C4 (C2 shape, double-double),
+#      C5 (sphere-packing shape, quad-double);
+#   3. the C3 body at 8/16/32 clusters (the per-rank share of the strong-scaling shards).
+# Outputs: gpurun_out/meas_$TAG/ and gpurun_out/prof_$TAG/.
 set -euo pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 OUT=gpurun_out/meas_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+bash tools/profile_round.sh $TAG > $OUT/profile.log 2>&1
+cp gpurun_out/prof_$TAG/schur_pmc.json profiles/${TAG}_schur_pmc.json
+cp gpurun_out/prof_$TAG/schur_pmc.json $OUT/schur_pmc.json
 timeout -k 10 200 python3 bench.py > $OUT/bench_c3_fp64.log 2>&1
 timeout -k 10 200 python3 bench.py --config c2 > $OUT/bench_c2_fp64.log 2>&1
 timeout -k 10 200 python3 bench.py --config c2 --precision 2 > $OUT/bench_c4_dd.log 2>&1
 timeout -k 10 200 python3 bench.py --config c5 --precision 4 > $OUT/bench_c5_qd.log 2>&1
-bash tools/profile_round.sh $TAG > $OUT/profile.log 2>&1
+for c in 8 16 32; do
+  timeout -k 10 120 python3 bench.py --clusters $c --no-cpu --steps 300 > $OUT/clusters_$c.log 2>&1
+done
 echo done
