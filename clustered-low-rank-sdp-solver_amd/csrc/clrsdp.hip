@@ -513,23 +513,28 @@ struct MatPlan : PlanBase {  // potrf / eigmin
         return;
       }
     }
+    // CLRSDP_EIG_NEWTON=0 keeps the multi-word multisection from the fp64 bracket (A/B)
+    static const bool newton = [] {
+      const char* e = std::getenv("CLRSDP_EIG_NEWTON");
+      return !(e && e[0] == '0');
+    }();
     // multi-word: eigmin_lds2 (two barriers per column) unless CLRSDP_EIG_LDS1=1
     static const bool lds1 = std::getenv("CLRSDP_EIG_LDS1") != nullptr;
     if (!std::is_same<T, double>::value && !lds1 && eig2_lds_bytes<T>(nmax) <= LDS_MAX) {
-      static std::atomic<unsigned long long> attr2{0};
-      lds_attr_once(attr2, (const void*)eigmin_lds2<T, true>, (int)LDS_MAX);
-      eigmin_lds2<T, true><<<(unsigned)h.size(), 512, eig2_lds_bytes<T>(nmax), s>>>(d, out);
+      static std::atomic<unsigned long long> attr2{0}, attr2f{0};
+      if (newton) {
+        lds_attr_once(attr2, (const void*)eigmin_lds2<T, true>, (int)LDS_MAX);
+        eigmin_lds2<T, true><<<(unsigned)h.size(), 512, eig2_lds_bytes<T>(nmax), s>>>(d, out);
+      } else {
+        lds_attr_once(attr2f, (const void*)eigmin_lds2<T, false>, (int)LDS_MAX);
+        eigmin_lds2<T, false><<<(unsigned)h.size(), 512, eig2_lds_bytes<T>(nmax), s>>>(d, out);
+      }
       HIPCHK(hipGetLastError());
       return;
     }
     if (eig_lds_bytes<T>(nmax) <= LDS_MAX) {
       const size_t lds = eig_lds_bytes<T>(nmax);
       static std::atomic<unsigned long long> attr_t{0}, attr_f{0};
-      // CLRSDP_EIG_NEWTON=0 keeps the multi-word multisection from the fp64 bracket
-      static const bool newton = [] {
-        const char* e = std::getenv("CLRSDP_EIG_NEWTON");
-        return !(e && e[0] == '0');
-      }();
       lds_attr_once(attr_t, (const void*)eigmin_lds<T, true>, (int)LDS_MAX);
       lds_attr_once(attr_f, (const void*)eigmin_lds<T, false>, (int)LDS_MAX);
       if (newton) eigmin_lds<T, true><<<(unsigned)h.size(), 512, lds, s>>>(d, out);

@@ -877,34 +877,50 @@ __device__ void eig_multisection(const T* __restrict__ dg, const T* __restrict__
     }
   }
   __syncthreads();
-  if constexpr (NEWTON && Num<T>::BITS > 120) {
-    // (2') quad-double: Newton on det(T - sigma I) from the fp64 centre (at dd the 11 parallel
-    // multisection rounds are as fast as the sequential Newton chain, so dd keeps them).  With the pivots of
+  if constexpr (NEWTON && Num<T>::BITS > 60) {  // (multi-word words only)
+    // (2') Newton on det(T - sigma I) from the fp64 centre.  (Before round 3 only at qd: at dd the
+    // 11 parallel multisection rounds were as fast as the sequential chain of divisions.)  With the pivots of
     // T - sigma I = L D L^T, q_i = (d_i - sigma) - e2_{i-1} / q_{i-1}, and s_i = dq_i/dsigma =
     // -1 + e2_{i-1} s_{i-1} / q_{i-1}^2, the Newton step is 1 / sum_i s_i / q_i.  It converges
     // quadratically from the fp64 estimate (3 steps for a simple eigenvalue, a 4th confirms).
     // The result is accepted only if it converged AND two multi-word Sturm counts bracket it
     // (no eigenvalue below sigma - delta, one at most sigma + delta, delta = 2^(12-BITS)
     // magnitudes); otherwise the multisection below runs as before.
+    // Division-free (round 3): the step is p_n / p_n' with the three-term recurrence of the
+    // leading principal minors and of their derivatives, p_i = (d_i - s) p_{i-1} - e2_{i-1}
+    // p_{i-2}, p_i' = (d_i - s) p_{i-1}' - p_{i-1} - e2_{i-1} p_{i-2}', the four values rescaled
+    // by one power of two per row (exact, the ratio is unchanged): four multi-word products per
+    // row and one division per step, against a division and three products per row.  A step
+    // below 2^(-BITS/2 - 24) of the magnitude is the last one (quadratic convergence puts the
+    // next correction far below the word); the two Sturm counts below accept the result.
     T* nres = Wv;  // free after the reduction: [0] = sigma
     const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
     if (tid == 0) {
       T s = T(0.5 * (bnd[2] + bnd[3]));
-      const double tol = ldexp(mag, -(Num<T>::BITS + 2)) + 1e-300;
+      const double tol = ldexp(mag, -(Num<T>::BITS / 2 + 24)) + 1e-300;
       int conv = 0;
       for (int it = 0; it < 4; ++it) {
-        T q = dg[0] - s;
-        if (q == T(0.0)) q = T(1e-300);
-        T r = T(1.0) / q, sd = T(-1.0), g = -r;
+        T pm = T(1.0), pc = dg[0] - s, dm = T(0.0), dc = T(-1.0);
         for (int i = 1; i < n; ++i) {
-          const T t = e2[i - 1] * r;
-          sd = (t * r) * sd - T(1.0);
-          q = (dg[i] - s) - t;
-          if (q == T(0.0)) q = T(1e-300);
-          r = T(1.0) / q;
-          g = g + sd * r;
+          const T t = dg[i] - s;
+          const T pn = t * pc - e2[i - 1] * pm;
+          const T dn = (t * dc - pc) - e2[i - 1] * dm;
+          pm = pc;
+          pc = pn;
+          dm = dc;
+          dc = dn;
+          const double mx = fmax(fmax(fabs(Num<T>::hi(pc)), fabs(Num<T>::hi(pm))),
+                                 fmax(fabs(Num<T>::hi(dc)), fabs(Num<T>::hi(dm))));
+          if (mx > 0.0 && mx < INFINITY) {
+            const int ex = __builtin_amdgcn_frexp_exp(mx);
+            pc = scale2(pc, -ex);
+            pm = scale2(pm, -ex);
+            dc = scale2(dc, -ex);
+            dm = scale2(dm, -ex);
+          }
         }
-        const T step = T(1.0) / g;
+        if (Num<T>::hi(dc) == 0.0) break;
+        const T step = pc / dc;
         s = s - step;
         const double as = fabs(Num<T>::hi(step));
         if (!(as == as)) break;  // NaN: leave conv = 0
