@@ -411,25 +411,35 @@ void GemmPlan<T>::launch_uni_impl(hipStream_t s, double alpha, double beta, cons
 
 template <class T>
 struct TrsmPlan : PlanBase {
-  static constexpr int NB = 16, NC = 64;
+  // NC: right-hand sides per workgroup.  Multi-word solves with many right-hand sides
+  // (W = L^-1 B) take 16 (one diagonal pass of 256 threads, and four times the workgroups of 64:
+  // the panel update's multi-word products spread over more CUs); CLRSDP_TRSM_NC64=1 keeps 64.
+  static constexpr int NB = 16, NCW = 64, NCN = 16;
   std::vector<TrsmDesc<T>> h;
   std::vector<int> t2d;
   TrsmDesc<T>* d = nullptr;
   int* dt = nullptr;
   int nmax = 0, rmax = 0;
+  bool narrow = false;
   void add(const T* L, int ldl, T* B, int ldb, int n, int nrhs) {
     if (n <= 0 || nrhs <= 0) return;
     rmax = std::max(rmax, nrhs);
     TrsmDesc<T> t;
     t.L = L; t.B = B; t.n = n; t.nrhs = nrhs; t.ldl = ldl; t.ldb = ldb;
-    t.tile0 = (int)t2d.size();
+    t.tile0 = 0;
     t.pad = 0;
-    for (int i = 0; i < (int)cdiv(nrhs, NC); ++i) t2d.push_back((int)h.size());
     h.push_back(t);
     nmax = std::max(nmax, n);
   }
   void finalize() {
     if (h.empty()) return;
+    narrow = mode == 0 && !std::is_same<T, double>::value && rmax >= 32 && !std::getenv("CLRSDP_TRSM_NC64");
+    const int nc = narrow ? NCN : NCW;
+    t2d.clear();
+    for (size_t q = 0; q < h.size(); ++q) {
+      h[q].tile0 = (int)t2d.size();
+      for (int i = 0; i < (int)cdiv(h[q].nrhs, nc); ++i) t2d.push_back((int)q);
+    }
     d = own(h);
     dt = own(t2d);
   }
@@ -438,8 +448,16 @@ struct TrsmPlan : PlanBase {
   int mode = 0;
   void launch(hipStream_t s, bool trans) const {
     if (h.empty()) return;
+    constexpr int NC = NCW;
     const size_t lds = sizeof(T) * ((size_t)NB * NB + (size_t)NB * NC + (size_t)NB * nmax);
     const unsigned grid = (unsigned)t2d.size();
+    if (narrow && mode == 0) {
+      const size_t ldsn = sizeof(T) * ((size_t)NB * NB + (size_t)NB * NCN + (size_t)NB * nmax);
+      if (trans) trsm_batched<T, true, NB, NCN, 256><<<grid, 256, ldsn, s>>>(d, dt);
+      else trsm_batched<T, false, NB, NCN, 256><<<grid, 256, ldsn, s>>>(d, dt);
+      HIPCHK(hipGetLastError());
+      return;
+    }
     if (mode == 1 && !trans) {
       trsm_batched<T, false, NB, NC, 256, true, false><<<grid, 256, lds, s>>>(d, dt);
       HIPCHK(hipGetLastError());
