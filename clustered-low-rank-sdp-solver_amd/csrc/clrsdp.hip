@@ -790,6 +790,7 @@ struct Solver final : HandleBase {
   // schur_fused_f64 (every local block delta <= 128): V^T X^-1 formed on chip, one workgroup
   // per 64-row block; CLRSDP_SCHUR_FUSED=0 keeps the V^T X^-1 GEMM + schur_pairs_f64 pair
   bool schur_fused = false;
+  bool fused_y = false;  // schur_fused_f64<0, true>: V^T Y on chip too (no p_ty); CLRSDP_SCHUR_FUSED_Y=0
   FusedPairDesc* d_fpd = nullptr;
   TileRef* d_fpt2d = nullptr;
   int n_fwg = 0;
@@ -1354,8 +1355,9 @@ struct Solver final : HandleBase {
           if (b.K == 0) continue;
           const PairTileDesc& t = ptd[q++];
           FusedPairDesc f;
-          f.Vt = t.Vt; f.Xinv = Xinv + b.off; f.TYt = t.TYt; f.lam = t.lam; f.G = t.G; f.AY = t.AY;
-          f.K = t.K; f.del = t.del; f.ldG = t.ldG; f.ldx = b.n;
+          f.Vt = t.Vt; f.Xinv = Xinv + b.off; f.TYt = t.TYt; f.Y = Y + b.off; f.lam = t.lam;
+          f.G = t.G; f.AY = t.AY;
+          f.K = t.K; f.del = t.del; f.ldG = t.ldG; f.ldx = b.n; f.ldy = b.n;
           fpd.push_back(f);
           fnt.push_back(cdiv(b.K, 64));
         }
@@ -1363,9 +1365,11 @@ struct Solver final : HandleBase {
         n_fwg = (int)ft2d.size();
         d_fpd = descs.own(fpd);
         d_fpt2d = descs.own(ft2d);
-        HIPCHK(hipFuncSetAttribute((const void*)schur_fused_f64<0>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)schur_fused::LDS));
+        const char* efy = std::getenv("CLRSDP_SCHUR_FUSED_Y");
+        fused_y = !(efy && efy[0] == '0');
+        for (const void* k : {(const void*)schur_fused_f64<0>, (const void*)schur_fused_f64<0, true>})
+          HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)schur_fused::LDS));
       }
       n_gsum = (int)gcd.size();
       if (n_gsum) d_gcd = descs.own(gcd);
@@ -1746,10 +1750,12 @@ struct Solver final : HandleBase {
         if (ty_ahead) {  // V^T Y came from the side stream
           HIPCHK(hipStreamWaitEvent(stream, ev_ty, 0));
           ty_ahead = false;
-        } else {
+        } else if (!(schur_fused && fused_y)) {
           p_ty.launch(stream, 1.0, 0.0);
         }
-        if (schur_fused)
+        if (schur_fused && fused_y)
+          schur_fused_f64<0, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4);
+        else if (schur_fused)
           schur_fused_f64<0><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4);
         else if (n_ptiles)
           schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d, stamps + 4);
@@ -2219,7 +2225,7 @@ struct Solver final : HandleBase {
     side(ev_m, [&] {
       // V^T Y of the Schur stage only needs the state: it runs beside chol_inv(X, Y), which leaves
       // half the CUs idle, and SCHUR waits for it (ev_ty) before the pairs launch
-      if (fast_schur && !p_ty.h.empty() && exp_knob != 4) {
+      if (fast_schur && !p_ty.h.empty() && exp_knob != 4 && !(schur_fused && fused_y)) {
         p_ty.launch(stream, 1.0, 0.0);
         HIPCHK(hipEventRecord(ev_ty, stream));
         ty_ahead = true;

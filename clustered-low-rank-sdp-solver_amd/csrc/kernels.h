@@ -1507,11 +1507,12 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
 struct FusedPairDesc {
   const double* Vt;    // K x delta, ld K
   const double* Xinv;  // delta x delta, ld ldx
-  const double* TYt;   // K x delta, ld K
+  const double* TYt;   // K x delta, ld K (YV = false)
+  const double* Y;     // delta x delta, ld ldy (YV = true: TYt_a = V_a^T Y formed on chip)
   const double* lam;   // K
   double* G;           // K x K, ld ldG
   double* AY;          // K
-  int K, del, ldG, ldx;
+  int K, del, ldG, ldx, ldy;
 };
 namespace schur_fused {
 constexpr int BK = 32;                  // phase-1 k-slab
@@ -1520,12 +1521,17 @@ constexpr int FR = 32 * 4 * 64;         // fragment-ordered 128 x 64 operand (TY
 constexpr int YR = 0, VR = FR, SR = 2 * FR, END = 2 * FR + 64 * 64;
 static_assert(BK * LA + BK * LBV <= FR && BK * LA + BK * LBV <= END - VR,
               "phase-1 images fit in the TYt_a region and in the V_b + staging regions");
+constexpr int P1Y = 2 * BK * LA + BK * LBV;  // YV: one image of the X^-1, Y and V_a slabs
+static_assert(P1Y <= END, "YV phase-1 image fits");
 constexpr size_t LDS = sizeof(double) * END;  // 160 KB
 __device__ __forceinline__ int st_idx(int row, int col) { return row * 64 + (col ^ (row & 31)); }
 }  // namespace schur_fused
 
-// DBG (timing experiments only): 1 = no phase-2 MFMAs, 2 = no phase-1 MFMAs
-template <int DBG = 0>
+// DBG (timing experiments only): 1 = no phase-2 MFMAs, 2 = no phase-1 MFMAs.
+// YV: phase 1 also forms TYt_a^T = Y V_a (sharing the V_a slab; one single-buffered image of
+// the three slabs), whose accumulators are written straight into the fragment-ordered TYt_a
+// region -- no V^T Y GEMM and no K x delta round trip through HBM for it either.
+template <int DBG = 0, bool YV = false>
 __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __restrict__ descs,
                                                        const TileRef* __restrict__ t2d,
                                                        unsigned long long* stamp = nullptr) {
@@ -1544,16 +1550,19 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nt = w & 3, h = w >> 2, lr = lane & 15, lk = lane >> 4;
   const int nb = (T % 2 == 0 && a >= T / 2) ? T / 2 : T / 2 + 1;  // tiles of this workgroup
-  // ---------------- phase 1: C' = X^-1 V_a
-  d4 c1[4];
+  // ---------------- phase 1: C' = X^-1 V_a (and Y V_a)
+  d4 c1[4], c1y[YV ? 4 : 1];
 #pragma unroll
   for (int q = 0; q < 4; ++q) c1[q] = d4{0.0, 0.0, 0.0, 0.0};
-  double ra[8], rb[4];
+#pragma unroll
+  for (int q = 0; q < (YV ? 4 : 1); ++q) c1y[q] = d4{0.0, 0.0, 0.0, 0.0};
+  double ra[8], rb[4], ryy[YV ? 8 : 1];
   auto load1 = [&](int k0) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {  // X^-1 (i, k'): i = e % 128 contiguous
       const int e = tid + 512 * q, i = e & 127, k = k0 + (e >> 7);
       ra[q] = gload(d.Xinv + min(i, D - 1) + (size_t)min(k, D - 1) * d.ldx);
+      if constexpr (YV) ryy[q] = gload(d.Y + min(i, D - 1) + (size_t)min(k, D - 1) * d.ldy);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // V_a (k', j) = Vt[a0 + j + k' K]
@@ -1561,16 +1570,19 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
       rb[q] = gload(d.Vt + min(a0 + j, K - 1) + (size_t)min(k, D - 1) * K);
     }
   };
+  // image layout: X^-1 slab [k][LA], (YV: Y slab [k][LA]), V_a slab [k][LBV]
+  constexpr int VOFF = (YV ? 2 : 1) * BK * LA;
   auto store1 = [&](double* S, int k0) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int e = tid + 512 * q, i = e & 127, k = e >> 7;
       S[k * LA + i] = (i < D && k0 + k < D) ? ra[q] : 0.0;
+      if constexpr (YV) S[BK * LA + k * LA + i] = (i < D && k0 + k < D) ? ryy[q] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tid + 512 * q, j = e & 63, k = e >> 6;
-      S[BK * LA + k * LBV + j] = k0 + k < D ? rb[q] : 0.0;
+      S[VOFF + k * LBV + j] = k0 + k < D ? rb[q] : 0.0;
     }
   };
   // V_b element (k, j) = Vt[b0 + j + k K]: thread element e = tid + 512 q is (k = e >> 6,
@@ -1621,22 +1633,37 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       if (DBG == 2) break;
-      const double bf = S[BK * LA + (kk + lk) * LBV + 16 * nt + lr];
+      const double bf = S[VOFF + (kk + lk) * LBV + 16 * nt + lr];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const double af = S[(kk + lk) * LA + 16 * (4 * h + q) + lr];
         c1[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, c1[q], 0, 0, 0);
+        if constexpr (YV) {
+          const double ay = S[BK * LA + (kk + lk) * LA + 16 * (4 * h + q) + lr];
+          c1y[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, bf, c1y[q], 0, 0, 0);
+        }
       }
     }
     if (!more) break;
-    img ^= 1;
-    store1(P1(img), k0 + BK);  // (the other image was last read before the previous barrier)
+    if constexpr (YV) {  // one image: wait for every wave before overwriting it
+      __syncthreads();
+      store1(P1(0), k0 + BK);
+    } else {
+      img ^= 1;
+      store1(P1(img), k0 + BK);  // (the other image was last read before the previous barrier)
+    }
     __syncthreads();
   }
   // phase 2's first operands load during the swap of the K halves (through the V_b region)
-  loady();
+  if constexpr (!YV) loady();
   loadv(a);
   __syncthreads();  // every wave is done with the last phase-1 image
+  if constexpr (YV) {  // TYt_a fragments straight from the accumulators (tile (mt, nt), mt = 4h + q)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Yf[(nt * 32 + 4 * (4 * h + q) + r) * 64 + lane] = c1y[q][r];
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1653,7 +1680,7 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     for (int r = 0; r < 4; ++r)
       tf[4 * mt + r] = (mt >> 2) == h ? c1[mt & 3][r] : Vf[((wp * 4 + (mt & 3)) * 4 + r) * 64 + lane];
   __syncthreads();
-  storey();
+  if constexpr (!YV) storey();
   storev();
   __syncthreads();
   const double* yrow = Yf + nt * 32 * 64 + lane;     // chunk c at yrow[64 c]

@@ -63,6 +63,7 @@ int main() {
     FusedPairDesc f;
     f.Vt = t.Vt; f.Xinv = Xi + (size_t)j * D * D; f.TYt = t.TYt; f.lam = t.lam;
     f.G = G1 + (size_t)j * K * K; f.AY = AY1 + (size_t)j * K; f.K = K; f.del = D; f.ldG = K; f.ldx = D;
+    f.Y = Xi + (size_t)j * D * D; f.ldy = D;  // (any symmetric matrix: timing only)
     fd.push_back(f);
   }
   std::vector<TileRef> pt, ft;
@@ -75,7 +76,7 @@ int main() {
   CK(hipMemcpy(dfd, fd.data(), fd.size() * sizeof(fd[0]), hipMemcpyHostToDevice));
   CK(hipMemcpy(dpt, pt.data(), pt.size() * sizeof(TileRef), hipMemcpyHostToDevice));
   CK(hipMemcpy(dft, ft.data(), ft.size() * sizeof(TileRef), hipMemcpyHostToDevice));
-  for (auto k : {(const void*)schur_fused_f64<0>, (const void*)schur_fused_f64<1>, (const void*)schur_fused_f64<2>})
+  for (auto k : {(const void*)schur_fused_f64<0>, (const void*)schur_fused_f64<1>, (const void*)schur_fused_f64<2>, (const void*)schur_fused_f64<0, true>})
     CK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)schur_fused::LDS));
   const unsigned gg = (unsigned)(J * 4 * 2);
   const float tg = timeit([&] { gemm_f64_uni<false, true, 0, 32, 8, false, false, true><<<gg, 512>>>(u, 1.0, 0.0); });
@@ -87,6 +88,8 @@ int main() {
   const float tf = timeit([&] { schur_fused_f64<0><<<(unsigned)ft.size(), 512, schur_fused::LDS>>>(dfd, dft, nullptr); });
   const float t1 = timeit([&] { schur_fused_f64<1><<<(unsigned)ft.size(), 512, schur_fused::LDS>>>(dfd, dft, nullptr); });
   const float t2 = timeit([&] { schur_fused_f64<2><<<(unsigned)ft.size(), 512, schur_fused::LDS>>>(dfd, dft, nullptr); });
+  const float ty = timeit([&] { schur_fused_f64<0, true><<<(unsigned)ft.size(), 512, schur_fused::LDS>>>(dfd, dft, nullptr); });
+  printf("fused with V^T Y on chip (YV): %.2f us\n", ty);
   // check
   CK(hipMemset(G1, 0, nG * 8));
   schur_fused_f64<0><<<(unsigned)ft.size(), 512, schur_fused::LDS>>>(dfd, dft, nullptr);
