@@ -7,10 +7,10 @@ Usage (on the GPU box, each counter in its own pass as MI355X_MICROARCH.md presc
     python3 tools/pmc_traffic.py gpurun_out/pmc/f/run_counter_collection.csv \
         gpurun_out/pmc/w/run_counter_collection.csv profiles/r01_schur_pmc.json
 
-FETCH_SIZE / WRITE_SIZE are in KB per dispatch.  The Schur stage is the TYt GEMM
-(gemm_f64_uni / gemm_f64_lds <false, true, 3, ...>, TAG 3, run ahead on the side stream) and
-schur_fused_f64 (round 3), or, with CLRSDP_SCHUR_FUSED=0, the TXt GEMM (TAG 1) and
-schur_pairs_f64.  Reported:
+FETCH_SIZE / WRITE_SIZE are in KB per dispatch.  The Schur stage is schur_fused_f64 alone
+(round 3: V^T X^-1 and V^T Y formed on chip); with CLRSDP_SCHUR_FUSED_Y=0 also the TYt GEMM
+(gemm_f64_uni / gemm_f64_lds <false, true, 3, ...>, TAG 3, ahead on the side stream), and with
+CLRSDP_SCHUR_FUSED=0 the TXt GEMM (TAG 1), the TYt GEMM and schur_pairs_f64.  Reported:
 the per-launch mean of each and their sum per iteration, in bytes.  gfx950 correction: the guide
 measured FETCH_SIZE = 1/2 of the bytes for 16-B-per-lane streaming reads; these kernels read
 8 B per lane (global_load_dwordx2), a width the guide calls uncalibrated, so the raw counter and
