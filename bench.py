@@ -283,9 +283,10 @@ def main():
     schur_src = "instrumented pass (per-stage events, no graph)"
     if schur_live[1] and schur_live[0] > 0.0:   # (the clock stamps exist on the fused fp64 path)
         sch_s = schur_live[0] / 1e3 / schur_live[1]
-        schur_src = ("device clock (s_memrealtime): the sum over the SCHUR launches (V^T X^-1, "
-                     "V^T Y, pairs) of first workgroup start to last workgroup end, inside the "
-                     "replayed graph, averaged over the timed region")
+        schur_src = ("device clock (s_memrealtime): the sum over the SCHUR launches (at C3 the "
+                     "one schur_fused_f64 launch; otherwise the V^T X^-1 and V^T Y GEMMs and the "
+                     "pairs) of first workgroup start to last workgroup end, inside the replayed "
+                     "graph, averaged over the timed region")
     traffic, traffic_src = schur_pmc_traffic(args.config, args.precision, world, args.clusters)
     achieved = fl / sch_s / 1e12   # in flops of the word type (multi-word flops when w > 1)
     peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]
