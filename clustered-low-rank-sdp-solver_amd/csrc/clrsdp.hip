@@ -145,6 +145,35 @@ template <class T> struct RegCfg { static constexpr int TR = 4, TC = 8, GR = 32,
 template <> struct RegCfg<dd> { static constexpr int TR = 1, TC = 4, GR = 64, GC = 16; };  // 1024 threads
 template <> struct RegCfg<qd> { static constexpr int TR = 1, TC = 1, GR = 32, GC = 32; };  // 1024 threads
 template <class T> constexpr int reg_nmax() { return std::is_same<T, double>::value ? 128 : RegCfg<T>::TR * RegCfg<T>::GR; }
+// multi-word blocks n <= 64 factor with chol_packed (liveness-packed slots, bitwise the same
+// factors as chol_inv_reg); CLRSDP_CHOL_PACKED=0 keeps the tile grid (A/B)
+inline bool chol_packed_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("CLRSDP_CHOL_PACKED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// quad-double factors in the square-root-free form (chol_packed LDL); CLRSDP_CHOL_LDL=0: LL^T
+inline bool chol_ldl_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("CLRSDP_CHOL_LDL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+template <class T, bool INV>
+void launch_chol_packed(unsigned nb, hipStream_t s, const MatDesc<T>* in, const MatDesc<T>* oi,
+                        const MatDesc<T>* ol, int* info) {
+  constexpr int NT = 1024;
+  if constexpr (std::is_same<T, mw::qd>::value) {
+    if (chol_ldl_on()) {
+      chol_packed<T, NT, INV, true><<<nb, NT, 0, s>>>(in, oi, ol, info);
+      return;
+    }
+  }
+  chol_packed<T, NT, INV, false><<<nb, NT, 0, s>>>(in, oi, ol, info);
+}
 // eigmin_lds: A (n^2), v, NC = 8 (n <= 64) or 4 partial vectors, dg, e2, w, scalars
 template <class T> size_t eig_lds_bytes(int n) {
   return sizeof(T) * ((size_t)n * n + (n <= 64 ? 14 : 10) * (size_t)n + 40);
@@ -510,7 +539,10 @@ struct MatPlan : PlanBase {  // potrf / eigmin
     if (h.empty()) return;
     if constexpr (!std::is_same<T, double>::value) {
       if (reg_potrf) {
-        chol_inv_reg<T, 1, 4, 64, 16, false><<<(unsigned)h.size(), 1024, 0, s>>>(d, d, d, info);
+        if (chol_packed_on())
+          launch_chol_packed<T, false>((unsigned)h.size(), s, d, d, d, info);
+        else
+          chol_inv_reg<T, 1, 4, 64, 16, false><<<(unsigned)h.size(), 1024, 0, s>>>(d, d, d, info);
         HIPCHK(hipGetLastError());
         return;
       }
@@ -643,7 +675,10 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
       else go<128>(s, nb, info);
     } else {
       using C = RegCfg<T>;
-      chol_inv_reg<T, C::TR, C::TC, C::GR, C::GC><<<nb, C::GR * C::GC, 0, s>>>(din, dout, dl, info);
+      if (chol_packed_on() && nmax <= 64)
+        launch_chol_packed<T, true>(nb, s, din, dout, dl, info);
+      else
+        chol_inv_reg<T, C::TR, C::TC, C::GR, C::GC><<<nb, C::GR * C::GC, 0, s>>>(din, dout, dl, info);
     }
     HIPCHK(hipGetLastError());
   }

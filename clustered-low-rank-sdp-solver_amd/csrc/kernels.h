@@ -753,11 +753,30 @@ __device__ inline void pivot_sqrt<mw::dd>(const mw::dd& d, mw::dd& s, mw::dd& r)
 
 template <>
 __device__ inline void pivot_sqrt<mw::qd>(const mw::qd& d, mw::qd& s, mw::qd& r) {
-  // sqrt_qd's Newton iteration on 1/sqrt(d) (three steps from the fp64 value), kept: r itself
-  // is the reciprocal, so no quad-double division follows
+  // Newton on 1/sqrt(d), r += r (1 - d r^2) / 2, with precision doubling: fp64 (hardware rsq and
+  // two fp64 steps, ~53 bits), one double-double step (~104 bits), then two steps whose residual
+  // e = 1 - d r^2 is quad-double and whose correction r e / 2 (|e| < 2^-100) is double-double.
+  // The second quad-double step also absorbs the double-double rounding of the first.  Four
+  // quad-double products and s = d r on the factorisations' serial pivot chain, against nine
+  // and s for three full quad-double steps (CLRSDP_QD_PIVOT_FULL: those, for A/B).
+#ifdef CLRSDP_QD_PIVOT_FULL
   const mw::qd h = d * 0.5;
   r = mw::qd(1.0 / sqrt(d.x[0]));
   for (int it = 0; it < 3; ++it) r = r + r * (mw::qd(0.5) - h * (r * r));
+#else
+  double r0 = __builtin_amdgcn_rsq(d.x[0]);
+  r0 = r0 * fma(-0.5 * d.x[0], r0 * r0, 1.5);
+  r0 = r0 * fma(-0.5 * d.x[0], r0 * r0, 1.5);
+  const mw::dd d2(d.x[0], d.x[1]);
+  mw::dd r2(r0);
+  r2 = r2 + (r2 * (mw::dd(1.0) - d2 * (r2 * r2))) * 0.5;
+  r = mw::qd(r2);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const mw::qd e = mw::qd(1.0) - d * (r * r);
+    r = r + mw::qd((mw::dd(r.x[0], r.x[1]) * mw::dd(e.x[0], e.x[1])) * 0.5);
+  }
+#endif
   s = d * r;
 }
 // 1/q: double-double from the hardware reciprocal (two fp64 Newton steps) and one
@@ -772,6 +791,23 @@ __device__ inline mw::dd recip_fast<mw::dd>(const mw::dd& q) {
   const mw::dd rr(r0);
   const mw::dd e = mw::dd(1.0) - q * rr;
   return rr + rr * e;
+}
+// 1/q at quad-double: the double-double reciprocal of the leading limbs, then two Newton steps
+// r += r (1 - q r) with a quad-double residual and a double-double correction (as pivot_sqrt):
+// two quad-double products against the long division's chain of quad-double x double steps
+template <>
+__device__ inline mw::qd recip_fast<mw::qd>(const mw::qd& q) {
+#ifdef CLRSDP_QD_PIVOT_FULL
+  return mw::qd(1.0) / q;
+#else
+  mw::qd r(recip_fast(mw::dd(q.x[0], q.x[1])));
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const mw::qd e = mw::qd(1.0) - q * r;
+    r = r + mw::qd(mw::dd(r.x[0], r.x[1]) * mw::dd(e.x[0], e.x[1]));
+  }
+  return r;
+#endif
 }
 
 template <class T, int NB, int NT = 256>
@@ -867,8 +903,11 @@ __global__ __launch_bounds__(NT) void potrf_batched(const MatDesc<T>* __restrict
 // of getrf_batched: forward U^T x = b (B^T U^-1, MPMP.jl:1457-1460) and, with TRANS, backward
 // U x = b (approx_solve_triu!, MPMP.jl:1772).
 // One workgroup per (matrix, NC-column tile of B); NB-row blocks; L panel staged in LDS.  The
-// diagonal enters as reciprocals (one division per row, not per right-hand side: a multi-word
-// division is an order of magnitude dearer than a product).
+// diagonal enters as reciprocals (one per row, not per right-hand side: a multi-word division
+// is an order of magnitude dearer than a product; multi-word words take recip_fast's Newton
+// form).  Multi-word words also pre-scale the diagonal block's off-diagonal entries by those
+// reciprocals (column q by 1/l_qq; transposed: row q), so that the serial chain of the block
+// solve carries one product per row (v_r -= l_rq/l_qq v_q) and x_q = v_q/l_qq leaves it.
 // ------------------------------------------------------------------------------------------
 template <class T, bool TRANS, int NB, int NC, int NT = 256, bool UNIT = false, bool STORE_T = false>
 __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict__ descs,
@@ -885,6 +924,7 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
   const T* L = d.L;
   const size_t ldl = d.ldl;
   auto lat = [&](int i, int j) -> T { return STORE_T ? L[j + (size_t)i * ldl] : L[i + (size_t)j * ldl]; };
+  constexpr bool PS = !UNIT && !std::is_same<T, double>::value;  // pre-scaled diagonal block
   T* B = d.B + (size_t)c0 * d.ldb;
   const int nblk = (n + NB - 1) / NB;
   for (int bi = 0; bi < nblk; ++bi) {
@@ -894,7 +934,14 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
       const int i = e % nb, j = e / nb;
       D[i + j * NB] = lat(i0 + i, i0 + j);
     }
-    if (tid < nb) rdg[tid] = UNIT ? T(1.0) : T(1.0) / lat(i0 + tid, i0 + tid);
+    if (tid < nb) rdg[tid] = UNIT ? T(1.0) : recip_fast(lat(i0 + tid, i0 + tid));
+    if constexpr (PS) {
+      __syncthreads();
+      for (int e = tid; e < nb * nb; e += blockDim.x) {
+        const int i = e % nb, j = e / nb;
+        if (i > j) D[i + j * NB] = D[i + j * NB] * rdg[TRANS ? i : j];
+      }
+    }
     // panel of the rows still to be updated
     const int pr0 = TRANS ? 0 : i0 + nb;
     const int pm = TRANS ? i0 : n - i0 - nb;
@@ -914,7 +961,18 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
       const bool act = r < nb && c < nc;
       T v = act ? B[(i0 + r) + (size_t)c * d.ldb] : T(0.0);
       T xr = T(0.0);
-      if (!TRANS) {
+      if constexpr (PS) {
+        // v_q is final once the steps before q have run: broadcast it, scale it off the chain
+#pragma unroll
+        for (int qq = 0; qq < NB; ++qq) {
+          const int q = TRANS ? NB - 1 - qq : qq;
+          if (q < nb) {
+            const T vq = shfl_t(v, base + q);
+            if (r == q) xr = v * rdg[q];
+            if (TRANS ? r < q : r > q) v = v - (TRANS ? D[q + r * NB] : D[r + q * NB]) * vq;
+          }
+        }
+      } else if (!TRANS) {
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
           if (q < nb) {

@@ -179,6 +179,194 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
 }
 
 // ------------------------------------------------------------------------------------------
+// chol_packed: the column steps of chol_inv_reg for multi-word blocks n <= 64, with the elements
+// placed by the steps at which they are live instead of on a fixed tile grid.  The lower
+// triangle of A is numbered column-major (element (r, c) is updated at the steps j < c) and cut
+// into 64-element slots; L^-1 (element (r, c) updated at the steps c <= j < r) is cut into 8 x 8
+// tiles on and below the diagonal.  Slot s is register s / NW of wave s % NW, and a wave skips a
+// slot (uniform branch) outside its live steps.  The waves then issue about n^3/384 multi-word
+// FMAs for A instead of the grid's ~n^2/2 (a grid wave stays busy while any of its 64 rows is
+// live) -- at quad-double one FMA is ~225 fp64 instructions.  With LDL = false every element goes
+// through the same operations in the same order as in chol_inv_reg, so L and L^-1 are bitwise
+// the same.
+// LDL = true (quad-double): the square-root-free form A = U D U^T (U unit lower), so that the
+// serial chain per column carries one reciprocal 1/d_j (two quad-double products) instead of a
+// square root and its reciprocal (five); L = U D^1/2 and L^-1 = D^-1/2 U^-1 follow at the end
+// with all n square roots side by side.  The factors then differ from chol_inv_reg's in the
+// last bits only.
+// ------------------------------------------------------------------------------------------
+template <class T, int NT, bool INV, bool LDL = false>
+__global__ __launch_bounds__(NT) void chol_packed(const MatDesc<T>* __restrict__ in,
+                                                  const MatDesc<T>* __restrict__ out_inv,
+                                                  const MatDesc<T>* __restrict__ out_l,
+                                                  int* __restrict__ info) {
+  constexpr int NMAX = 64, NW = NT / 64;
+  constexpr int SA = (NMAX * (NMAX + 1) / 2 + 63) / 64;  // 33 slots of A at n = 64
+  constexpr int SX = (NMAX / 8) * (NMAX / 8 + 1) / 2;     // 36 tiles of L^-1
+  constexpr int KA = (SA + NW - 1) / NW, KX = INV ? (SX + NW - 1) / NW : 1;
+  __shared__ T col[NMAX];   // column j of L (LDL: of U)
+  __shared__ T row[NMAX];   // row j of L^-1 (LDL: of U^-1)
+  __shared__ T colu[LDL ? NMAX : 1];  // LDL: column j of the trailing matrix, unscaled
+  __shared__ T dgl[LDL ? NMAX : 1];   // LDL: the pivots d_j
+  __shared__ T sd, rsd;
+  __shared__ int fail;
+  const MatDesc<T> d = in[blockIdx.x];
+  const int n = d.n, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  auto wave_max = [](int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return __builtin_amdgcn_readfirstlane(v);
+  };
+  // A: slot w + NW k, element e = 64 slot + lane of the column-major lower triangle
+  T a[KA];
+  int ar[KA], ac[KA], alo[KA], ahi[KA];  // (ar, ac) = -1: no element; [alo, ahi] slot columns
+  const int ne = n * (n + 1) / 2;
+#pragma unroll
+  for (int k = 0; k < KA; ++k) {
+    const int e = 64 * (w + NW * k) + lane;
+    int r = -1, c = -1;
+    if (e < ne) {
+      int rem = e;
+      c = 0;
+      while (rem >= n - c) {
+        rem -= n - c;
+        ++c;
+      }
+      r = c + rem;
+    }
+    ar[k] = r;
+    ac[k] = c;
+    a[k] = c >= 0 ? d.A[r + (size_t)c * d.lda] : T(0.0);
+    ahi[k] = wave_max(c);
+    alo[k] = -wave_max(c >= 0 ? -c : -NMAX);
+  }
+  // L^-1: tile w + NW k of the column-major 8 x 8 tiles (R >= C); lane (r, c) = (8R + l%8, 8C + l/8)
+  T x[KX];
+  int xr[KX], xc[KX], xR[KX], xC[KX];  // xR = -1: no tile
+  if constexpr (INV) {
+    const int nt8 = (n + 7) / 8;
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+      int t = w + NW * k, C = 0;
+      while (C < nt8 && t >= nt8 - C) {
+        t -= nt8 - C;
+        ++C;
+      }
+      const bool tv = C < nt8;
+      const int R = C + t;
+      xR[k] = tv ? R : -1;
+      xC[k] = tv ? C : 0;
+      const int r = 8 * R + (lane & 7), c = 8 * C + (lane >> 3);
+      const bool v = tv && r < n && c < n;
+      xr[k] = v ? r : -1;
+      xc[k] = v ? c : NMAX;
+      x[k] = (v && r == c) ? T(1.0) : T(0.0);
+    }
+  }
+  // the pivot of column jp from its (updated) diagonal entry dn: sd = sqrt, rsd = 1/sqrt (LDL:
+  // dgl[jp] = dn, rsd = 1/dn)
+  auto pivot = [&](int jp, const T& dn) {
+    if (!(dn > T(0.0))) fail = jp + 1;
+    if constexpr (LDL) {
+      dgl[jp] = dn;
+      rsd = recip_fast(dn);
+    } else {
+      pivot_sqrt(dn, sd, rsd);
+    }
+  };
+  if (tid == 0) {
+    fail = 0;
+    pivot(0, d.A[0]);
+  }
+  __syncthreads();
+  for (int j = 0; j < n; ++j) {
+    if (fail) break;
+    const T s = sd, rs = rsd;
+    // column j of L -> col[] (LDL: of U, and the unscaled column -> colu[]), row j of L^-1 -> row[]
+#pragma unroll
+    for (int k = 0; k < KA; ++k)
+      if (alo[k] <= j && j <= ahi[k] && ac[k] == j) {
+        if constexpr (LDL) {
+          if (ar[k] > j) {  // (the diagonal keeps d_j; dgl holds it)
+            const T u = a[k];
+            a[k] = u * rs;
+            col[ar[k]] = a[k];
+            colu[ar[k]] = u;
+          }
+        } else {
+          const T l = (ar[k] == j) ? s : a[k] * rs;
+          a[k] = l;
+          col[ar[k]] = l;
+        }
+      }
+    if constexpr (INV) {
+#pragma unroll
+      for (int k = 0; k < KX; ++k)
+        if (xR[k] == (j >> 3) && xr[k] == j && xc[k] <= j) {
+          if constexpr (!LDL) x[k] = x[k] * rs;  // (U^-1 has a unit diagonal)
+          row[xc[k]] = x[k];
+        }
+    }
+    __syncthreads();
+    // trailing update of A and of L^-1
+#pragma unroll
+    for (int k = 0; k < KA; ++k)
+      if (ahi[k] > j && ac[k] > j) a[k] = a[k] - col[ar[k]] * (LDL ? colu : col)[ac[k]];
+    if constexpr (INV) {
+#pragma unroll
+      for (int k = 0; k < KX; ++k)
+        if (xR[k] >= 0 && 8 * xC[k] <= j && j < 8 * xR[k] + 7 && xr[k] > j && xc[k] <= j)
+          x[k] = x[k] - col[xr[k]] * row[xc[k]];
+    }
+    // next pivot, by the owner of (j+1, j+1)
+    const int jn = j + 1;
+    if (jn < n) {
+#pragma unroll
+      for (int k = 0; k < KA; ++k)
+        if (alo[k] <= jn && jn <= ahi[k] && ar[k] == jn && ac[k] == jn) pivot(jn, a[k]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && info) info[blockIdx.x] = fail;
+  if constexpr (LDL) {
+    // L = U D^1/2 (column c times sqrt d_c, the diagonal sqrt d_c), L^-1 = D^-1/2 U^-1 (row r
+    // times 1/sqrt d_r): the n square roots side by side, into col (sqrt) and row (1/sqrt)
+    if (!fail) {
+      for (int c = tid; c < n; c += NT) pivot_sqrt(dgl[c], col[c], row[c]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KA; ++k)
+      if (ac[k] >= 0) a[k] = (ar[k] == ac[k]) ? col[ac[k]] : a[k] * col[ac[k]];
+    if constexpr (INV) {
+#pragma unroll
+      for (int k = 0; k < KX; ++k)
+        if (xr[k] >= 0) x[k] = x[k] * row[xr[k]];
+    }
+  }
+  if constexpr (INV) {
+    const MatDesc<T> o = out_inv[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < KX; ++k)
+      if (xr[k] >= 0) o.A[xr[k] + (size_t)xc[k] * o.lda] = x[k];
+    for (int e = tid; e < n * n; e += NT) {  // zeros above the diagonal tiles
+      const int r = e % n, c = e / n;
+      if ((c >> 3) > (r >> 3)) o.A[r + (size_t)c * o.lda] = T(0.0);
+    }
+  }
+  if (out_l) {
+    const MatDesc<T> ol = out_l[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < KA; ++k)
+      if (ac[k] >= 0) ol.A[ar[k] + (size_t)ac[k] * ol.lda] = a[k];
+    for (int e = tid; e < n * n; e += NT) {
+      const int r = e % n, c = e / n;
+      if (c > r) ol.A[r + (size_t)c * ol.lda] = T(0.0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // eigmin_lds: smallest eigenvalue of a symmetric matrix (n <= NMAX), 512 threads.  The matrix
 // is symmetrised into LDS (ld = n), tridiagonalised by Householder reflections (full storage),
 // then one wave runs a 64-point Sturm multisection.
