@@ -411,6 +411,61 @@ __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__
   }
 }
 
+// gemm_valu_ks: the same product with 8 x 8 output tiles and K split four ways inside the
+// workgroup (wave s takes k = s mod 4 of every 32-k chunk, two accumulation chains each; the
+// four partial sums meet in LDS).  A multi-word FMA is ~20 (dd) to ~225 (qd) fp64 instructions,
+// so one wave issuing a whole 16-long k-chunk per output was both issue- and chain-bound on the
+// few workgroups of the small-block configs; here every thread carries a quarter of K and a
+// launch has four times the workgroups.
+template <class T, bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_valu_ks(const GemmDesc<T>* __restrict__ descs,
+                                                    const TileRef* __restrict__ t2d, double alpha,
+                                                    double beta) {
+  constexpr int BM = 8, BN = 8, BK = 32;
+  __shared__ T As[BK][BM + 1];
+  __shared__ T Bs[BK][BN + 1];
+  __shared__ T red[4][64];
+  const TileRef tr = t2d[blockIdx.x];
+  const GemmDesc<T> d = descs[tr.p];
+  const int t = tr.t;
+  const int m0 = (t / d.tn) * BM, n0 = (t % d.tn) * BN;
+  const int tid = threadIdx.x, o = tid & 63, s = tid >> 6;
+  const int ti = o & 7, tj = o >> 3;
+  T acc0 = T(0.0), acc1 = T(0.0);
+  for (int k0 = 0; k0 < d.K; k0 += BK) {
+    {  // A tile 8 x 32 (the contiguous index fastest)
+      const int i = TA ? (tid >> 5) : (tid & 7), k = TA ? (tid & 31) : (tid >> 3);
+      const int gi = m0 + i, gk = k0 + k;
+      T v = T(0.0);
+      if (gi < d.M && gk < d.K) v = TA ? d.A[gk + (size_t)gi * d.lda] : d.A[gi + (size_t)gk * d.lda];
+      As[k][i] = v;
+    }
+    {  // B tile 32 x 8
+      const int j = TB ? (tid & 7) : (tid >> 5), k = TB ? (tid >> 3) : (tid & 31);
+      const int gj = n0 + j, gk = k0 + k;
+      T v = T(0.0);
+      if (gj < d.N && gk < d.K) v = TB ? d.B[gj + (size_t)gk * d.ldb] : d.B[gk + (size_t)gj * d.ldb];
+      Bs[k][j] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < BK / 4; u += 2) {
+      acc0 += As[s + 4 * u][ti] * Bs[s + 4 * u][tj];
+      acc1 += As[s + 4 * u + 4][ti] * Bs[s + 4 * u + 4][tj];
+    }
+    __syncthreads();
+  }
+  red[s][o] = acc0 + acc1;
+  __syncthreads();
+  if (s != 0) return;
+  const int row = m0 + ti, col = n0 + tj;
+  if (row < d.M && col < d.N) {
+    T v = ((red[0][o] + red[1][o]) + (red[2][o] + red[3][o])) * T(alpha);
+    if (beta != 0.0) v += d.Cin[row + (size_t)col * d.ldcin] * T(beta);
+    d.C[row + (size_t)col * d.ldc] = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Batched GEMV (the N = 1 problems of a GemmDesc batch): y = alpha op(A) x + beta y_in.
 // One 256-thread workgroup per 64 outputs.  TA = false: 64 rows x 4 k-classes (coalesced along
@@ -1006,6 +1061,68 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
     }
     __syncthreads();
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// trsv_wave: the multi-word vector solves of potrf's L (n <= 64, a few right-hand sides:
+// t_j = L_j^-1 rhs_j, the two solves with L_Q, dx_j = L_j^-T (...), MPMP.jl:1751-1773), one wave
+// per right-hand side with lane r holding row r.  The workgroup first stages L with its
+// off-diagonal entries scaled by the reciprocal pivots into LDS, in the order the wave reads
+// them (Ls[r + 64 q] = l_rq / l_qq, transposed: l_qr / l_qq), so each of the n serial steps is
+// one broadcast (v_readlane) and one multi-word product and subtraction per lane:
+//   v_r -= Ls[r, q] v_q   (r > q; transposed r < q),   and at the end x_r = v_r / l_rr.
+// trsm_batched's 16-row blocks carried, per block, a 16-step diagonal chain AND a 16-long
+// dependent dot product per row of the panel update on a mostly idle workgroup.
+// One workgroup per (matrix, NW right-hand sides), t2d as for trsm_batched with NC = NW.
+// ------------------------------------------------------------------------------------------
+template <class T>
+__device__ __forceinline__ T readlane_t(const T& v, int src) {  // src wave-uniform
+  T t;
+  int* ti = reinterpret_cast<int*>(&t);
+  const int* vi = reinterpret_cast<const int*>(&v);
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(T) / 4); ++q) ti[q] = __builtin_amdgcn_readlane(vi[q], src);
+  return t;
+}
+template <class T> constexpr size_t trsv_wave_lds() { return sizeof(T) * (64 * 64 + 64); }
+template <class T, bool TRANS, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void trsv_wave(const TrsmDesc<T>* __restrict__ descs,
+                                                     const int* __restrict__ t2d) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Ls = reinterpret_cast<T*>(smem_raw);  // 64 x 64, Ls[r + 64 q]
+  T* rdg = Ls + 64 * 64;                    // 1 / l_qq
+  const TrsmDesc<T> d = descs[t2d[blockIdx.x]];
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63;
+  const T* L = d.L;
+  const size_t ldl = d.ldl;
+  if (tid < n) rdg[tid] = recip_fast(L[tid + (size_t)tid * ldl]);
+  __syncthreads();
+  // column q of L (rows > q) scaled by 1/l_qq; transposed: row q (columns < q), read as column
+  for (int e = tid; e < n * n; e += 64 * NW) {
+    const int i = e % n, j = e / n;  // coalesced: i runs over the rows of L
+    if (i > j) {
+      const T v = L[i + (size_t)j * ldl] * rdg[TRANS ? i : j];
+      if (TRANS) Ls[j + 64 * i] = v;
+      else Ls[i + 64 * j] = v;
+    }
+  }
+  __syncthreads();
+  const int c = (blockIdx.x - d.tile0) * NW + (tid >> 6);
+  if (c >= d.nrhs) return;  // (whole waves; no barrier follows)
+  T* B = d.B + (size_t)c * d.ldb;
+  T v = lane < n ? B[lane] : T(0.0);
+  if (!TRANS) {
+    for (int q = 0; q + 1 < n; ++q) {
+      const T vq = readlane_t(v, q);
+      if (lane > q && lane < n) v = v - Ls[lane + 64 * q] * vq;
+    }
+  } else {
+    for (int q = n - 1; q > 0; --q) {
+      const T vq = readlane_t(v, q);
+      if (lane < q) v = v - Ls[lane + 64 * q] * vq;
+    }
+  }
+  if (lane < n) B[lane] = v * rdg[lane];
 }
 
 // ------------------------------------------------------------------------------------------
