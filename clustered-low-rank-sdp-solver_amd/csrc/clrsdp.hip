@@ -162,17 +162,17 @@ inline bool chol_ldl_on() {
   }();
   return on;
 }
-template <class T, bool INV>
+template <class T, bool INV, int NMAX = 64>
 void launch_chol_packed(unsigned nb, hipStream_t s, const MatDesc<T>* in, const MatDesc<T>* oi,
                         const MatDesc<T>* ol, int* info) {
   constexpr int NT = 1024;
   if constexpr (std::is_same<T, mw::qd>::value) {
     if (chol_ldl_on()) {
-      chol_packed<T, NT, INV, true><<<nb, NT, 0, s>>>(in, oi, ol, info);
+      chol_packed<T, NT, INV, true, NMAX><<<nb, NT, 0, s>>>(in, oi, ol, info);
       return;
     }
   }
-  chol_packed<T, NT, INV, false><<<nb, NT, 0, s>>>(in, oi, ol, info);
+  chol_packed<T, NT, INV, false, NMAX><<<nb, NT, 0, s>>>(in, oi, ol, info);
 }
 // eigmin_lds: A (n^2), v, NC = 8 (n <= 64) or 4 partial vectors, dg, e2, w, scalars
 template <class T> size_t eig_lds_bytes(int n) {
@@ -218,8 +218,9 @@ struct GemmPlan : PlanBase {
   std::vector<TileRef> t2d;
   GemmDesc<T>* d = nullptr;
   TileRef* dt = nullptr;
-  // gemm_f64_lds (fp64) and gemm_valu (multi-word) output tiles
-  static constexpr int TILE = std::is_same<T, double>::value ? 64 : 16;
+  // gemm_f64_lds (fp64) and gemm_valu_ks (multi-word; CLRSDP_GEMM_VALU16=1: gemm_valu) output
+  // tiles, fixed when the plan is created
+  const int TILE = std::is_same<T, double>::value ? 64 : std::getenv("CLRSDP_GEMM_VALU16") ? 16 : 8;
 
   void add(const T* A, int lda, const T* B, int ldb, const T* Cin, int ldcin, T* C, int ldc, int M,
            int N, int K) {
@@ -389,6 +390,11 @@ struct GemmPlan : PlanBase {
       else if (ta && !tb) gemm_f64_lds<true, false><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
       else if (!ta && tb) gemm_f64_lds<false, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
       else gemm_f64_lds<true, true><<<grid, 512, 0, s>>>(d, dt, alpha, beta, ds, dmult);
+    } else if (TILE == 8) {
+      if (!ta && !tb) gemm_valu_ks<T, false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (ta && !tb) gemm_valu_ks<T, true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (!ta && tb) gemm_valu_ks<T, false, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else gemm_valu_ks<T, true, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
     } else {
       if (!ta && !tb) gemm_valu<T, false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else if (ta && !tb) gemm_valu<T, true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
@@ -450,6 +456,12 @@ struct TrsmPlan : PlanBase {
   int* dt = nullptr;
   int nmax = 0, rmax = 0;
   bool narrow = false;
+  // multi-word solves with n <= 64: trsv_wave, one wave per right-hand side, 4 waves per
+  // workgroup for vector solves and 16 (four per SIMD, their chains interleaved; one LDS copy of
+  // L per 16 right-hand sides) for W_j = L_j^-1 B_j (CLRSDP_TRSV_BLOCKED=1 keeps trsm_batched)
+  static constexpr int NCV = 4, NCV16 = 16;
+  bool vec = false;
+  int ncv = NCV;
   void add(const T* L, int ldl, T* B, int ldb, int n, int nrhs) {
     if (n <= 0 || nrhs <= 0) return;
     rmax = std::max(rmax, nrhs);
@@ -463,7 +475,27 @@ struct TrsmPlan : PlanBase {
   void finalize() {
     if (h.empty()) return;
     narrow = mode == 0 && !std::is_same<T, double>::value && rmax >= 32 && !std::getenv("CLRSDP_TRSM_NC64");
-    const int nc = narrow ? NCN : NCW;
+    // (64 < n <= 128: trsv_wave128, L through LDS in 32-step chunks; CLRSDP_TRSV128=0 keeps
+    // trsm_batched there)
+    const char* e128 = std::getenv("CLRSDP_TRSV128");
+    vec = mode == 0 && !std::is_same<T, double>::value && !std::getenv("CLRSDP_TRSV_BLOCKED") &&
+          (nmax <= 64 || (nmax <= 128 && !(e128 && e128[0] == '0')));
+    ncv = rmax <= NCV ? NCV : NCV16;
+    const int nc = vec ? ncv : narrow ? NCN : NCW;
+    if constexpr (!std::is_same<T, double>::value) {
+      if (vec) {  // (outside any graph capture)
+        static std::atomic<unsigned long long> attr_f{0}, attr_t{0};
+        static std::atomic<unsigned long long> attr_f16{0}, attr_t16{0}, a128[4];
+        lds_attr_once(a128[0], (const void*)trsv_wave128<T, true, NCV>, (int)trsv_wave128_lds<T>());
+        lds_attr_once(a128[1], (const void*)trsv_wave128<T, false, NCV>, (int)trsv_wave128_lds<T>());
+        lds_attr_once(a128[2], (const void*)trsv_wave128<T, true, NCV16>, (int)trsv_wave128_lds<T>());
+        lds_attr_once(a128[3], (const void*)trsv_wave128<T, false, NCV16>, (int)trsv_wave128_lds<T>());
+        lds_attr_once(attr_t, (const void*)trsv_wave<T, true, NCV>, (int)trsv_wave_lds<T>());
+        lds_attr_once(attr_f, (const void*)trsv_wave<T, false, NCV>, (int)trsv_wave_lds<T>());
+        lds_attr_once(attr_t16, (const void*)trsv_wave<T, true, NCV16>, (int)trsv_wave_lds<T>());
+        lds_attr_once(attr_f16, (const void*)trsv_wave<T, false, NCV16>, (int)trsv_wave_lds<T>());
+      }
+    }
     t2d.clear();
     for (size_t q = 0; q < h.size(); ++q) {
       h[q].tile0 = (int)t2d.size();
@@ -480,6 +512,28 @@ struct TrsmPlan : PlanBase {
     constexpr int NC = NCW;
     const size_t lds = sizeof(T) * ((size_t)NB * NB + (size_t)NB * NC + (size_t)NB * nmax);
     const unsigned grid = (unsigned)t2d.size();
+    if constexpr (!std::is_same<T, double>::value) {
+      if (vec && mode == 0) {
+        if (nmax > 64) {
+          const size_t l = trsv_wave128_lds<T>();
+          if (ncv == NCV16) {
+            if (trans) trsv_wave128<T, true, NCV16><<<grid, 64 * NCV16, l, s>>>(d, dt);
+            else trsv_wave128<T, false, NCV16><<<grid, 64 * NCV16, l, s>>>(d, dt);
+          } else {
+            if (trans) trsv_wave128<T, true, NCV><<<grid, 64 * NCV, l, s>>>(d, dt);
+            else trsv_wave128<T, false, NCV><<<grid, 64 * NCV, l, s>>>(d, dt);
+          }
+        } else if (ncv == NCV16) {
+          if (trans) trsv_wave<T, true, NCV16><<<grid, 64 * NCV16, trsv_wave_lds<T>(), s>>>(d, dt);
+          else trsv_wave<T, false, NCV16><<<grid, 64 * NCV16, trsv_wave_lds<T>(), s>>>(d, dt);
+        } else {
+          if (trans) trsv_wave<T, true, NCV><<<grid, 64 * NCV, trsv_wave_lds<T>(), s>>>(d, dt);
+          else trsv_wave<T, false, NCV><<<grid, 64 * NCV, trsv_wave_lds<T>(), s>>>(d, dt);
+        }
+        HIPCHK(hipGetLastError());
+        return;
+      }
+    }
     if (narrow && mode == 0) {
       const size_t ldsn = sizeof(T) * ((size_t)NB * NB + (size_t)NB * NCN + (size_t)NB * nmax);
       if (trans) trsm_batched<T, true, NB, NCN, 256><<<grid, 256, ldsn, s>>>(d, dt);
@@ -524,21 +578,33 @@ struct MatPlan : PlanBase {  // potrf / eigmin
     h.push_back(m);
     nmax = std::max(nmax, n);
   }
-  // multi-word Cholesky factors of blocks with n <= 64: the register-resident chol_inv_reg
+  // multi-word Cholesky factors of blocks with n <= 128: the register-resident chol_packed
   // without the inverse (1024 threads, the whole block on chip, two barriers per column) writes
-  // L in place -- against potrf_batched's 16-column panels with a serial pivot chain.  Set
-  // before finalize(); CLRSDP_REG_POTRF=0 keeps potrf_batched.
+  // L in place -- against potrf_batched's 16-column panels with a serial pivot chain (n <= 64
+  // falls back to chol_inv_reg with CLRSDP_CHOL_PACKED=0).  Set before finalize();
+  // CLRSDP_REG_POTRF=0 keeps potrf_batched.
   bool reg_potrf = false;
   void finalize() {
     if (h.empty()) return;
     d = own(h);
     const char* e = std::getenv("CLRSDP_REG_POTRF");
-    reg_potrf = reg_potrf && !std::is_same<T, double>::value && nmax <= 64 && !(e && e[0] == '0');
+    // (double-double blocks 65..128: chol_packed only, CLRSDP_CHOL_PACKED128=0 keeps
+    // potrf_batched there; quad-double would spill at nine slots per thread)
+    const char* e2 = std::getenv("CLRSDP_CHOL_PACKED128");
+    const int lim = std::is_same<T, mw::dd>::value && chol_packed_on() && !(e2 && e2[0] == '0') ? 128 : 64;
+    reg_potrf = reg_potrf && !std::is_same<T, double>::value && nmax <= lim && !(e && e[0] == '0');
   }
   void potrf(hipStream_t s, int* info) const {
     if (h.empty()) return;
     if constexpr (!std::is_same<T, double>::value) {
       if (reg_potrf) {
+        if constexpr (std::is_same<T, mw::dd>::value) {
+          if (nmax > 64) {
+            chol_packed<T, 1024, false, false, 128><<<(unsigned)h.size(), 1024, 0, s>>>(d, d, d, info);
+            HIPCHK(hipGetLastError());
+            return;
+          }
+        }
         if (chol_packed_on())
           launch_chol_packed<T, false>((unsigned)h.size(), s, d, d, d, info);
         else

@@ -1125,6 +1125,55 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave(const TrsmDesc<T>* __restri
   if (lane < n) B[lane] = v * rdg[lane];
 }
 
+// trsv_wave128: the same for 64 < n <= 128 (the double-double S_j of config 4): lane r holds
+// rows r and r + 64, and the scaled L passes through LDS in chunks of 32 steps (the whole matrix
+// would not fit), staged by the workgroup between two barriers per chunk.
+template <class T> constexpr size_t trsv_wave128_lds() { return sizeof(T) * (32 * 128 + 128); }
+template <class T, bool TRANS, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void trsv_wave128(const TrsmDesc<T>* __restrict__ descs,
+                                                        const int* __restrict__ t2d) {
+  constexpr int CH = 32;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Ls = reinterpret_cast<T*>(smem_raw);  // Ls[i + 128 qq]: row i at step q0 + qq
+  T* rdg = Ls + CH * 128;
+  const TrsmDesc<T> d = descs[t2d[blockIdx.x]];
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63;
+  const T* L = d.L;
+  const size_t ldl = d.ldl;
+  for (int i = tid; i < n; i += 64 * NW) rdg[i] = recip_fast(L[i + (size_t)i * ldl]);
+  const int c = (blockIdx.x - d.tile0) * NW + (tid >> 6);
+  const bool act = c < d.nrhs;  // (wave-uniform; every wave stays for the barriers)
+  T* B = d.B + (size_t)(act ? c : 0) * d.ldb;
+  T v0 = act && lane < n ? B[lane] : T(0.0);
+  T v1 = act && lane + 64 < n ? B[lane + 64] : T(0.0);
+  const int nch = (n + CH - 1) / CH;
+  for (int ci = 0; ci < nch; ++ci) {
+    const int q0 = (TRANS ? nch - 1 - ci : ci) * CH, qn = min(CH, n - q0);
+    __syncthreads();  // the previous chunk is consumed (first pass: rdg is written)
+    for (int e = tid; e < qn * n; e += 64 * NW) {
+      int i, qq;
+      if (TRANS) { qq = e % qn; i = e / qn; } else { i = e % n; qq = e / n; }  // (coalesced)
+      const int q = q0 + qq;
+      T val = T(0.0);
+      if (TRANS ? i < q : i > q) val = (TRANS ? L[q + (size_t)i * ldl] : L[i + (size_t)q * ldl]) * rdg[q];
+      Ls[i + 128 * qq] = val;
+    }
+    __syncthreads();
+    if (act) {
+      for (int u = 0; u < qn; ++u) {
+        const int qq = TRANS ? qn - 1 - u : u, q = q0 + qq;
+        const T vq = readlane_t(q < 64 ? v0 : v1, q & 63);
+        if (TRANS ? lane < q : (lane > q && lane < n)) v0 = v0 - Ls[lane + 128 * qq] * vq;
+        if (TRANS ? lane + 64 < q : (lane + 64 > q && lane + 64 < n)) v1 = v1 - Ls[lane + 64 + 128 * qq] * vq;
+      }
+    }
+  }
+  if (act) {
+    if (lane < n) B[lane] = v0 * rdg[lane];
+    if (lane + 64 < n) B[lane + 64] = v1 * rdg[lane + 64];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // LU with partial pivoting in place, A[perm] = L U (L unit lower, U upper): approx_lu!
 // (MPMP.jl:1436, 1501) on midpoints, and the factor of approx_inv! (MPMP.jl:781, 788).  The

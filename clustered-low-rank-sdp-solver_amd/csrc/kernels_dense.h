@@ -195,12 +195,14 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
 // with all n square roots side by side.  The factors then differ from chol_inv_reg's in the
 // last bits only.
 // ------------------------------------------------------------------------------------------
-template <class T, int NT, bool INV, bool LDL = false>
+// NMAX = 128 (round 3, late): the multi-word potrf of blocks up to 128 (the double-double S_j
+// of config 4), 129 slots of A, nine registers per thread at 1024 threads.
+template <class T, int NT, bool INV, bool LDL = false, int NMAX = 64>
 __global__ __launch_bounds__(NT) void chol_packed(const MatDesc<T>* __restrict__ in,
                                                   const MatDesc<T>* __restrict__ out_inv,
                                                   const MatDesc<T>* __restrict__ out_l,
                                                   int* __restrict__ info) {
-  constexpr int NMAX = 64, NW = NT / 64;
+  constexpr int NW = NT / 64;
   constexpr int SA = (NMAX * (NMAX + 1) / 2 + 63) / 64;  // 33 slots of A at n = 64
   constexpr int SX = (NMAX / 8) * (NMAX / 8 + 1) / 2;     // 36 tiles of L^-1
   constexpr int KA = (SA + NW - 1) / NW, KX = INV ? (SX + NW - 1) / NW : 1;
@@ -1429,6 +1431,8 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
       if (i > k && i < n) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
+          if (8 * t >= n) break;         // (uniform: no column of the slot inside the matrix)
+          if (8 * t + 7 <= k) continue;  // (uniform: every column of the slot done)
           const int j = cls + 8 * t;
           if (j > k && j < n) acc[t & 3] += A[i + (size_t)j * ld] * v[j];
         }
@@ -1477,6 +1481,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
 #pragma unroll
         for (int t0 = 0; t0 < 16; t0 += 4) {
           if (cls + 8 * t0 >= n) break;  // (this lane has no live slot from t0 on)
+          if (8 * t0 + 31 <= c1) continue;  // (uniform: the four slots' columns are all done)
           T av[4], pj[4], vj[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
