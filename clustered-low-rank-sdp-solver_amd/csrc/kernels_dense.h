@@ -1431,8 +1431,6 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
       if (i > k && i < n) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-          if (8 * t >= n) break;         // (uniform: no column of the slot inside the matrix)
-          if (8 * t + 7 <= k) continue;  // (uniform: every column of the slot done)
           const int j = cls + 8 * t;
           if (j > k && j < n) acc[t & 3] += A[i + (size_t)j * ld] * v[j];
         }
@@ -1481,7 +1479,6 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
 #pragma unroll
         for (int t0 = 0; t0 < 16; t0 += 4) {
           if (cls + 8 * t0 >= n) break;  // (this lane has no live slot from t0 on)
-          if (8 * t0 + 31 <= c1) continue;  // (uniform: the four slots' columns are all done)
           T av[4], pj[4], vj[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
