@@ -926,6 +926,21 @@ __device__ inline mw::dd scale2(const mw::dd& v, int e) { return mw::dd(ldexp(v.
 __device__ inline mw::qd scale2(const mw::qd& v, int e) {
   return mw::qd(ldexp(v.x[0], e), ldexp(v.x[1], e), ldexp(v.x[2], e), ldexp(v.x[3], e));
 }
+// The half-width word of a multi-word type and the rounding to it (the leading words of the
+// non-overlapping representation).
+template <class T> struct HalfWord;
+template <> struct HalfWord<double> {
+  using type = double;
+  __device__ static double half(double v) { return v; }
+};
+template <> struct HalfWord<mw::dd> {
+  using type = double;
+  __device__ static double half(const mw::dd& v) { return v.hi; }
+};
+template <> struct HalfWord<mw::qd> {
+  using type = mw::dd;
+  __device__ static mw::dd half(const mw::qd& v) { return mw::dd(v.x[0], v.x[1]); }
+};
 // Multi-word "count >= 1" of the Sturm sequence (some eigenvalue of the tridiagonal below sigma),
 // division-free as sturm_any_below: with p_0 = 1 the count is >= 1 iff some leading principal
 // minor p_i = (d_i - sigma) p_{i-1} - e2_{i-1} p_{i-2} is negative (a zero minor is followed by a
@@ -1083,24 +1098,65 @@ __device__ void eig_multisection(const T* __restrict__ dg, const T* __restrict__
     // row and one division per step, against a division and three products per row.  A step
     // below 2^(-BITS/2 - 24) of the magnitude is the last one (quadratic convergence puts the
     // next correction far below the word); the two Sturm counts below accept the result.
+    // Mixed precision (round 3, late): the derivative recurrence runs in the half-width word H
+    // (dd for qd, fp64 for dd).  The step p/p' is a correction of the current error e, so a
+    // relative error eta of p' only adds eta * e to the next error (quadratic convergence becomes
+    // e^2 + eta e); p itself stays at full width.  At qd the first steps run entirely at dd
+    // (from the fp64 centre to ~2^-100 of the magnitude), so only the last two steps carry qd
+    // products, two per row instead of four.  The two Sturm counts below still decide.
+    using H = typename HalfWord<T>::type;
     T* nres = Wv;  // free after the reduction: [0] = sigma
     const double mag = fmax(fabs(bnd[0]), fabs(bnd[1]));
     if (tid == 0) {
       T s = T(0.5 * (bnd[2] + bnd[3]));
+      if constexpr (Num<T>::BITS > 150) {  // qd: dd pre-iterations on the dd-rounded tridiagonal
+        H sh = H(0.5 * (bnd[2] + bnd[3]));
+        const double tolh = ldexp(mag, -(Num<H>::BITS / 2 + 24)) + 1e-300;
+        for (int it = 0; it < 3; ++it) {
+          H pm = H(1.0), pc = HalfWord<T>::half(dg[0]) - sh, dm = H(0.0), dc = H(-1.0);
+          for (int i = 1; i < n; ++i) {
+            const H t = HalfWord<T>::half(dg[i]) - sh, e = HalfWord<T>::half(e2[i - 1]);
+            const H pn = t * pc - e * pm;
+            const H dn = (t * dc - pc) - e * dm;
+            pm = pc;
+            pc = pn;
+            dm = dc;
+            dc = dn;
+            const double mx = fmax(fmax(fabs(Num<H>::hi(pc)), fabs(Num<H>::hi(pm))),
+                                   fmax(fabs(Num<H>::hi(dc)), fabs(Num<H>::hi(dm))));
+            if (mx > 0.0 && mx < INFINITY) {
+              const int ex = __builtin_amdgcn_frexp_exp(mx);
+              pc = scale2(pc, -ex);
+              pm = scale2(pm, -ex);
+              dc = scale2(dc, -ex);
+              dm = scale2(dm, -ex);
+            }
+          }
+          if (Num<H>::hi(dc) == 0.0) break;
+          const H step = pc / dc;
+          const double as = fabs(Num<H>::hi(step));
+          if (!(as == as)) break;  // NaN: keep the last finite estimate
+          sh = sh - step;
+          if (as <= tolh) break;
+        }
+        s = T(sh);
+      }
       const double tol = ldexp(mag, -(Num<T>::BITS / 2 + 24)) + 1e-300;
       int conv = 0;
       for (int it = 0; it < 4; ++it) {
-        T pm = T(1.0), pc = dg[0] - s, dm = T(0.0), dc = T(-1.0);
+        T pm = T(1.0), pc = dg[0] - s;
+        H dm = H(0.0), dc = H(-1.0);
         for (int i = 1; i < n; ++i) {
           const T t = dg[i] - s;
           const T pn = t * pc - e2[i - 1] * pm;
-          const T dn = (t * dc - pc) - e2[i - 1] * dm;
+          const H dn = (HalfWord<T>::half(t) * dc - HalfWord<T>::half(pc)) -
+                       HalfWord<T>::half(e2[i - 1]) * dm;
           pm = pc;
           pc = pn;
           dm = dc;
           dc = dn;
           const double mx = fmax(fmax(fabs(Num<T>::hi(pc)), fabs(Num<T>::hi(pm))),
-                                 fmax(fabs(Num<T>::hi(dc)), fabs(Num<T>::hi(dm))));
+                                 fmax(fabs(Num<H>::hi(dc)), fabs(Num<H>::hi(dm))));
           if (mx > 0.0 && mx < INFINITY) {
             const int ex = __builtin_amdgcn_frexp_exp(mx);
             pc = scale2(pc, -ex);
@@ -1109,8 +1165,8 @@ __device__ void eig_multisection(const T* __restrict__ dg, const T* __restrict__
             dm = scale2(dm, -ex);
           }
         }
-        if (Num<T>::hi(dc) == 0.0) break;
-        const T step = pc / dc;
+        if (Num<H>::hi(dc) == 0.0) break;
+        const T step = pc / T(dc);
         s = s - step;
         const double as = fabs(Num<T>::hi(step));
         if (!(as == as)) break;  // NaN: leave conv = 0
