@@ -97,3 +97,28 @@ def test_reused_handle_new_thresholds(pk):
     assert first[-1].iterations < second[-1].iterations
     assert second[-1].iterations == fresh[-1].iterations
     assert [r[2:] for r in second[-1].log] == [r[2:] for r in fresh[-1].log]
+
+
+def test_step_length_all_1x1_blocks(pk):
+    """Every block 1 x 1 (an LP-like instance): the symmetric-epilogue flag and the one-column
+    gemv path meet in the plan; the product is trivially symmetric and must not be refused."""
+    from clrsdp_amd.solver import compute_step_length
+    M = [np.array([[v]]) for v in (2.0, 0.5, 3.0)]
+    dM = [np.array([[v]]) for v in (-1.0, 0.25, -6.0)]
+    alpha, flag, eig = compute_step_length(M, dM, 0.7, return_eigs=True)
+    ref = np.array([-0.5, 0.5, -2.0])
+    assert np.allclose(eig, ref, rtol=1e-15, atol=0.0)
+    assert abs(alpha - 0.35) <= 1e-15
+    assert flag is False
+
+
+def test_device_solver_all_1x1_blocks(pk):
+    """A handle whose local blocks are all 1 x 1 (delta = 1) is created and runs the loop body to
+    the same log as the oracle-checked host loop would stop at (no E_ARG at plan build)."""
+    cons, b = pk.synth(J=3, delta=1, rank=1, n_y=2, seed=11)
+    bi = pk.get_block_info(cons)
+    out = pk.solverank1sdp(cons, b, bi, omega_p=10.0, omega_d=10.0, duality_gap_threshold=1e-6,
+                           primal_error_threshold=1e-6, dual_error_threshold=1e-6,
+                           maxiterations=60, verbose=False, return_info=True)
+    assert out[-1].iterations > 0
+    assert out[-1].status in ("terminated", "optimal", "maxiterations")
