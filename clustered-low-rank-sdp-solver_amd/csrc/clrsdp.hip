@@ -636,7 +636,8 @@ struct MatPlan : PlanBase {  // potrf / eigmin
     }();
     // multi-word: eigmin_lds2 (two barriers per column) unless CLRSDP_EIG_LDS1=1
     static const bool lds1 = std::getenv("CLRSDP_EIG_LDS1") != nullptr;
-    if (!std::is_same<T, double>::value && !lds1 && eig2_lds_bytes<T>(nmax) <= LDS_MAX) {
+    if (!std::is_same<T, double>::value && !lds1 && eig2_lds_bytes<T>(nmax) <= LDS_MAX &&
+        (sizeof(T) <= 16 || nmax <= 64)) {  // (qd: 8 column slots per lane, n <= 64)
       static std::atomic<unsigned long long> attr2{0}, attr2f{0};
       if (newton) {
         lds_attr_once(attr2, (const void*)eigmin_lds2<T, true>, (int)LDS_MAX);

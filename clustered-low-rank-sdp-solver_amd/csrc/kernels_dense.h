@@ -919,6 +919,21 @@ __device__ inline T wave_sum_mw(T v) {
   v = v + swap_mw<32>(v);
   return v;
 }
+// The same butterfly when only lane 0 needs the sum and only lanes 0..m-1 hold nonzero values:
+// after level L lane 0 holds the sum of lanes 0..2^L - 1, so the levels past ceil(log2 m) would
+// only add zeros (uniform branches on m).  eigmin_lds2's v^T p partials live on lanes 0-7 and
+// its reflector norms on the first m = n - c - 1 lanes: half of the multi-word additions of
+// those two sums are dropped from the per-column chain.
+template <class T>
+__device__ inline T lane0_sum_mw(T v, int m) {
+  if (m > 1) v = v + dpp_mw<0xB1>(v);
+  if (m > 2) v = v + dpp_mw<0x4E>(v);
+  if (m > 4) v = v + dpp_mw<0x141>(v);
+  if (m > 8) v = v + dpp_mw<0x140>(v);
+  if (m > 16) v = v + swap_mw<16>(v);
+  if (m > 32) v = v + swap_mw<32>(v);
+  return v;
+}
 
 // exact power-of-two scaling of every limb
 __device__ inline double scale2(double v, int e) { return ldexp(v, e); }
@@ -1404,6 +1419,10 @@ template <class T, bool NEWTON = true, int DBG = 0>
 __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict__ descs,
                                                    T* __restrict__ out) {
   constexpr int NT = 512;
+  // column slots per lane (j = cls + 8 t) and rows per lane in the reflector: a quad-double
+  // image fits LDS only for n <= 64 (the launch checks it), so qd carries 8 slots and one row,
+  // which keeps its per-lane words out of scratch
+  constexpr int NSL = sizeof(T) > 16 ? 8 : 16, NH = sizeof(T) > 16 ? 1 : 2;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const MatDesc<T> d = descs[blockIdx.x];
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1430,11 +1449,11 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
   const int npass = (n + 63) / 64;
   // reflector of column c from its entries x_i = col[i] (i > c; lane l holds rows c+1+l and
   // c+65+l), by wave 0: v into vb[c & 1], beta into scal[c & 1], dg[c] = diag, e2[c]
-  auto reflector = [&](int c, const T (&x)[2], const T& diag) {
+  auto reflector = [&](int c, const T (&x)[NH], const T& diag) {
     T s = T(0.0);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) s += x[h] * x[h];
-    s = wave_sum_mw(s);
+    for (int h = 0; h < NH; ++h) s += x[h] * x[h];
+    s = lane0_sum_mw(s, n - c - 1);  // (only lane 0 uses s: beta, v0, e2[c])
     const T x0 = shfl_t(x[0], 0);  // row c+1
     const T tail = s - x0 * x0;
     T* v = vb + (c & 1) * ld;
@@ -1448,12 +1467,12 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
       beta = recip_fast(tail + v0 * v0) * T(2.0);
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NH; ++h) {
       const int i = c + 1 + lane + 64 * h;
       if (i < n) v[i] = (i == c + 1) ? v0 : x[h];
     }
     if (lane < c + 1 && lane < ld) v[lane] = T(0.0);
-    if (lane + 64 < c + 1) v[lane + 64] = T(0.0);
+    if (NH > 1 && lane + 64 < c + 1) v[lane + 64] = T(0.0);
     if (lane == 0) {
       dg[c] = diag;
       e2[c] = e2c;
@@ -1465,9 +1484,9 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
     return;
   }
   if (w == 0) {  // the reflector of column 0 from the input
-    T x[2];
+    T x[NH];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NH; ++h) {
       const int i = 1 + lane + 64 * h;
       x[h] = i < n ? A[i] : T(0.0);
     }
@@ -1486,7 +1505,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
       T acc[4] = {T(0.0), T(0.0), T(0.0), T(0.0)};
       if (i > k && i < n) {
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
+        for (int t = 0; t < NSL; ++t) {
           const int j = cls + 8 * t;
           if (j > k && j < n) acc[t & 3] += A[i + (size_t)j * ld] * v[j];
         }
@@ -1500,7 +1519,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
         if (i > k) vp += v[i] * pi;
       }
     }
-    vp = wave_sum_mw(vp);
+    vp = lane0_sum_mw(vp, 8);  // (nonzero on the class-0 lanes 0-7 only)
     if (lane == 0) redw[(k & 1) * 8 + w] = vp;
     __syncthreads();
     // ---- (D) A' -= v w^T + w v^T on rows/columns > k+1; wave 0: column k+1 and its reflector
@@ -1510,9 +1529,9 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
     const int c1 = k + 1;
     const T pc = p[c1], vc = v[c1];
     if (w == 0) {  // column c1 (rows > c1) and its diagonal, updated in registers
-      T x[2];
+      T x[NH];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < NH; ++h) {
         const int i = c1 + 1 + lane + 64 * h;
         x[h] = T(0.0);
         if (i < n) {
@@ -1533,7 +1552,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
         // groups of 4 slots: all loads, then the 4 independent updates, then the stores (the
         // stores may alias later loads of the same LDS image, which would order every chain)
 #pragma unroll
-        for (int t0 = 0; t0 < 16; t0 += 4) {
+        for (int t0 = 0; t0 < NSL; t0 += 4) {
           if (cls + 8 * t0 >= n) break;  // (this lane has no live slot from t0 on)
           T av[4], pj[4], vj[4];
 #pragma unroll
