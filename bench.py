@@ -265,9 +265,31 @@ def main():
         phase += ph
         schur_ms += ph[_lib.STAGE_SCHUR]
     barrier_sync()
+    dev.set_timing(False)
+    # host cost of enqueueing one loop body eagerly (launch by launch, no graph: the sharded
+    # path's default), i.e. the host time inside clrsdp_iterate_async; from the initial point,
+    # after the timed region
+    dev.restore_state()
+    barrier_sync()
+    dev.set_graph(False)
+    enq, body = [], []
+    for _ in range(12):
+        t1 = time.perf_counter()
+        dev.iterate_async(prm)
+        t2 = time.perf_counter()
+        dev.iterate_wait()
+        body.append(time.perf_counter() - t1)
+        enq.append(t2 - t1)
+    dev.set_graph(True)
+    host_enqueue_ms = float(np.median(enq[2:])) * 1e3
+    eager_body_ms = float(np.median(body[2:])) * 1e3
+    barrier_sync()
     if dist is not None:
         dt = dist.max_over_ranks(dt)
         schur_ms = dist.max_over_ranks(schur_ms)
+        host_enqueue_ms = dist.max_over_ranks(host_enqueue_ms)
+        eager_body_ms = dist.max_over_ranks(eager_body_ms)
+    xranks, xbackend = dev.comm_info()
 
     if rank != 0:
         dev.close()   # the RCCL communicator goes with the handle, before the control plane
@@ -330,6 +352,15 @@ def main():
         "graph_replay": world == 1 or (getattr(dist, "backend", "") == "rccl"
                                        and os.environ.get("CLRSDP_GRAPH_RCCL") is not None),
         "exchange": "none (1 GPU)" if dist is None else dist.backend,
+        # the communicator the library's loop body really uses: ranks from ncclCommCount on the
+        # native RCCL path (clrsdp_comm_info), world_size on the callback path
+        "exchange_ranks": xranks,
+        "exchange_backend_native": xbackend,
+        "host_enqueue_ms": host_enqueue_ms,
+        "host_enqueue_source": ("median host time of clrsdp_iterate_async with the graph off "
+                                "(clrsdp_set_graph(0): the ~100 launches of one loop body enqueued "
+                                "eagerly, as the sharded path does), 10 bodies from the initial point"),
+        "eager_body_ms": eager_body_ms,
         "host_loop": "pipelined (host one loop body behind, device-side pd_feas/terminate)"
                      if pipelined else "synchronous (one hipGraph replay per loop body)",
     }

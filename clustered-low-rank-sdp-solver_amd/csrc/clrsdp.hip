@@ -80,6 +80,7 @@ struct Rccl {
   decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclCommCount) comm_count = nullptr;
 };
 
 const Rccl& rccl() {
@@ -99,6 +100,7 @@ const Rccl& rccl() {
       api.all_gather = reinterpret_cast<decltype(api.all_gather)>(dlsym(so, "ncclAllGather"));
       api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(so, "ncclCommDestroy"));
       api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(so, "ncclGetErrorString"));
+      api.comm_count = reinterpret_cast<decltype(api.comm_count)>(dlsym(so, "ncclCommCount"));
       if (!api.get_unique_id || !api.comm_init_rank || !api.all_gather || !api.comm_destroy ||
           !api.error_string) {
         api = Rccl{};
@@ -191,6 +193,13 @@ inline std::vector<TileRef> tile_major(const std::vector<int>& ntiles) {
   return out;
 }
 
+// a development switch is on when set to anything but a value starting with '0' (so that
+// NAME=0 switches it off again, for every switch alike)
+static inline bool env_on(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] != '0';
+}
+
 // the plans own their device descriptor arrays (freed with the plan; plans are never copied)
 struct PlanBase {
   std::vector<void*> owned_dev;
@@ -220,8 +229,15 @@ struct GemmPlan : PlanBase {
   TileRef* dt = nullptr;
   // gemm_f64_lds (fp64) and gemm_valu_ks (multi-word; CLRSDP_GEMM_VALU16=1: gemm_valu) output
   // tiles, fixed when the plan is created
-  const int TILE = std::is_same<T, double>::value ? 64 : std::getenv("CLRSDP_GEMM_VALU16") ? 16 : 8;
+  const int TILE = std::is_same<T, double>::value ? 64 : env_on("CLRSDP_GEMM_VALU16") ? 16 : 8;
 
+  void clear() {  // back to an empty plan (a failed build_lu_plans)
+    h.clear();
+    ntiles.clear();
+    t2d.clear();
+    d = nullptr;
+    dt = nullptr;
+  }
   void add(const T* A, int lda, const T* B, int ldb, const T* Cin, int ldcin, T* C, int ldc, int M,
            int N, int K) {
     if (M <= 0 || N <= 0) return;
@@ -300,7 +316,7 @@ struct GemmPlan : PlanBase {
   UniGemm ug{};
   void detect_uniform() {
     if constexpr (std::is_same<T, double>::value) {
-      static const bool off = std::getenv("CLRSDP_NO_UNI_GEMM") != nullptr;
+      static const bool off = env_on("CLRSDP_NO_UNI_GEMM");
       if (off || gemv || dyn || h.empty()) return;
       const GemmDesc<T>& g0 = h[0];
       auto stride = [&](auto get, long long& st) {
@@ -474,11 +490,11 @@ struct TrsmPlan : PlanBase {
   }
   void finalize() {
     if (h.empty()) return;
-    narrow = mode == 0 && !std::is_same<T, double>::value && rmax >= 32 && !std::getenv("CLRSDP_TRSM_NC64");
+    narrow = mode == 0 && !std::is_same<T, double>::value && rmax >= 32 && !env_on("CLRSDP_TRSM_NC64");
     // (64 < n <= 128: trsv_wave128, L through LDS in 32-step chunks; CLRSDP_TRSV128=0 keeps
     // trsm_batched there)
     const char* e128 = std::getenv("CLRSDP_TRSV128");
-    vec = mode == 0 && !std::is_same<T, double>::value && !std::getenv("CLRSDP_TRSV_BLOCKED") &&
+    vec = mode == 0 && !std::is_same<T, double>::value && !env_on("CLRSDP_TRSV_BLOCKED") &&
           (nmax <= 64 || (nmax <= 128 && !(e128 && e128[0] == '0')));
     ncv = rmax <= NCV ? NCV : NCV16;
     const int nc = vec ? ncv : narrow ? NCN : NCW;
@@ -623,8 +639,12 @@ struct MatPlan : PlanBase {  // potrf / eigmin
   void eigmin(hipStream_t s, T* out) const {
     if (h.empty()) return;
     if constexpr (std::is_same<T, double>::value) {
-      if (nmax <= 128) {  // matrix in registers (eigmin_reg)
-        eigmin_reg<<<(unsigned)h.size(), 512, 0, s>>>(d, out);
+      if (nmax <= 128) {  // matrix in registers
+        // eigmin_split (round 4: one reflector chain wave + 8 bulk waves) unless
+        // CLRSDP_EIG_REG=1 (eigmin_reg: every live wave builds the reflector)
+        static const bool reg = env_on("CLRSDP_EIG_REG");
+        if (reg) eigmin_reg<<<(unsigned)h.size(), 512, 0, s>>>(d, out);
+        else eigmin_split<<<(unsigned)h.size(), 576, 0, s>>>(d, out);
         HIPCHK(hipGetLastError());
         return;
       }
@@ -635,7 +655,7 @@ struct MatPlan : PlanBase {  // potrf / eigmin
       return !(e && e[0] == '0');
     }();
     // multi-word: eigmin_lds2 (two barriers per column) unless CLRSDP_EIG_LDS1=1
-    static const bool lds1 = std::getenv("CLRSDP_EIG_LDS1") != nullptr;
+    static const bool lds1 = env_on("CLRSDP_EIG_LDS1");
     if (!std::is_same<T, double>::value && !lds1 && eig2_lds_bytes<T>(nmax) <= LDS_MAX &&
         (sizeof(T) <= 16 || nmax <= 64)) {  // (qd: 8 column slots per lane, n <= 64)
       static std::atomic<unsigned long long> attr2{0}, attr2f{0};
@@ -784,6 +804,8 @@ struct HandleBase {
   virtual void restore_state() = 0;
   virtual void set_factorization(int flags) = 0;
   virtual int get_factorization() const = 0;
+  virtual void set_graph(int on) = 0;
+  virtual void comm_info(int* nranks, int* backend) const = 0;
 };
 
 template <class T>
@@ -1015,7 +1037,7 @@ struct Solver final : HandleBase {
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
     // CLRSDP_ONE_STREAM=1: the side-stream work runs in order on the main stream (experiment:
     // graph-boundary and join idle time against the lost overlap)
-    if (std::getenv("CLRSDP_ONE_STREAM")) aux = own_stream;
+    if (env_on("CLRSDP_ONE_STREAM")) aux = own_stream;
     else HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
     for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21, &ev_ty, &ev_join})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -1492,8 +1514,32 @@ struct Solver final : HandleBase {
   //   solves:  t_j = L_j^-1 rhs_j[perm_j]; u = sum_j W2_j^T t_j; dy = U_Q^-1 L_Q^-1 (p - u)[perm];
   //            dx_j = U_j^-1 (t_j + W1_j dy)                                  (MPMP.jl:1743-1776)
   //   X^-1:    X_b[perm_b] = L_b U_b; X_b^-1 = U_b^-1 L_b^-1 (P_b I)          (approx_inv!, 781)
+  // the on-chip panel of getrf_batched bounds the LU fallback (fp64 ~624, dd ~312, qd ~156)
+  bool lu_fits() const {
+    int nmax = (int)n_y;
+    for (int c = 0; c < nc(); ++c) nmax = std::max(nmax, (int)Ds[oc[c]]);
+    for (const LBlk& b : lb) nmax = std::max(nmax, b.n);
+    return getrf_lds_bytes<T, LuPlan<T>::NB>(nmax) <= LDS_MAX - 4096;
+  }
   void build_lu_plans() {
     if (lu_built) return;
+    if (!lu_fits())
+      throw ClrsdpError{CLRSDP_E_ARG, "LU factorization: a matrix is too large for the on-chip panel of getrf_batched"};
+    try {
+      build_lu_plans_();
+    } catch (...) {  // transactional: no half-built plans or buffers survive a failure
+      for (LuPlan<T>* l : {&lu_S, &lu_Q, &lu_X}) l->h.clear();
+      for (PermPlan<T>* q : {&pm_B, &pm_rhs, &pm_r, &pm_I}) q->h.clear();
+      for (TrsmPlan<T>* t : {&tl_W1, &tl_W2, &tl_t, &tl_dx, &tl_Q1, &tl_Q2, &tl_X1, &tl_X2}) t->h.clear();
+      for (GemmPlan<T>* g : {&lq_slab, &lq_Wt}) g->clear();
+      if (lperm) (void)hipFree(lperm);
+      if (W2m) (void)hipFree(W2m);
+      lperm = nullptr;
+      W2m = nullptr;
+      throw;
+    }
+  }
+  void build_lu_plans_() {
     int64_t np = nx + n_y;
     for (const LBlk& b : lb) np += b.n;
     lperm = dmalloc<int>(std::max<int64_t>(np, 1));
@@ -2242,7 +2288,9 @@ struct Solver final : HandleBase {
   }
   int check_info(const char* blk = nullptr) {
     const int* h = reinterpret_cast<const int*>((blk ? blk : stat_host) + stat_info_off);
-    const int b = (world > 1 && (comm || xfn)) ? h[info_G] : fail_bits(h);
+    // local bits always (run_stage reports a failure at the stage where it happens); with
+    // world > 1 also the OR over all ranks, which STEP's exchange wrote into info_G
+    const int b = fail_bits(h) | ((world > 1 && (comm || xfn)) ? h[info_G] : 0);
     if (b & 4) {
       if (lu_x()) {  // X^-1 came from LU; cho!(X) of the step length failed (MPMP.jl:1846-1882)
         err = "The step length could not be calculated correctly (X not PD).";
@@ -2264,7 +2312,7 @@ struct Solver final : HandleBase {
     int add = 0;
     if ((rc == CLRSDP_E_NOT_PD_S || rc == CLRSDP_E_NOT_PD_Q) && !lu_sq()) add = CLRSDP_FACT_LU_SQ;
     else if (rc == CLRSDP_E_NOT_PD_X && !lu_x()) add = CLRSDP_FACT_LU_X;
-    if (!add) return false;
+    if (!add || !lu_fits()) return false;  // beyond the LU panel: the reference's error stands
     build_lu_plans();
     fact_flags |= add;
     drop_graphs();
@@ -2390,11 +2438,25 @@ struct Solver final : HandleBase {
   hipGraphExec_t gexec[4] = {nullptr, nullptr, nullptr, nullptr};
   clrsdp_params gprm[4];
   unsigned graph_launches = 0;
-  bool use_graph = std::getenv("CLRSDP_NO_GRAPH") == nullptr;
+  bool use_graph = !env_on("CLRSDP_NO_GRAPH");
   // multi-rank loop bodies with the native communicator are enqueued eagerly by default (the
   // pipelined host loop hides the enqueue); CLRSDP_GRAPH_RCCL=1 captures the all-gathers into
   // the replayed graph as well
-  bool graph_rccl = std::getenv("CLRSDP_GRAPH_RCCL") != nullptr;
+  bool graph_rccl = env_on("CLRSDP_GRAPH_RCCL");
+  void set_graph(int on) override {
+    if (inflight) throw ClrsdpError{CLRSDP_E_STATE, "set_graph with loop bodies in flight"};
+    use_graph = on != 0;
+  }
+  // the exchange the loop body uses: backend 0 none (one rank), 1 the native RCCL communicator
+  // (nranks = ncclCommCount), 2 the registered callback (nranks = world_size)
+  void comm_info(int* nranks, int* backend) const override {
+    *backend = comm ? 1 : (xfn ? 2 : 0);
+    *nranks = world;
+    if (comm && rccl().comm_count) {
+      int n = 0;
+      if (rccl().comm_count(comm, &n) == ncclSuccess) *nranks = n;
+    }
+  }
   bool graph_ok() const { return use_graph && timing != 1 && (world == 1 || (comm && graph_rccl)); }
   // forget every captured loop body (they are re-captured on their next use)
   void drop_graphs() {
@@ -2538,11 +2600,14 @@ struct Solver final : HandleBase {
     if (halted) return CLRSDP_OK;   // skipped body: its factorisations may fail, nothing applied
     const int rc = check_info(ring_host[slot]);
     st->status = rc;
-    if (fallback(rc)) {
-      // the bodies behind this one ran on the same (unchanged) state and failed alike: wait for
-      // them, then re-enqueue this body and those behind it with the LU factorisations
-      const int behind = inflight;
+    const int behind = inflight;
+    // a failed body: the bodies behind it may still execute (from the replayed graphs), so they
+    // are waited for before fallback() destroys any graph
+    if (rc != CLRSDP_OK)
       for (int q = 0; q < behind; ++q) HIPCHK(hipEventSynchronize(ring_ev[(ring_head + q) % 2]));
+    if (fallback(rc)) {
+      // the bodies behind this one ran on the same (unchanged) state and failed alike:
+      // re-enqueue this body and those behind it with the LU factorisations
       inflight = 0;
       const clrsdp_params prm = last_prm;
       for (int q = 0; q <= behind; ++q) {
@@ -2915,6 +2980,20 @@ int32_t clrsdp_step_length(int32_t device, int64_t nblocks, const int64_t* n, co
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on) {
   if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
   GUARD(h, { h->impl->set_timing(on); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_set_graph(clrsdp_handle* h, int32_t on) {
+  if (!h) { g_last_error = "null handle"; return CLRSDP_E_ARG; }
+  GUARD(h, { h->impl->set_graph(on); return CLRSDP_OK; })
+}
+
+int32_t clrsdp_comm_info(const clrsdp_handle* h, int32_t* nranks, int32_t* backend) {
+  if (!h || !nranks || !backend) { g_last_error = "null argument"; return CLRSDP_E_ARG; }
+  int n = 0, b = 0;
+  h->impl->comm_info(&n, &b);
+  *nranks = n;
+  *backend = b;
+  return CLRSDP_OK;
 }
 
 int32_t clrsdp_set_factorization(clrsdp_handle* h, int32_t flags) {

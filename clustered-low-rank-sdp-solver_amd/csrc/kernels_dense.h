@@ -870,6 +870,307 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
 #undef ER_STAMP
 }
 
+// ------------------------------------------------------------------------------------------
+// eigmin_split (round 4): lambda_min of a symmetric fp64 block (n <= 128), the same Householder
+// tridiagonalisation as eigmin_reg with the matrix in the registers of 8 "bulk" waves (same
+// layout), but the reflector of each column is built ONCE, by a ninth "chain" wave at raised
+// issue priority, instead of redundantly by every live wave: that redundancy made eigmin_reg
+// VALU-issue bound (~300 instructions per column and wave against 96 useful FMAs, two waves per
+// SIMD).  Two barriers per column k:
+//   bulk:  p = A_k v_k in registers, per-wave v^T p, the rows of p to LDS          -- barrier 1
+//   bulk:  w = beta p - K v; A_{k+1} = A_k - v w^T - w v^T in registers; the owners of row k+2
+//          publish it (for step k+1)
+//   chain: row k+1 of A_{k+1} from the copy its owners published a step earlier (their own
+//          operations), the reflector v_{k+1} and beta_{k+1}, the tridiagonal entries -> LDS
+//                                                                                   -- barrier 2
+// The rank-2 update (two of the three FMAs per entry) runs under the chain's latency; per column
+// only the matvec, two LDS round trips and the chain's ~40 dependent operations are serial.
+// The chain lane (c, t16) holds the same column pair j0 = 2c + 8 t16 as a bulk lane, so its sums
+// run in eigmin_reg's order.  Same scaling, Gershgorin bracket and multisection as eigmin_reg.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __restrict__ descs,
+                                                     double* __restrict__ out) {
+  constexpr int NS = 16, NWB = 8;
+  __shared__ __attribute__((aligned(16))) double rowb[2][128];
+  __shared__ __attribute__((aligned(16))) double pb[2][128];
+  __shared__ __attribute__((aligned(16))) double vb[2][128];
+  __shared__ __attribute__((aligned(16))) double redw[2][NWB];
+  __shared__ double betab[2];
+  __shared__ double dg[128], e2[128];
+  __shared__ __attribute__((aligned(16))) double sd[128], se[128];
+  __shared__ double bnd[2];
+  __shared__ unsigned long long masks[8];
+  __shared__ double amaxw[NWB];
+  const MatDesc<double> d = descs[blockIdx.x];
+  const int n = d.n, lda = d.lda, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const bool chain = w == NWB;
+  const int blk = w < 4 ? w : 11 - w;  // bulk row block (pairs 0/7, 1/6, 2/5, 3/4 per SIMD)
+  const int c = lane >> 4, t16 = lane & 15;
+  const int i = blk * 16 + t16;       // bulk: this lane's row
+  const int j0 = 2 * c + 8 * t16;     // this lane's column pair (bulk: broadcast slot; chain: x_j)
+  double a[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) a[s][0] = a[s][1] = 0.0;
+  if (!chain) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * c + 8 * s + e;
+        const int ic = min(i, n - 1), jc = min(j, n - 1);
+        const double v = gload(d.A + ic + (size_t)jc * lda);
+        a[s][e] = (i < n && j < n) ? v : 0.0;
+      }
+    double amax = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) amax = fmax(amax, fmax(fabs(a[s][0]), fabs(a[s][1])));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
+    if (lane == 0) amaxw[w] = amax;
+  }
+  __syncthreads();
+  int ex0;
+  {
+    double amax = amaxw[0];
+#pragma unroll
+    for (int r = 1; r < NWB; ++r) amax = fmax(amax, amaxw[r]);
+    ex0 = (amax > 0.0 && amax < INFINITY) ? __builtin_amdgcn_frexp_exp(amax) : 0;
+  }
+  if (!chain) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      a[s][0] = __builtin_ldexp(a[s][0], -ex0);
+      a[s][1] = __builtin_ldexp(a[s][1], -ex0);
+    }
+  }
+  auto publish_row = [&](int r, double* dst) {  // the owners of row r write its 128 entries
+    if (!chain && blk == (r >> 4) && t16 == (r & 15)) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        *reinterpret_cast<double2*>(dst + 2 * c + 8 * s) = make_double2(a[s][0], a[s][1]);
+    }
+  };
+  // chain state: v of the current step at the lane's column pair, and beta
+  double cx = 0.0, cy = 0.0, beta = 0.0, vi = 0.0;
+  // the reflector of column r from x = row r of the current matrix (chain wave only):
+  // v_j = 0 (j <= r), v0 (j = r+1), x_j (j > r+1), H = I - beta v v^T
+  auto reflector = [&](int r, double xj0, double xj1, double xr, double x0) {
+    double tl = (j0 >= r + 2 ? xj0 * xj0 : 0.0);
+    tl = fma(j0 + 1 >= r + 2 ? xj1 : 0.0, xj1, tl);
+    tl = xsum32(xsum16(row16_sum(tl)));  // sum_{j >= r+2} x_j^2
+    double bt = 0.0, v0 = x0, e2r = x0 * x0;
+    if (tl > 0.0) {
+      const double ss = fma(x0, x0, tl);
+      double nrm;
+      if (ss > 0x1p-900) {  // Newton-refined hardware rsq / rcp (~1 ulp)
+        double rs = __builtin_amdgcn_rsq(ss);
+        rs = rs * fma(-0.5 * ss, rs * rs, 1.5);
+        nrm = ss * rs;
+        nrm = fma(fma(-nrm, nrm, ss), 0.5 * rs, nrm);
+      } else {
+        nrm = sqrt(ss);
+      }
+      const double alpha = x0 > 0.0 ? -nrm : nrm;
+      v0 = x0 - alpha;
+      const double q = fma(v0, v0, tl);
+      double rc = __builtin_amdgcn_rcp(q);
+      rc = fma(fma(-q, rc, 1.0), rc, rc);
+      rc = fma(fma(-q, rc, 1.0), rc, rc);
+      bt = 2.0 * rc;
+      e2r = alpha * alpha;
+    }
+    cx = j0 <= r ? 0.0 : (j0 == r + 1 ? v0 : xj0);
+    cy = j0 + 1 <= r ? 0.0 : (j0 + 1 == r + 1 ? v0 : xj1);
+    beta = bt;
+    *reinterpret_cast<double2*>(&vb[r & 1][j0]) = make_double2(cx, cy);
+    if (lane == 0) {
+      dg[r] = xr;
+      e2[r] = e2r;
+      betab[r & 1] = bt;
+    }
+  };
+  publish_row(0, rowb[0]);
+  if (n >= 2) publish_row(1, rowb[1]);
+  __syncthreads();
+  if (chain) {
+    __builtin_amdgcn_s_setprio(3);
+    if (n >= 2) {
+      const double2 xr = *reinterpret_cast<const double2*>(&rowb[0][j0]);
+      reflector(0, xr.x, xr.y, rowb[0][0], rowb[0][1]);
+    } else if (lane == 0) {
+      dg[0] = rowb[0][0];
+    }
+  }
+  __syncthreads();
+  if (!chain && n >= 2) {
+    const double2 v2 = *reinterpret_cast<const double2*>(&vb[0][j0]);
+    cx = v2.x;
+    cy = v2.y;
+    vi = vb[0][i];
+    beta = betab[0];
+  }
+  for (int k = 0; k + 2 < n; ++k) {
+    const int lo = (k + 1) >> 3;  // slots s < lo hold columns <= k only
+    double pp = 0.0;
+    if (!chain) {
+      // ---- p = A_k v_k and this wave's part of v^T p (two FMA chains per column parity)
+      const bool live = blk * 16 + 15 > k && blk * 16 < n;
+      double pa[4] = {0.0, 0.0, 0.0, 0.0};
+      if (live) {
+        static_for<0, NS / 4>([&](auto G) {
+          constexpr int g = decltype(G)::value;
+          if (4 * g + 3 >= lo) {
+            static_for<4 * g, 4 * g + 4>([&](auto S) {
+              constexpr int s = decltype(S)::value;
+              fmac_bcast<s, s == 4 * g>(pa[2 * (s & 1)], cx, a[s][0]);
+              fmac_bcast<s, false>(pa[2 * (s & 1) + 1], cy, a[s][1]);
+            });
+          }
+        });
+      }
+      pp = xsum32(xsum16((pa[0] + pa[1]) + (pa[2] + pa[3])));
+      double t = 0.0;
+      if (c == 0) {
+        pb[k & 1][i] = i > k ? pp : 0.0;
+        t = vi * pp;
+      }
+      t = row16_sum(t);  // class-0 lanes carry the rows' v_i p_i
+      if (lane == 0) redw[k & 1][w] = t;
+    }
+    __syncthreads();
+    const int r = k + 1;
+    if (chain) {
+      // ---- row r of A_{k+1} and the reflector v_{k+1}
+      double rw[NWB];
+#pragma unroll
+      for (int q = 0; q < NWB; q += 2) {
+        const double2 v2 = *reinterpret_cast<const double2*>(&redw[k & 1][q]);
+        rw[q] = v2.x;
+        rw[q + 1] = v2.y;
+      }
+      const double* old = rowb[r & 1];
+      const double2 pj = *reinterpret_cast<const double2*>(&pb[k & 1][j0]);
+      const double2 o = *reinterpret_cast<const double2*>(old + j0);
+      const double orr = old[r], or1 = old[r + 1];
+      const double vr = vb[k & 1][r], vr1 = vb[k & 1][r + 1];
+      const double pr = pb[k & 1][r], pr1 = pb[k & 1][r + 1];
+      const double tot = ((rw[0] + rw[1]) + (rw[2] + rw[3])) + ((rw[4] + rw[5]) + (rw[6] + rw[7]));
+      const double Kc = beta * beta * tot * 0.5;
+      const double wr = fma(beta, pr, -(Kc * vr));
+      const double gr = fma(Kc, vr, -wr), mhr = -(beta * vr);
+      const double xj0 = fma(cx, gr, fma(pj.x, mhr, o.x));
+      const double xj1 = fma(cy, gr, fma(pj.y, mhr, o.y));
+      const double xr = fma(vr, gr, fma(pr, mhr, orr));
+      const double x0 = fma(vr1, gr, fma(pr1, mhr, or1));
+      reflector(r, xj0, xj1, xr, x0);
+    } else if (blk * 16 + 15 > k + 1 && blk * 16 < n) {
+      // ---- w = beta p - K v;  A -= v w^T + w v^T, i.e. a_ij += g_i v_j - h_i p_j
+      double rw[NWB];
+#pragma unroll
+      for (int q = 0; q < NWB; q += 2) {
+        const double2 v2 = *reinterpret_cast<const double2*>(&redw[k & 1][q]);
+        rw[q] = v2.x;
+        rw[q + 1] = v2.y;
+      }
+      const double2 pv = *reinterpret_cast<const double2*>(&pb[k & 1][j0]);
+      const double tot = ((rw[0] + rw[1]) + (rw[2] + rw[3])) + ((rw[4] + rw[5]) + (rw[6] + rw[7]));
+      const double Kc = beta * beta * tot * 0.5;
+      const double wi = fma(beta, pp, -(Kc * vi));
+      const double gi = fma(Kc, vi, -wi), mhi = -(beta * vi);
+      static_for<0, NS / 4>([&](auto G) {
+        constexpr int g = decltype(G)::value;
+        if (4 * g + 3 >= lo) {
+          static_for<4 * g, 4 * g + 4>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            fmac_bcast<s, s == 4 * g>(a[s][0], pv.x, mhi);
+            fmac_bcast<s, false>(a[s][1], pv.y, mhi);
+          });
+          static_for<4 * g, 4 * g + 4>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            fmac_bcast<s, false>(a[s][0], cx, gi);
+            fmac_bcast<s, false>(a[s][1], cy, gi);
+          });
+        }
+      });
+      publish_row(k + 2, rowb[k & 1]);
+    }
+    __syncthreads();
+    if (!chain) {
+      const double2 v2 = *reinterpret_cast<const double2*>(&vb[r & 1][j0]);
+      cx = v2.x;
+      cy = v2.y;
+      vi = vb[r & 1][i];
+      beta = betab[r & 1];
+    }
+  }
+  if (chain) __builtin_amdgcn_s_setprio(0);
+  // the last diagonal entry: row n-1 as its owners published it at the last step (or at the start)
+  if (tid == 0 && n >= 2) dg[n - 1] = rowb[(n - 1) & 1][n - 1];
+  __syncthreads();
+  // Gershgorin interval, scaling and 256-way multisection: as eigmin_reg
+  int bnd_ex = 0;
+  {
+    double lo = INFINITY, hi = -INFINITY;
+    if (tid < n) {
+      double rr = 0.0;
+      if (tid > 0) rr += sqrt(e2[tid - 1]);
+      if (tid + 1 < n) rr += sqrt(e2[tid]);
+      lo = dg[tid] - rr;
+      hi = dg[tid] + rr;
+    }
+    if (w < 2) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o));
+        hi = fmax(hi, __shfl_xor(hi, o));
+      }
+      if (lane == 0) {
+        reinterpret_cast<double*>(masks)[2 * w] = lo;
+        reinterpret_cast<double*>(masks)[2 * w + 1] = hi;
+      }
+    }
+    __syncthreads();
+    const double* m = reinterpret_cast<const double*>(masks);
+    const double l = fmin(m[0], m[2]), h = fmax(m[1], m[3]);
+    const double mag = fmax(fabs(l), fabs(h));
+    const int ex = (mag > 0.0 && mag < INFINITY) ? __builtin_amdgcn_frexp_exp(mag) : 0;
+    bnd_ex = ex;
+    if (tid < 128) {
+      sd[tid] = tid < n ? __builtin_ldexp(dg[tid], -ex) : 4.0;
+      se[tid] = (tid >= 1 && tid < n) ? fmax(__builtin_ldexp(e2[tid - 1], -2 * ex), 0x1p-900) : 0.0;
+    }
+    if (tid == 0) {
+      const double ls = __builtin_ldexp(l, -ex), hs = __builtin_ldexp(h, -ex);
+      const double span = hs - ls;
+      bnd[0] = ls - span * 1e-3 - 1e-300;
+      bnd[1] = hs + span * 1e-3 + 1e-300;
+    }
+  }
+  __syncthreads();
+  double lo = bnd[0], hi = bnd[1];
+  const int nr = (n + 7) & ~7;
+  for (int it = 0; it < 7; ++it) {
+    const double width = hi - lo;
+    if (w < 4) {
+      const double sigma = lo + width * ((double)(tid + 1) / 257.0);
+      const unsigned long long mk = __ballot(sturm_any_below(sd, se, nr, sigma));
+      if (lane == 0) masks[w] = mk;
+    }
+    __syncthreads();
+    int f = -1;
+    for (int q = 0; q < 4 && f < 0; ++q)
+      if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
+    __syncthreads();
+    if (f < 0) {
+      lo = lo + width * (256.0 / 257.0);
+    } else {
+      hi = lo + width * ((double)(f + 1) / 257.0);
+      if (f > 0) lo = lo + width * ((double)f / 257.0);
+    }
+  }
+  if (tid == 0) out[blockIdx.x] = __builtin_ldexp((lo + hi) * 0.5, bnd_ex + ex0);
+}
+
 #ifdef CLRSDP_EIG_STAMPS
 __device__ unsigned long long g_eig_stamps[8];
 #define EIG_STAMP(slot)                                                     \

@@ -141,6 +141,43 @@ def synth_mixed(specs, n_y: int, seed: int = 0) -> tuple:
     return cons, b
 
 
+def synth_C(bi, seed: int, scale: float = 0.125) -> list:
+    """A nonzero constant matrix C (the ``C`` keyword of solverank1sdp, MPMP.jl:599, 691-695) in
+    the block structure of X: per (j,l) a symmetric matrix with entries scale * U[-1,1) (lower
+    triangle drawn, mirrored, so C is exactly symmetric)."""
+    out = []
+    q = 0
+    for j, bj in enumerate(bi.Y_blocksizes):
+        row = []
+        for n in bj:
+            u = uniform(seed, 900_001 + q, n * n).reshape(n, n) * scale
+            Cb = np.tril(u) + np.tril(u, -1).T
+            row.append(Cb)
+            q += 1
+        out.append(row)
+    return out
+
+
+def synth_start(bi, seed: int) -> tuple:
+    """A seeded interior start point (x, X, y, Y) for ``initial_solutions`` (MPMP.jl:613,
+    687-689): X, Y = diagonal in [1, 3) plus a symmetric perturbation below 1/(4n) per entry
+    (strictly diagonally dominant, so positive definite); x, y ~ U[-1/2, 1/2)."""
+    def spd(stream, n):
+        d = uniform(seed, stream, n, 1.0, 3.0)
+        u = uniform(seed, stream + 1, n * n, -1.0, 1.0).reshape(n, n) / (4.0 * n)
+        return np.diag(d) + np.tril(u, -1) + np.tril(u, -1).T
+    nx = sum(bi.dim_S)
+    x = uniform(seed, 810_001, nx, -0.5, 0.5)
+    y = uniform(seed, 810_003, bi.n_y, -0.5, 0.5)
+    X, Y = [], []
+    q = 0
+    for bj in bi.Y_blocksizes:
+        X.append([spd(820_001 + 4 * (q + l), n) for l, n in enumerate(bj)])
+        Y.append([spd(830_001 + 4 * (q + l), n) for l, n in enumerate(bj)])
+        q += len(bj)
+    return x, X, y, Y
+
+
 # Block structure of the sphere-packing instance of examples/SpherePacking.jl (n = 3, d = 8,
 # N = 2 radii; SP.jl:56-105): J = 7 clusters, blocks {2}, {18, 16}, {9, 8} x 3, {1} x 2,
 # dim_S = {3, 51, 17, 17, 17, 1, 1}, n_y = 52 (SURVEY.md §8 "C5").

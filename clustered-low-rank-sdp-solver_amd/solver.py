@@ -248,6 +248,17 @@ class DeviceSolver:
         self.check(self.L.clrsdp_get_factorization(self.h, C.byref(f)))
         return f.value
 
+    def set_graph(self, on: bool):
+        """clrsdp_set_graph: hipGraph replay of the loop body on/off (off: eager enqueue)."""
+        self.check(self.L.clrsdp_set_graph(self.h, 1 if on else 0))
+
+    def comm_info(self):
+        """(ranks, backend) of the exchange: backend 'none', 'rccl' (native communicator, ranks
+        from ncclCommCount) or 'callback' (clrsdp_set_exchange)."""
+        n, b = C.c_int32(0), C.c_int32(0)
+        self.check(self.L.clrsdp_comm_info(self.h, C.byref(n), C.byref(b)))
+        return n.value, {0: "none", 1: "rccl", 2: "callback"}.get(b.value, str(b.value))
+
     def set_stream(self, stream_ptr: int):
         self.check(self.L.clrsdp_set_stream(self.h, C.c_void_p(stream_ptr)))
 
@@ -323,6 +334,20 @@ def initial_point(bi: BlockInfo, omega_p, omega_d):
     y = np.zeros(bi.n_y)
     Y = [[float(omega_d) * np.eye(n) for n in bj] for bj in bi.Y_blocksizes]
     return x, X, y, Y
+
+
+def device_threshold(v, words):
+    """A threshold as the device holds it at `words` limbs (clrsdp_set_control sums the first
+    `words` limbs of :func:`limbs` in the word type, exactly): a float at fp64, else the exact
+    mpmath value, so host comparisons at dd/qd are the device's own."""
+    lv = limbs(v)
+    if words == 1:
+        return lv[0]
+    import mpmath
+    s = mpmath.mpf(0)
+    for x in lv[:words]:
+        s = mpmath.fadd(s, x, exact=True)
+    return s
 
 
 def _terminate(gap, perr, derr, gthr, pthr, dthr, need_p, need_d, out):
@@ -423,9 +448,15 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     dev = solver or DeviceSolver(constraints, b, bi, precision_words=precision_words, C_blocks=C,
                                  device=device)
     prm = make_params(prm_v["beta_infeasible"], prm_v["beta_feasible"], prm_v["gamma"], b0)
-    gthr = float(prm_v["duality_gap_threshold"])
-    pthr = float(prm_v["primal_error_threshold"])
-    dthr = float(prm_v["dual_error_threshold"])
+    # loop control at the state's full width (MPMP.jl:942-945, 1067-1078, 1147-1185 run at the
+    # working precision): at dd/qd the thresholds are the device's exact multi-word values and
+    # the gap, errors and pd_feas are the device's own control_update results (all limbs), so a
+    # threshold below fp64 resolution is decided at the word's precision, and the synchronous
+    # and pipelined loops decide alike
+    exact_ctl = dev.w > 1
+    gthr = device_threshold(prm_v["duality_gap_threshold"], dev.w)
+    pthr = device_threshold(prm_v["primal_error_threshold"], dev.w)
+    dthr = device_threshold(prm_v["dual_error_threshold"], dev.w)
     if initial_solutions is not None and len(initial_solutions) == 4:
         x, X, y, Y = initial_solutions
     else:
@@ -450,6 +481,15 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     dual_gap = abs((p_obj - b0f) - (d_obj - b0f)) / max(1.0, abs((p_obj - b0f) + (d_obj - b0f)))
     perr = max(st.p_err, st.P_err)
     derr = st.d_err
+
+    def device_control():
+        """(gap, primal error, dual error) of the device's last control_update, all limbs."""
+        sc = dev.buffer(_lib.BUF_SCALARS, exact=True)
+        SC = _lib.SC
+        return sc[SC["gap"]], max(sc[SC["err_P"]], sc[SC["err_p"]]), sc[SC["err_d"]]
+
+    if exact_ctl:
+        dual_gap, perr, derr = device_control()
     pd_feas = perr < pthr and derr < dthr
     it = 1
     log = []
@@ -462,7 +502,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
 
     timed = bool(getattr(dev, "timing", False))
 
-    def record(st):
+    def record(st, ctl=None):
         nonlocal p_obj, d_obj, dual_gap, perr, derr, pd_feas, it, fact_seen
         f = dev.factorization
         if f != fact_seen:   # the device switched to LU for the rest of the solve
@@ -483,9 +523,12 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
         log.append(row)
         out("%5d %8.1f %11.3e %11.3e %11.3e %10.2e %10.2e %10.2e %10.2e %10.2e %10.2e %10.2e" % row)
         p_obj, d_obj = st.p_obj, st.d_obj
-        dual_gap = abs(p_obj - d_obj) / max(1.0, abs(p_obj + d_obj))          # MPMP.jl:942
-        perr = max(st.p_err, st.P_err)                                         # MPMP.jl:943
-        derr = st.d_err
+        if ctl is not None:   # the device's full-width values (dd/qd)
+            dual_gap, perr, derr = ctl
+        else:
+            dual_gap = abs(p_obj - d_obj) / max(1.0, abs(p_obj + d_obj))      # MPMP.jl:942
+            perr = max(st.p_err, st.P_err)                                     # MPMP.jl:943
+            derr = st.d_err
         it += 1
         pd_feas = perr < pthr and derr < dthr                                  # MPMP.jl:949-953
 
@@ -524,6 +567,9 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
                 except Exception:
                     pass
                 inflight -= 1
+        if exact_ctl and it > 1:
+            # the control of the last body that ran (a skipped or failed body leaves it as is)
+            dual_gap, perr, derr = device_control()
         if it > 1 or halted:
             # the reference evaluates terminate() (which prints the reason) before iter < maxit
             if term() or halted:
@@ -537,10 +583,16 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
         if it == 3:
             t_after2 = time.time()
         st = dev.iterate(prm, pd_feas)
+        ctl = None
         if record_exact:
             sc = dev.buffer(_lib.BUF_SCALARS, exact=True)
             exact.append({k: sc[v] for k, v in _lib.SC.items()})
-        record(st)
+            if exact_ctl:
+                ctl = (sc[_lib.SC["gap"]], max(sc[_lib.SC["err_P"]], sc[_lib.SC["err_p"]]),
+                       sc[_lib.SC["err_d"]])
+        elif exact_ctl:
+            ctl = device_control()
+        record(st, ctl)
     t_total = time.time() - t_start
     out(HEADER)
     out(_time_spent(t_total, phase / 1e3 if timed else None))

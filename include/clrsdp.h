@@ -255,6 +255,17 @@ int32_t clrsdp_synchronize(clrsdp_handle* h);
  * native RCCL communicator), clrsdp_iterate replays a captured hipGraph of the loop body. */
 int32_t clrsdp_set_timing(clrsdp_handle* h, int32_t on);
 
+/* Loop-body hipGraph replay on (default) or off (on = 0: every body is enqueued eagerly from the
+ * host, launch by launch, as the sharded path without CLRSDP_GRAPH_RCCL does; a measurement
+ * switch, e.g. for the host enqueue time of one body).  No reference counterpart. */
+int32_t clrsdp_set_graph(clrsdp_handle* h, int32_t on);
+
+/* The exchange this handle's loop body uses: *backend 0 = none (one rank),
+ * 1 = the native RCCL communicator of clrsdp_comm_init (*nranks = ncclCommCount of it),
+ * 2 = the clrsdp_set_exchange callback (*nranks = world_size).  Replaces nothing in the
+ * reference (shared-memory threads, MPMP.jl:1486-1494, 1758-1761). */
+int32_t clrsdp_comm_info(const clrsdp_handle* h, int32_t* nranks, int32_t* backend);
+
 /* Factorisations of S_j, Q and X (flags, default CLRSDP_FACT_FALLBACK).  The device factorises
  * S_j and Q by Cholesky (they are SPD) and X^-1 by the Cholesky inverse (spd_inv!).  The
  * reference factorises S_j and Q by partially pivoted LU (approx_lu!, MPMP.jl:1433-1442,

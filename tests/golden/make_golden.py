@@ -45,7 +45,29 @@ def make_instance(inst):
     return pk.synth(**inst)
 
 
-def run(name, inst, iters, prec=None, tol=1e-9, params=None):
+def keyword_args(pk_, ar, bi, kw):
+    """The solverank1sdp keywords of a golden run (round 4): C from synth_C(C_seed, C_scale), b0,
+    need_primal/dual_feasible, initial_solutions from synth_start(start_seed); the same
+    construction is used by the GPU tests (tests/test_gpu_keywords.py)."""
+    out = {}
+    if not kw:
+        return out
+    if "C_seed" in kw:
+        Cb = pk_.synth_C(bi, kw["C_seed"], kw.get("C_scale", 0.125))
+        out["C"] = [[ar.asarray(m) for m in row] for row in Cb]
+    if "b0" in kw:
+        out["b0"] = kw["b0"]
+    for k in ("need_primal_feasible", "need_dual_feasible"):
+        if kw.get(k):
+            out[k] = True
+    if "start_seed" in kw:
+        x, X, y, Y = pk_.synth_start(bi, kw["start_seed"])
+        out["initial_solutions"] = (ar.asarray(x), [[ar.asarray(m) for m in r] for r in X],
+                                    ar.asarray(y), [[ar.asarray(m) for m in r] for r in Y])
+    return out
+
+
+def run(name, inst, iters, prec=None, tol=1e-9, params=None, keywords=None):
     cons, b = make_instance(inst)
     bi = O.get_block_info(cons)
     if prec:
@@ -56,11 +78,15 @@ def run(name, inst, iters, prec=None, tol=1e-9, params=None):
         ar = O.Fp64()
         consr, br = cons, b
     params = params or PARAMS
-    res = O.solverank1sdp(consr, br, bi, ar=ar, maxiterations=iters + 1, **params)
+    kwa = keyword_args(pk, ar, bi, keywords)
+    if "b0" in kwa:
+        kwa["b0"] = ar.num(kwa["b0"]) if prec else kwa["b0"]
+    res = O.solverank1sdp(consr, br, bi, ar=ar, maxiterations=iters + 1, **params, **kwa)
     fmt = (lambda v: mpmath.nstr(v, 70)) if prec else (lambda v: repr(float(v)))
     out = {
         "generator": "tests/golden/make_golden.py (oracle/mpmp_oracle.py, %s)" % ar.name,
         "instance": inst, "params": params, "iterations": iters, "tolerance_fp64": tol,
+        "keywords": keywords or {},
         "log": [{k: fmt(getattr(r, k)) for k in ("mu", "p_obj", "d_obj", "gap", "P_err", "p_err",
                                                   "d_err", "alpha_p", "alpha_d", "beta")}
                 for r in res.log],
@@ -84,6 +110,25 @@ if __name__ == "__main__":
         run("sp_real_d8_mp256_full", dict(kind="sphere_packing", n=3, d=8), 120, prec=256,
             params=dict(omega_p=100.0, omega_d=100.0, duality_gap_threshold=1e-15,
                         primal_error_threshold=1e-30, dual_error_threshold=1e-30))
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "gap24":
+        # round 4: loop control below fp64 resolution (duality gap 1e-24, double-double on the
+        # device): the 256-bit run to termination fixes the iteration the dd loops must stop at
+        run("rank2_mp256_seed5_gap24", dict(J=2, delta=3, rank=2, n_y=3, seed=5), 120, prec=256,
+            params=dict(omega_p=10.0, omega_d=10.0, duality_gap_threshold=1e-24,
+                        primal_error_threshold=1e-20, dual_error_threshold=1e-20))
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "keywords":
+        # round 4: the solverank1sdp keywords every earlier golden left at their defaults
+        # (C = 0, b0 = 0, no early feasibility stop, the default start; MPMP.jl:599-613)
+        m2 = dict(J=2, delta=3, rank=1, n_y=3, m=2, L=2, seed=4)
+        c1 = dict(J=2, delta=4, rank=1, n_y=4, seed=3)
+        run("kw_C_b0_mp256", m2, 12, prec=256, keywords=dict(C_seed=21, C_scale=0.125, b0=0.75))
+        run("kw_needp_mp256", c1, 40, prec=256, keywords=dict(need_primal_feasible=True),
+            params=dict(PARAMS, primal_error_threshold=1e-6))
+        run("kw_needd_mp256", m2, 40, prec=256, keywords=dict(need_dual_feasible=True),
+            params=dict(PARAMS, dual_error_threshold=1e-6))
+        run("kw_start_mp256", c1, 12, prec=256, keywords=dict(start_seed=5, C_seed=22))
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "sp":  # only the config-5-shape vector (~40 s)
         run("sp_mp256_seed1", dict(kind="sphere_packing_shape", seed=1), 12, prec=256)
