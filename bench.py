@@ -259,10 +259,12 @@ def main():
     n_inst = max(3, min(args.steps, 10))
     schur_ms = 0.0
     phase = np.zeros(_lib.NUM_STAGES)
+    inner = np.zeros(_lib.NUM_INNER)
     for _ in range(n_inst):
         st = step()
         ph = np.array(st.phase_ms[:])
         phase += ph
+        inner += np.array(st.inner_ms[:])
         schur_ms += ph[_lib.STAGE_SCHUR]
     barrier_sync()
     dev.set_timing(False)
@@ -349,6 +351,8 @@ def main():
                      "schur_time_source": schur_src,
                      "schur_alg_gbs": by / sch_s / 1e9},
         "phase_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.STAGE_NAMES, phase)},
+        # the reference's inner buckets (MPMP.jl:997-1012), same instrumented pass
+        "inner_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.INNER_NAMES, inner)},
         "graph_replay": world == 1 or (getattr(dist, "backend", "") == "rccl"
                                        and os.environ.get("CLRSDP_GRAPH_RCCL") is not None),
         "exchange": "none (1 GPU)" if dist is None else dist.backend,

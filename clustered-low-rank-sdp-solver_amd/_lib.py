@@ -17,6 +17,10 @@ E_ARG, E_HIP, E_NOT_PD_X, E_NOT_PD_S, E_NOT_PD_Q, E_STEP, E_EXCHANGE, E_STATE = 
 STAGE_MU_R, STAGE_XINV, STAGE_SCHUR, STAGE_FACTOR, STAGE_RESIDUALS, STAGE_PREDICTOR, \
     STAGE_CORRECTOR_R, STAGE_CORRECTOR, STAGE_STEP, STAGE_UPDATE = range(10)
 NUM_STAGES = 10
+NUM_INNER = 10
+# the reference's inner timing buckets (MPMP.jl:897-898, 997-1012), clrsdp_iter_stats.inner_ms
+INNER_NAMES = ["schur", "chol_S", "comp CinvB", "comp Q", "chol_Q", "calc Z", "calc rhs x",
+               "solve system", "calc dX", "calc dY"]
 STAGE_NAMES = ["mu_R", "Xinv", "schur", "factor", "residuals", "predictor", "corrector_R",
                "corrector", "step", "update"]
 
@@ -70,7 +74,10 @@ class IterStats(C.Structure):
     _fields_ = [("mu", C.c_double), ("P_err", C.c_double), ("p_err", C.c_double),
                 ("d_err", C.c_double), ("alpha_p", C.c_double), ("alpha_d", C.c_double),
                 ("beta_c", C.c_double), ("p_obj", C.c_double), ("d_obj", C.c_double),
-                ("phase_ms", C.c_double * NUM_STAGES), ("status", C.c_int32)]
+                ("phase_ms", C.c_double * NUM_STAGES), ("status", C.c_int32),
+                ("inner_ms", C.c_double * NUM_INNER), ("gap_w", C.c_double * 4),
+                ("P_err_w", C.c_double * 4), ("p_err_w", C.c_double * 4),
+                ("d_err_w", C.c_double * 4)]
 
 
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.c_int64, C.c_void_p)

@@ -18,7 +18,10 @@
 #include <cstdlib>
 #include <memory>
 #include <string>
+#include <array>
 #include <vector>
+#include <vector>
+#include <array>
 
 #include "../../include/clrsdp.h"
 #include "kernels.h"
@@ -931,6 +934,27 @@ struct Solver final : HandleBase {
   TupleDesc* d_td = nullptr;
   TupleBlock* d_tb = nullptr;
   hipEvent_t ev[CLRSDP_NUM_STAGES + 1];
+  // timing mode 1: inner buckets (CLRSDP_INNER_*), one event pair per segment, recorded on the
+  // stream the segment's launches go to (so side-stream work is measured on its own stream)
+  std::vector<hipEvent_t> seg_pool;
+  std::vector<std::array<int, 3>> segs;  // (bucket, begin event, end event)
+  template <class F>
+  void seg(int bucket, F&& work) {
+    if (timing != 1) {
+      work();
+      return;
+    }
+    const int b = (int)segs.size() * 2;
+    while ((int)seg_pool.size() < b + 2) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      seg_pool.push_back(e);
+    }
+    HIPCHK(hipEventRecord(seg_pool[b], stream));
+    work();
+    HIPCHK(hipEventRecord(seg_pool[b + 1], stream));
+    segs.push_back({bucket, b, b + 1});
+  }
   // side stream: the local residuals overlap the Schur factorisation, chol(Q) overlaps the
   // first part of the predictor (iterate only; run_stage stays serial)
   hipStream_t aux = nullptr;
@@ -1067,6 +1091,7 @@ struct Solver final : HandleBase {
     for (char* r : ring_host)
       if (r) (void)hipHostFree(r);
     for (auto& e : ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : seg_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ev_ty, ev_join, ring_ev[0], ring_ev[1]})
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
@@ -1930,50 +1955,66 @@ struct Solver final : HandleBase {
   }
   // side_x21: X21 on the side stream (the loop body), joined before the first solve
   void factor_local(bool side_x21 = false) {
+    // (inner timing buckets: a mixed batch counts where most of its work is; the reference's
+    // chol_S / CinvB / Q split, MPMP.jl:1429-1495)
     if (lu_sq()) {                            // approx_lu! (MPMP.jl:1433-1494)
-      lu_S.launch(stream, info + info_S0);
-      pm_B.launch(stream);
-      tl_W1.launch(stream, false);            // W1_j = L_j^-1 B_j[perm_j]
-      vlin(W2m, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
-      tl_W2.launch(stream, false);            // W2_j = U_j^-T B_j
-      lq_slab.launch(stream, 1.0, 0.0);       // slab_j = W2_j^T W1_j
-      sum_q_slabs();
+      seg(CLRSDP_INNER_CHOL_S, [&] { lu_S.launch(stream, info + info_S0); });
+      seg(CLRSDP_INNER_CINVB, [&] {
+        pm_B.launch(stream);
+        tl_W1.launch(stream, false);          // W1_j = L_j^-1 B_j[perm_j]
+        vlin(W2m, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
+        tl_W2.launch(stream, false);          // W2_j = U_j^-T B_j
+      });
+      seg(CLRSDP_INNER_Q, [&] {
+        lq_slab.launch(stream, 1.0, 0.0);     // slab_j = W2_j^T W1_j
+        sum_q_slabs();
+      });
       return;
     }
     if (fac2) {                               // fp64: S_j <- L_j^-1 in place, W_j and Q's slabs
-      ci_S.launch(stream, info + info_S0);    // S (dim_S <= 128) and S11 blocks
-      f_a.launch(stream, 1.0, 0.0);
-      f_b.launch(stream, 1.0, 0.0);
+      seg(CLRSDP_INNER_CHOL_S, [&] { ci_S.launch(stream, info + info_S0); });  // S / S11 blocks
+      seg(CLRSDP_INNER_CINVB, [&] { f_a.launch(stream, 1.0, 0.0); });          // {L21^T, W1}
+      seg(CLRSDP_INNER_CHOL_S, [&] { f_b.launch(stream, 1.0, 0.0); });         // S22 - L21 L21^T, ...
       if (nc2) {
-        ci_S22.launch(stream, info + info_S0 + nc());
+        seg(CLRSDP_INNER_CHOL_S, [&] { ci_S22.launch(stream, info + info_S0 + nc()); });
         if (side_x21) {
           const hipStream_t main_s = stream;
           HIPCHK(hipEventRecord(ev_x2, main_s));
           HIPCHK(hipStreamWaitEvent(aux, ev_x2, 0));
-          f_x1.launch(aux, 1.0, 0.0);
-          f_x2.launch(aux, -1.0, 0.0);
+          stream = aux;
+          seg(CLRSDP_INNER_CHOL_S, [&] {
+            f_x1.launch(aux, 1.0, 0.0);
+            f_x2.launch(aux, -1.0, 0.0);
+          });
+          stream = main_s;
           HIPCHK(hipEventRecord(ev_x21, aux));
           pending_x21 = true;
         } else {
-          f_x1.launch(stream, 1.0, 0.0);
-          f_x2.launch(stream, -1.0, 0.0);
+          seg(CLRSDP_INNER_CHOL_S, [&] {
+            f_x1.launch(stream, 1.0, 0.0);
+            f_x2.launch(stream, -1.0, 0.0);
+          });
         }
-        f_c.launch(stream, 1.0, 0.0);
-        f_d.launch(stream, 1.0, 1.0);
+        seg(CLRSDP_INNER_CINVB, [&] { f_c.launch(stream, 1.0, 0.0); });
+        seg(CLRSDP_INNER_Q, [&] { f_d.launch(stream, 1.0, 1.0); });
       }
-      sum_q_slabs();
+      seg(CLRSDP_INNER_Q, [&] { sum_q_slabs(); });
       return;
     }
     if (reg_S) {                              // S_j <- L_j^-1 in place; W_j = L_j^-1 B_j (MFMA)
-      ci_S.launch(stream, info + info_S0);
-      q_W.launch(stream, 1.0, 0.0);
+      seg(CLRSDP_INNER_CHOL_S, [&] { ci_S.launch(stream, info + info_S0); });
+      seg(CLRSDP_INNER_CINVB, [&] { q_W.launch(stream, 1.0, 0.0); });
     } else {
-      f_S.potrf(stream, info + info_S0);
-      vlin(Wm, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
-      t_W.launch(stream, false);              // W_j = L_j^-1 B_j
+      seg(CLRSDP_INNER_CHOL_S, [&] { f_S.potrf(stream, info + info_S0); });
+      seg(CLRSDP_INNER_CINVB, [&] {
+        vlin(Wm, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
+        t_W.launch(stream, false);            // W_j = L_j^-1 B_j
+      });
     }
-    p_Q.launch(stream, 1.0, 0.0);             // slab_j = W_j^T W_j
-    sum_q_slabs();
+    seg(CLRSDP_INNER_Q, [&] {
+      p_Q.launch(stream, 1.0, 0.0);           // slab_j = W_j^T W_j
+      sum_q_slabs();
+    });
   }
   // Q = sum_j slab_j (all-gathered over the ranks)
   void sum_q_slabs() {
@@ -1988,6 +2029,9 @@ struct Solver final : HandleBase {
     }
   }
   void factor_q() {
+    seg(CLRSDP_INNER_CHOL_Q, [&] { factor_q_(); });
+  }
+  void factor_q_() {
     const int64_t q2 = n_y * n_y;
     if (lu_sq()) {                            // approx_lu!(perm, Q) (MPMP.jl:1499-1505)
       vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
@@ -2060,6 +2104,9 @@ struct Solver final : HandleBase {
   // Z = sym(X^-1 (P Y - R)) and the trace_A products U = Z V (no factorisation needed: in a
   // loop body the predictor's share runs on the side stream during FACTOR)
   void direction_Z() {
+    seg(CLRSDP_INNER_Z, [&] { direction_Z_(); });
+  }
+  void direction_Z_() {
     p_PY.launch(stream, 1.0, -1.0);
     p_Z.launch(stream, 1.0, 0.0);
     // Z is only consumed by trace_A: v^T Z v = v^T sym(Z) v, so the symmetrisation
@@ -2069,6 +2116,9 @@ struct Solver final : HandleBase {
   }
   // rhs_x = -d - Tr(A_* Z)   (MPMP.jl:1733-1739)
   void direction_rhs() {
+    seg(CLRSDP_INNER_RHS_X, [&] { direction_rhs_(); });
+  }
+  void direction_rhs_() {
     if (trivial_tuples) {
       dim3 g(cdiv(max_K, 4), n_pair);
       colsum_rhs<T><<<g, 256, 0, stream>>>(d_pair, TU, V, lam, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
@@ -2079,13 +2129,15 @@ struct Solver final : HandleBase {
   }
   // the block solve (MPMP.jl:1743-1776), dX and dY
   void direction_rest(int tag) {
-    direction_solves(tag);
+    seg(CLRSDP_INNER_SOLVE, [&] { direction_solves(tag); });
     // dX = P + sum_i dx_i A_i
-    weighted_A(dx, p_wA_dX, dX, 1.0);
+    seg(CLRSDP_INNER_DX, [&] { weighted_A(dx, p_wA_dX, dX, 1.0); });
     // dY = sym(X^-1 (R - dX Y))
-    p_dXY.launch(stream, -1.0, 1.0);
-    p_dY.launch(stream, 1.0, 0.0);
-    sym(dY, dY, 0);
+    seg(CLRSDP_INNER_DY, [&] {
+      p_dXY.launch(stream, -1.0, 1.0);
+      p_dY.launch(stream, 1.0, 0.0);
+      sym(dY, dY, 0);
+    });
   }
   // the three-stage solve and dx as separate batched launches (any word type / rank count)
   void direction_solves(int tag) {
@@ -2333,6 +2385,14 @@ struct Solver final : HandleBase {
     st->beta_c = f(SC_BETA_C);
     st->p_obj = f(SC_POBJ);
     st->d_obj = f(SC_DOBJ);
+    auto limbs_of = [&](int i, double* dst) {
+      const double* l = reinterpret_cast<const double*>(&h[i]);
+      for (int q = 0; q < 4; ++q) dst[q] = q < Num<T>::W ? l[q] : 0.0;
+    };
+    limbs_of(SC_GAP, st->gap_w);
+    limbs_of(SC_ERR_PMAT, st->P_err_w);
+    limbs_of(SC_ERR_PVEC, st->p_err_w);
+    limbs_of(SC_ERR_DVEC, st->d_err_w);
   }
 
   int initial(const clrsdp_params* prm, clrsdp_iter_stats* st) override {
@@ -2347,6 +2407,7 @@ struct Solver final : HandleBase {
 
   // Enqueue one loop body (all stages) on `stream`, with the side stream joined back in.
   void enqueue_iteration(const clrsdp_params* prm, int pd_feas) {
+    segs.clear();
     // (the status words are cleared by the first scalar launch of MU_R)
     auto mark = [&](int s) {
       if (timing == 1) HIPCHK(hipEventRecord(ev[s], stream));
@@ -2517,12 +2578,19 @@ struct Solver final : HandleBase {
         if (t[2 * q + 1] > t[2 * q]) ticks += (double)(t[2 * q + 1] - t[2 * q]);
       st->phase_ms[CLRSDP_STAGE_SCHUR] = ticks * 1e-5;  // 100 MHz
     }
-    if (timing == 1)
+    if (timing == 1) {
       for (int s = 0; s < CLRSDP_NUM_STAGES; ++s) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ev[s], ev[s + 1]));
         st->phase_ms[s] = ms;
       }
+      for (const auto& g : segs) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, seg_pool[g[1]], seg_pool[g[2]]));
+        st->inner_ms[g[0]] += ms;
+      }
+      st->inner_ms[CLRSDP_INNER_SCHUR] = st->phase_ms[CLRSDP_STAGE_SCHUR];
+    }
     const int rc = check_info();
     st->status = rc;
     return rc;
@@ -2621,7 +2689,10 @@ struct Solver final : HandleBase {
 
   int run_stage(int s, const clrsdp_params* prm, int pd_feas) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
-    if (s == 0) HIPCHK(hipMemsetAsync(info, 0, info_count * sizeof(int), stream));
+    if (s == 0) {
+      HIPCHK(hipMemsetAsync(info, 0, info_count * sizeof(int), stream));
+      segs.clear();
+    }
     stage(s, prm, pd_feas);
     flush_scalars();
     stat_fetch();

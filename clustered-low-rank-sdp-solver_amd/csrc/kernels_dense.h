@@ -888,9 +888,27 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
 // The chain lane (c, t16) holds the same column pair j0 = 2c + 8 t16 as a bulk lane, so its sums
 // run in eigmin_reg's order.  Same scaling, Gershgorin bracket and multisection as eigmin_reg.
 // ------------------------------------------------------------------------------------------
+#ifdef CLRSDP_EIGSPLIT_STAMPS
+__device__ unsigned long long g_eigsplit_stamps[8];
+#endif
 __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __restrict__ descs,
                                                      double* __restrict__ out) {
   constexpr int NS = 16, NWB = 8;
+#ifdef CLRSDP_EIGSPLIT_STAMPS
+  // per column: chain lane 0 (slots 0-2: wait at barrier 1, reflector, wait at barrier 2) and
+  // bulk wave 4 lane 0 (row block 7, live to the end; slots 3-6: matvec phase, wait at barrier
+  // 1, update phase, wait at barrier 2); slot 7: multisection
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#define ES_STAMP(slot)                                            \
+  {                                                               \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+    st_acc[slot] += t_ - t_prev;                                  \
+    t_prev = t_;                                                  \
+  }
+#else
+#define ES_STAMP(slot)
+#endif
   __shared__ __attribute__((aligned(16))) double rowb[2][128];
   __shared__ __attribute__((aligned(16))) double pb[2][128];
   __shared__ __attribute__((aligned(16))) double vb[2][128];
@@ -1036,8 +1054,10 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
       }
       t = row16_sum(t);  // class-0 lanes carry the rows' v_i p_i
       if (lane == 0) redw[k & 1][w] = t;
+      ES_STAMP(3)
     }
     __syncthreads();
+    ES_STAMP(chain ? 0 : 4)
     const int r = k + 1;
     if (chain) {
       // ---- row r of A_{k+1} and the reflector v_{k+1}
@@ -1063,6 +1083,7 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
       const double xr = fma(vr, gr, fma(pr, mhr, orr));
       const double x0 = fma(vr1, gr, fma(pr1, mhr, or1));
       reflector(r, xj0, xj1, xr, x0);
+      ES_STAMP(1)
     } else if (blk * 16 + 15 > k + 1 && blk * 16 < n) {
       // ---- w = beta p - K v;  A -= v w^T + w v^T, i.e. a_ij += g_i v_j - h_i p_j
       double rw[NWB];
@@ -1093,8 +1114,10 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
         }
       });
       publish_row(k + 2, rowb[k & 1]);
+      ES_STAMP(5)
     }
     __syncthreads();
+    ES_STAMP(chain ? 2 : 6)
     if (!chain) {
       const double2 v2 = *reinterpret_cast<const double2*>(&vb[r & 1][j0]);
       cx = v2.x;
@@ -1169,6 +1192,13 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
     }
   }
   if (tid == 0) out[blockIdx.x] = __builtin_ldexp((lo + hi) * 0.5, bnd_ex + ex0);
+#ifdef CLRSDP_EIGSPLIT_STAMPS
+  ES_STAMP(7)
+  if (lane == 0 && (chain || w == 4))
+    for (int q = 0; q < 8; ++q)
+      if ((chain && q < 3) || (!chain && q >= 3)) atomicAdd(&g_eigsplit_stamps[q], st_acc[q]);
+#endif
+#undef ES_STAMP
 }
 
 #ifdef CLRSDP_EIG_STAMPS

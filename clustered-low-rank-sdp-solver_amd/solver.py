@@ -381,6 +381,7 @@ class RunInfo:
     exact: list = None   # per iteration, the device scalar slots at full precision (record_exact)
     factorization: int = 1  # clrsdp_get_factorization at the end (an LU fallback adds its flag)
     lu_switch: int = 0      # iteration whose loop body switched to LU (0: none)
+    inner_ms: np.ndarray = None  # the reference's inner buckets summed from iteration 3 (ms)
 
 
 def _stage_groups(ph):
@@ -399,7 +400,7 @@ def _first_iteration_times(ph):
                 g["Xinv"], g["R"], g["res"]))
 
 
-def _time_spent(total, ph):
+def _time_spent(total, ph, inner=None):
     """MPMP.jl:973-1012.  Per-stage device times (sums over iterations 3, 4, ...) need the
     handle's HIP-event timing (DeviceSolver(timing=True)); without it only the total is known."""
     cols = ["total", "Decomp", "predict_dir", "correct_dir", "alpha", "Xinv", "R", "res"]
@@ -411,8 +412,19 @@ def _time_spent(total, ph):
         return "\n".join(lines) + "\n"
     g = _stage_groups(ph)
     lines.append(("%11.5e " * len(cols)).rstrip() % tuple([total] + [g[c] for c in cols[1:]]))
-    lines.append("\nTime inside decomp:\n%11s %11s\n%11.5e %11.5e" % (
-        "schur", "factor", ph[2], ph[3]))
+    if inner is None:
+        lines.append("\nTime inside decomp:\n%11s %11s\n%11.5e %11.5e" % (
+            "schur", "factor", ph[2], ph[3]))
+        return "\n".join(lines) + "\n"
+    # MPMP.jl:997-1012: the inner buckets (clrsdp_iter_stats.inner_ms, device time of each
+    # bucket's launches; the direction buckets summed over predictor and corrector)
+    lines.append("\nTime inside decomp:")
+    lines.append(("%11s " * 5).rstrip() % ("schur", "chol_S", "comp CinvB", "comp Q", "chol_Q"))
+    lines.append(("%11.5e " * 5).rstrip() % tuple(inner[:5]))
+    lines.append("\nTime inside search directions (both predictor & corrector step)")
+    lines.append(("%11s " * 5).rstrip() % ("calc Z", "calc rhs x", "solve system", "calc dX",
+                                          "calc dY"))
+    lines.append(("%11.5e " * 5).rstrip() % tuple(inner[5:10]))
     return "\n".join(lines) + "\n"
 
 
@@ -482,18 +494,25 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     perr = max(st.p_err, st.P_err)
     derr = st.d_err
 
-    def device_control():
-        """(gap, primal error, dual error) of the device's last control_update, all limbs."""
-        sc = dev.buffer(_lib.BUF_SCALARS, exact=True)
-        SC = _lib.SC
-        return sc[SC["gap"]], max(sc[SC["err_P"]], sc[SC["err_p"]]), sc[SC["err_d"]]
+    def device_control(st):
+        """(gap, primal error, dual error) of the device's control_update for the state after
+        the body `st` reports, all limbs (exact mpmath sums)."""
+        import mpmath
+
+        def v(limbs_):
+            r = mpmath.mpf(0)
+            for x in list(limbs_)[:dev.w]:
+                r = mpmath.fadd(r, x, exact=True)
+            return r
+        return v(st.gap_w), max(v(st.P_err_w), v(st.p_err_w)), v(st.d_err_w)
 
     if exact_ctl:
-        dual_gap, perr, derr = device_control()
+        dual_gap, perr, derr = device_control(st)
     pd_feas = perr < pthr and derr < dthr
     it = 1
     log = []
     phase = np.zeros(_lib.NUM_STAGES)
+    inner = np.zeros(_lib.NUM_INNER)
     t_start = time.time()
     t_after2 = None
     status = "maxiterations"
@@ -502,7 +521,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
 
     timed = bool(getattr(dev, "timing", False))
 
-    def record(st, ctl=None):
+    def record(st):
         nonlocal p_obj, d_obj, dual_gap, perr, derr, pd_feas, it, fact_seen
         f = dev.factorization
         if f != fact_seen:   # the device switched to LU for the rest of the solve
@@ -516,6 +535,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
             lu_switch[0] = lu_switch[0] or it
         if it > 2:
             phase[:] += np.array(st.phase_ms[:])
+            inner[:] += np.array(st.inner_ms[:])
         elif testing and timed:  # MPMP.jl:899-920: the times of the first iterations
             out(_first_iteration_times(np.array(st.phase_ms[:]) / 1e3))
         row = (it, time.time() - t_start, st.mu, p_obj, d_obj, dual_gap, st.P_err, st.p_err,
@@ -523,8 +543,8 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
         log.append(row)
         out("%5d %8.1f %11.3e %11.3e %11.3e %10.2e %10.2e %10.2e %10.2e %10.2e %10.2e %10.2e" % row)
         p_obj, d_obj = st.p_obj, st.d_obj
-        if ctl is not None:   # the device's full-width values (dd/qd)
-            dual_gap, perr, derr = ctl
+        if exact_ctl:   # the device's full-width values (dd/qd)
+            dual_gap, perr, derr = device_control(st)
         else:
             dual_gap = abs(p_obj - d_obj) / max(1.0, abs(p_obj + d_obj))      # MPMP.jl:942
             perr = max(st.p_err, st.P_err)                                     # MPMP.jl:943
@@ -567,9 +587,6 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
                 except Exception:
                     pass
                 inflight -= 1
-        if exact_ctl and it > 1:
-            # the control of the last body that ran (a skipped or failed body leaves it as is)
-            dual_gap, perr, derr = device_control()
         if it > 1 or halted:
             # the reference evaluates terminate() (which prints the reason) before iter < maxit
             if term() or halted:
@@ -583,19 +600,13 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
         if it == 3:
             t_after2 = time.time()
         st = dev.iterate(prm, pd_feas)
-        ctl = None
         if record_exact:
             sc = dev.buffer(_lib.BUF_SCALARS, exact=True)
             exact.append({k: sc[v] for k, v in _lib.SC.items()})
-            if exact_ctl:
-                ctl = (sc[_lib.SC["gap"]], max(sc[_lib.SC["err_P"]], sc[_lib.SC["err_p"]]),
-                       sc[_lib.SC["err_d"]])
-        elif exact_ctl:
-            ctl = device_control()
-        record(st, ctl)
+        record(st)
     t_total = time.time() - t_start
     out(HEADER)
-    out(_time_spent(t_total, phase / 1e3 if timed else None))
+    out(_time_spent(t_total, phase / 1e3 if timed else None, inner / 1e3 if timed else None))
     xf, Xf, yf, Yf = dev.get_state()
     P, d = dev.global_P_d()
     p = dev.buffer(_lib.BUF_PVEC)
@@ -615,7 +626,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     if return_info:
         res = res + (RunInfo(it - 1, log, phase, t_total,
                              (time.time() - t_after2) if t_after2 else 0.0, status, exact,
-                             dev.factorization, lu_switch[0]),)
+                             dev.factorization, lu_switch[0], inner),)
     if solver is None:
         dev.close()
     return res

@@ -52,6 +52,20 @@ extern "C" {
 #define CLRSDP_STAGE_UPDATE 9      /* x,y,X,Y += alpha d*, new objectives     (877-887, 940-941) */
 #define CLRSDP_NUM_STAGES 10
 
+/* Inner buckets of the reference's timing table (MPMP.jl:897-898: "Time inside decomp" and
+ * "Time inside search directions", printed at 997-1012) */
+#define CLRSDP_INNER_SCHUR 0       /* compute_S_integrated                                       */
+#define CLRSDP_INNER_CHOL_S 1      /* factorisation of S_j (Cholesky + L^-1, or approx_lu!)      */
+#define CLRSDP_INNER_CINVB 2       /* L_j^-1 B_j (and B_j^T U_j^-1)                               */
+#define CLRSDP_INNER_Q 3           /* Q = sum_j W_j^T W_j (+ the exchange)                        */
+#define CLRSDP_INNER_CHOL_Q 4      /* factorisation of Q                                          */
+#define CLRSDP_INNER_Z 5           /* Z = sym(X^-1 (P Y - R)) and its trace_A products            */
+#define CLRSDP_INNER_RHS_X 6       /* rhs_x = -d - Tr(A_* Z)                                      */
+#define CLRSDP_INNER_SOLVE 7       /* the block solve for dx, dy                                  */
+#define CLRSDP_INNER_DX 8          /* dX = P + sum dx_i A_i                                        */
+#define CLRSDP_INNER_DY 9          /* dY = sym(X^-1 (R - dX Y))                                    */
+#define CLRSDP_NUM_INNER 10
+
 /* ---- device buffers readable with clrsdp_get_buffer (stage-level parity tests) ----------- */
 #define CLRSDP_BUF_X 0        /* block-diagonal state X, blocks concatenated, column-major   */
 #define CLRSDP_BUF_Y 1
@@ -147,6 +161,18 @@ typedef struct {
   double d_obj;     /* <C,Y> + <b,y> + b0 after the update                        (941)      */
   double phase_ms[CLRSDP_NUM_STAGES]; /* per-stage device time when config.timing != 0       */
   int32_t status;
+  /* timing mode 1 only: the reference's inner timings (MPMP.jl:897-898, 997-1012), device time
+   * of the launches of each bucket (side-stream work included, measured on its own stream):
+   * CLRSDP_INNER_* below; the direction buckets are predictor + corrector */
+  double inner_ms[CLRSDP_NUM_INNER];
+  /* the loop control of the state after this body at the word's full width (up to 4 limbs, hi
+   * first; unused limbs 0): the duality gap (MPMP.jl:942; for clrsdp_initial_residuals the gap
+   * without b0, 725) and the errors of the residuals computed in this body (943-944), as the
+   * device's terminate()/check_pd_feasibility() compares them (1147-1185) */
+  double gap_w[4];
+  double P_err_w[4];
+  double p_err_w[4];
+  double d_err_w[4];
 } clrsdp_iter_stats;
 
 /* Multi-rank exchange: gather `bytes` bytes from `send_dev` on every rank into `recv_dev`

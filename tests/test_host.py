@@ -185,3 +185,86 @@ def test_time_spent_report_groups_stages_like_the_reference(pk):
     txt = _time_spent(2.0, ph)
     assert "Time spent" in txt and "Decomp" in txt and "Time inside decomp" in txt
     assert "timing=True" in _time_spent(2.0, None)
+
+
+def test_time_spent_report_prints_the_reference_inner_buckets(pk):
+    """With the inner buckets (clrsdp_iter_stats.inner_ms) the report has MPMP.jl:997-1012's two
+    inner tables: schur / chol_S / comp CinvB / comp Q / chol_Q and calc Z ... calc dY."""
+    from clrsdp_amd import _lib
+    from clrsdp_amd.solver import _time_spent
+    assert _lib.NUM_INNER == len(_lib.INNER_NAMES) == 10
+    ph = np.ones(_lib.NUM_STAGES)
+    txt = _time_spent(1.0, ph, np.arange(1.0, 11.0))
+    for h in ("chol_S", "comp CinvB", "comp Q", "chol_Q", "calc Z", "calc rhs x", "solve system",
+              "calc dX", "calc dY", "Time inside search directions"):
+        assert h in txt
+    assert "1.00000e+01" in txt   # the last bucket (calc dY)
+
+
+def test_iter_stats_layout_matches_the_header(pk):
+    """The ctypes mirror of clrsdp_iter_stats has the header's fields in order (the full-width
+    loop-control limbs and the inner buckets were appended in round 4)."""
+    import re
+    from clrsdp_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "clrsdp.h")).read()
+    body = re.search(r"typedef struct \{([^}]*)\} clrsdp_iter_stats;", hdr, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"(\w+)(?:\[[^\]]*\])?;", body)
+    assert names == [f[0] for f in _lib.IterStats._fields_]
+
+
+def test_device_thresholds_are_exact_limb_sums():
+    """Loop control at dd/qd compares against the threshold the device holds (the first w limbs
+    of the decimal string, summed exactly), so 1e-24 is not rounded to fp64 on the host."""
+    import mpmath
+    from clrsdp_amd.solver import device_threshold, limbs
+    assert device_threshold("1e-24", 1) == float("1e-24")
+    for w in (2, 4):
+        t = device_threshold("1e-24", w)
+        assert isinstance(t, mpmath.mpf)
+        with mpmath.workprec(400):
+            assert t == mpmath.fsum(limbs("1e-24")[:w])
+            assert abs(t - mpmath.mpf("1e-24")) < mpmath.mpf("1e-24") * mpmath.mpf(2) ** (-52 * w)
+    # a gap a few ulps of fp64 below the threshold is decided correctly at dd
+    g = device_threshold("1e-24", 2) * (1 - mpmath.mpf(2) ** -80)
+    assert g < device_threshold("1e-24", 2) and not float(g) < float("1e-24") * (1 - 2 ** -52)
+
+
+def test_keyword_generators(pk):
+    """synth_C is exactly symmetric in X's block structure; synth_start is strictly positive
+    definite (diagonally dominant) and deterministic."""
+    cons, b = pk.synth(J=2, delta=3, rank=1, n_y=3, m=2, L=2, seed=4)
+    bi = pk.get_block_info(cons)
+    C = pk.synth_C(bi, 21)
+    assert [[c.shape[0] for c in row] for row in C] == bi.Y_blocksizes
+    assert all(np.array_equal(c, c.T) and np.any(c != 0) for row in C for c in row)
+    x, X, y, Y = pk.synth_start(bi, 5)
+    x2, X2, y2, Y2 = pk.synth_start(bi, 5)
+    assert np.array_equal(x, x2) and np.array_equal(Y[1][0], Y2[1][0])
+    assert len(x) == sum(bi.dim_S) and len(y) == bi.n_y
+    for M in [m for row in X + Y for m in row]:
+        assert np.array_equal(M, M.T) and np.linalg.eigvalsh(M).min() > 0.5
+
+
+def test_round4_goldens_are_consistent():
+    """The keyword goldens carry their keywords and stop as their thresholds say; the gap-1e-24
+    golden terminates with the final gap below 1e-24 and the previous one above it (so the
+    double-double loops have an unambiguous iteration to stop at)."""
+    import json
+    import mpmath
+    gd = os.path.join(ROOT, "tests", "golden")
+    with mpmath.workprec(256):
+        g = json.load(open(os.path.join(gd, "rank2_mp256_seed5_gap24.json")))
+        assert g["status"] == "terminated"
+        thr = mpmath.mpf(g["params"]["duality_gap_threshold"])
+        assert mpmath.mpf(g["final"]["gap"]) < thr < mpmath.mpf(g["log"][-1]["gap"])
+        assert all(mpmath.mpf(r["gap"]) > thr for r in g["log"][1:])
+        for name, kw in (("kw_C_b0_mp256", "C_seed"), ("kw_needp_mp256", "need_primal_feasible"),
+                         ("kw_needd_mp256", "need_dual_feasible"), ("kw_start_mp256", "start_seed")):
+            k = json.load(open(os.path.join(gd, name + ".json")))
+            assert kw in k["keywords"]
+        p = json.load(open(os.path.join(gd, "kw_needp_mp256.json")))
+        assert p["status"] == "terminated" and len(p["log"]) < p["iterations"]
+        last = p["log"][-1]
+        assert max(mpmath.mpf(last["P_err"]), mpmath.mpf(last["p_err"])) < \
+            mpmath.mpf(p["params"]["primal_error_threshold"])

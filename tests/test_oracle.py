@@ -223,3 +223,26 @@ def test_stage_fixtures_agree_with_fp64_oracle(pk, oracle, name, bits):
     sc = residual_scales(cons, b, state[1])
     e = {k: compare_summary(ref[k], rec, sc.get(k, 0.0)) for k, rec in fx["buffers"].items()}
     assert max(e.values()) < 1e-9, e
+
+
+@pytest.mark.parametrize("name", ["kw_C_b0_mp256", "kw_needp_mp256", "kw_needd_mp256",
+                                  "kw_start_mp256"])
+def test_keyword_goldens_fp64_oracle(pk, oracle, name):
+    """The fp64 oracle with the golden's keywords (C, b0, need_*_feasible, initial_solutions;
+    MPMP.jl:599-613) reproduces the 256-bit keyword goldens' logs to fp64 round-off and stops
+    at the same iteration with the same status."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    M = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(M)
+    g = json.load(open(os.path.join(GOLDEN, name + ".json")))
+    cons, b = pk.synth(**g["instance"])
+    bi = oracle.get_block_info(cons)
+    ar = oracle.Fp64()
+    kw = M.keyword_args(pk, ar, bi, g["keywords"])
+    res = oracle.solverank1sdp(cons, b, bi, ar=ar, maxiterations=g["iterations"] + 1,
+                               **g["params"], **kw)
+    assert res.status == g["status"] and len(res.log) == len(g["log"])
+    for row, ref in zip(res.log, g["log"]):
+        for key in ("mu", "alpha_p", "alpha_d", "beta", "p_obj", "d_obj", "gap"):
+            assert abs(float(getattr(row, key)) - float(ref[key])) <= 1e-9 * max(1.0, abs(float(ref[key]))), key

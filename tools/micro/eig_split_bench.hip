@@ -117,8 +117,23 @@ int run(int n, int nb, double scale, int kind, bool check_host) {
   return bad;
 }
 
-int main() {
+int main(int argc, char** argv) {
   int bad = 0;
+#ifdef CLRSDP_EIGSPLIT_STAMPS
+  {
+    const int nb = argc > 1 ? atoi(argv[1]) : 128;
+    run(128, nb, 1.0, 0, false);
+    unsigned long long st[8];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_eigsplit_stamps), sizeof(st)));
+    const char* names[] = {"chain: wait b1", "chain: reflector", "chain: wait b2", "bulk: matvec",
+                           "bulk: wait b1", "bulk: update", "bulk: wait b2", "multisection"};
+    // run() launches each kernel 1 + 5 times
+    for (int q = 0; q < 8; ++q)
+      printf("  %-18s %9.0f cycles per matrix (%6.1f per column)\n", names[q], st[q] / (6.0 * nb),
+             st[q] / (6.0 * nb * 126));
+    return 0;
+  }
+#endif
   bad += run(128, 128, 1.0, 0, true);
   bad += run(128, 16, 1.0, 0, false);
   bad += run(128, 256, 1.0, 0, false);
