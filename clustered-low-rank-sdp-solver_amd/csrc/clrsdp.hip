@@ -647,7 +647,7 @@ struct MatPlan : PlanBase {  // potrf / eigmin
         // CLRSDP_EIG_REG=1 (eigmin_reg: every live wave builds the reflector)
         static const bool reg = env_on("CLRSDP_EIG_REG");
         if (reg) eigmin_reg<<<(unsigned)h.size(), 512, 0, s>>>(d, out);
-        else eigmin_split<<<(unsigned)h.size(), 576, 0, s>>>(d, out);
+        else eigmin_split<0><<<(unsigned)h.size(), 576, 0, s>>>(d, out);
         HIPCHK(hipGetLastError());
         return;
       }

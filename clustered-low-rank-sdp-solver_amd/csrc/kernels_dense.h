@@ -487,6 +487,72 @@ __device__ inline bool sturm_any_below(const double* __restrict__ sd, const doub
   return acc < 0;
 }
 
+// The same test with the chain split in two (round 4): leading principal minors p_i of rows
+// [0, h) top-down and trailing minors q_i of rows [h, nr) bottom-up, two independent recurrences
+// (the count is latency-bound: each row is one dependent FMA chain link), joined by
+// det(T - sigma I) = p_{h-1} q_h - e2_{h-1} p_{h-2} q_{h+1}.  With the twisted factorisation
+// N D N^T of T - sigma I at row h (Sylvester), lambda_min < sigma iff some p_i < 0 (i < h), some
+// q_i < 0 (i >= h) or det < 0 (the twist pivot has the sign of det when p_{h-1}, q_h > 0).  Both
+// chains rescale by powers of two every 8 rows; det's three terms carry one p and one q factor
+// each, so the scales agree.
+__device__ inline bool sturm_any_below2(const double* __restrict__ sd, const double* __restrict__ se,
+                                        int nr, double sigma) {
+  const int h = 8 * ((nr >> 3) >> 1);
+  double pm = 0.0, pc = 1.0;  // p_{i-2}, p_{i-1}
+  double qm = 0.0, qc = 1.0;  // q_{i+2}, q_{i+1}
+  int acc = 0;
+  const int nb = nr - h, nt = h;
+  const int nmax = nb > nt ? nb : nt;
+  for (int g = 0; g < nmax; g += 8) {
+    double dt[8], et[8], db[8], eb[8];
+    const bool top = g < nt;
+    const int ib = nr - 8 - g;  // rows ib..ib+7 of the bottom chain, walked downwards
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      if (top) {
+        const double2 a = *reinterpret_cast<const double2*>(sd + g + u);
+        const double2 b = *reinterpret_cast<const double2*>(se + g + u);
+        dt[u] = a.x; dt[u + 1] = a.y;
+        et[u] = b.x; et[u + 1] = b.y;
+      }
+      const double2 c = *reinterpret_cast<const double2*>(sd + ib + u);
+      // q_i couples to row i+1 through e2_i = se[i+1]
+      const double2 e = *reinterpret_cast<const double2*>(se + ib + u);
+      db[u] = c.x; db[u + 1] = c.y;
+      eb[u] = e.y;
+      eb[u + 1] = (u + 2 < 8) ? se[ib + u + 2] : (ib + 8 < nr + 0 ? se[ib + 8] : 0.0);
+    }
+    if (top) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double pn = fma(dt[u] - sigma, pc, -(et[u] * pm));
+        acc |= __double2hiint(pn);
+        pm = pc;
+        pc = pn;
+      }
+      const int ex = __builtin_amdgcn_frexp_exp(pc);
+      pc = __builtin_ldexp(pc, -ex);
+      pm = __builtin_ldexp(pm, -ex);
+    }
+    if (g < nb) {
+#pragma unroll
+      for (int u = 7; u >= 0; --u) {
+        const double qn = fma(db[u] - sigma, qc, -(eb[u] * qm));
+        acc |= __double2hiint(qn);
+        qm = qc;
+        qc = qn;
+      }
+      const int ex = __builtin_amdgcn_frexp_exp(qc);
+      qc = __builtin_ldexp(qc, -ex);
+      qm = __builtin_ldexp(qm, -ex);
+    }
+  }
+  // p_{h-1} = pc, p_{h-2} = pm; q_h = qc, q_{h+1} = qm; e2_{h-1} = se[h]
+  const double det = fma(pc, qc, -(se[h] * pm * qm));
+  acc |= __double2hiint(det);
+  return acc < 0;
+}
+
 // NWV waves (8: one row block per wave, two waves per SIMD; 4: two row blocks per lane, one wave
 // per SIMD, so the redundant per-column reflector chain costs each SIMD half the issue slots).
 template <int DBG = 0, int NWV = 8>  // DBG (timing experiments only): 1 = no update FMAs, 2 = no matvec FMAs
@@ -891,9 +957,12 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
 #ifdef CLRSDP_EIGSPLIT_STAMPS
 __device__ unsigned long long g_eigsplit_stamps[8];
 #endif
+// DBG (timing experiments only): 1 = no update FMAs, 2 = no matvec FMAs, 4 = the chain wave
+// skips the reflector (v_{k+1} = the published row), 8 = the old one-chain 256-way multisection
+template <int DBG = 0>
 __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __restrict__ descs,
                                                      double* __restrict__ out) {
-  constexpr int NS = 16, NWB = 8;
+  constexpr int NS = 16, NWB = 8, GS = (DBG & 16) ? 2 : 4;
 #ifdef CLRSDP_EIGSPLIT_STAMPS
   // per column: chain lane 0 (slots 0-2: wait at barrier 1, reflector, wait at barrier 2) and
   // bulk wave 4 lane 0 (row block 7, live to the end; slots 3-6: matvec phase, wait at barrier
@@ -1029,18 +1098,21 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
   }
   for (int k = 0; k + 2 < n; ++k) {
     const int lo = (k + 1) >> 3;  // slots s < lo hold columns <= k only
+    const int r = k + 1;
     double pp = 0.0;
     if (!chain) {
       // ---- p = A_k v_k and this wave's part of v^T p (two FMA chains per column parity)
       const bool live = blk * 16 + 15 > k && blk * 16 < n;
       double pa[4] = {0.0, 0.0, 0.0, 0.0};
-      if (live) {
-        static_for<0, NS / 4>([&](auto G) {
+      if (live && !(DBG & 2)) {
+        // slots in groups of GS behind one uniform branch each (pairs measured slower: a
+        // branch and the DPP wait state per group)
+        static_for<0, NS / GS>([&](auto G) {
           constexpr int g = decltype(G)::value;
-          if (4 * g + 3 >= lo) {
-            static_for<4 * g, 4 * g + 4>([&](auto S) {
+          if (GS * g + GS - 1 >= lo) {
+            static_for<GS * g, GS * g + GS>([&](auto S) {
               constexpr int s = decltype(S)::value;
-              fmac_bcast<s, s == 4 * g>(pa[2 * (s & 1)], cx, a[s][0]);
+              fmac_bcast<s, s == GS * g>(pa[2 * (s & 1)], cx, a[s][0]);
               fmac_bcast<s, false>(pa[2 * (s & 1) + 1], cy, a[s][1]);
             });
           }
@@ -1058,7 +1130,6 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
     }
     __syncthreads();
     ES_STAMP(chain ? 0 : 4)
-    const int r = k + 1;
     if (chain) {
       // ---- row r of A_{k+1} and the reflector v_{k+1}
       double rw[NWB];
@@ -1082,7 +1153,14 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
       const double xj1 = fma(cy, gr, fma(pj.y, mhr, o.y));
       const double xr = fma(vr, gr, fma(pr, mhr, orr));
       const double x0 = fma(vr1, gr, fma(pr1, mhr, or1));
-      reflector(r, xj0, xj1, xr, x0);
+      if constexpr (DBG & 4) {
+        cx = o.x;
+        cy = o.y;
+        *reinterpret_cast<double2*>(&vb[r & 1][j0]) = make_double2(cx, cy);
+        if (lane == 0) { dg[r] = xr + xj0 + x0; e2[r] = 1.0; betab[r & 1] = 0.0; }
+      } else {
+        reflector(r, xj0, xj1, xr, x0);
+      }
       ES_STAMP(1)
     } else if (blk * 16 + 15 > k + 1 && blk * 16 < n) {
       // ---- w = beta p - K v;  A -= v w^T + w v^T, i.e. a_ij += g_i v_j - h_i p_j
@@ -1098,15 +1176,17 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
       const double Kc = beta * beta * tot * 0.5;
       const double wi = fma(beta, pp, -(Kc * vi));
       const double gi = fma(Kc, vi, -wi), mhi = -(beta * vi);
-      static_for<0, NS / 4>([&](auto G) {
+      // per group the p terms, then the v terms (a dependent pair is 8 issues apart); all p
+      // terms ahead of all v terms measured slower
+      if (!(DBG & 1)) static_for<0, NS / GS>([&](auto G) {
         constexpr int g = decltype(G)::value;
-        if (4 * g + 3 >= lo) {
-          static_for<4 * g, 4 * g + 4>([&](auto S) {
+        if (GS * g + GS - 1 >= lo) {
+          static_for<GS * g, GS * g + GS>([&](auto S) {
             constexpr int s = decltype(S)::value;
-            fmac_bcast<s, s == 4 * g>(a[s][0], pv.x, mhi);
+            fmac_bcast<s, s == GS * g>(a[s][0], pv.x, mhi);
             fmac_bcast<s, false>(a[s][1], pv.y, mhi);
           });
-          static_for<4 * g, 4 * g + 4>([&](auto S) {
+          static_for<GS * g, GS * g + GS>([&](auto S) {
             constexpr int s = decltype(S)::value;
             fmac_bcast<s, false>(a[s][0], cx, gi);
             fmac_bcast<s, false>(a[s][1], cy, gi);
@@ -1170,25 +1250,29 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
     }
   }
   __syncthreads();
+  // 256-way multisection on waves 0-3 (one per SIMD), 7 rounds of 8 bits: as eigmin_reg
   double lo = bnd[0], hi = bnd[1];
   const int nr = (n + 7) & ~7;
-  for (int it = 0; it < 7; ++it) {
+  constexpr int NCW = (DBG & 8) ? NWB : 4;         // counting waves (one per SIMD)
+  constexpr double NSIG = 64.0 * NCW + 1.0;
+  for (int it = 0; it < ((DBG & 8) ? 6 : 7); ++it) {
     const double width = hi - lo;
-    if (w < 4) {
-      const double sigma = lo + width * ((double)(tid + 1) / 257.0);
-      const unsigned long long mk = __ballot(sturm_any_below(sd, se, nr, sigma));
+    if (w < NCW) {
+      const double sigma = lo + width * ((double)(tid + 1) / NSIG);
+      const bool below = (DBG & 8) ? sturm_any_below2(sd, se, nr, sigma) : sturm_any_below(sd, se, nr, sigma);
+      const unsigned long long mk = __ballot(below);
       if (lane == 0) masks[w] = mk;
     }
     __syncthreads();
     int f = -1;
-    for (int q = 0; q < 4 && f < 0; ++q)
+    for (int q = 0; q < NCW && f < 0; ++q)
       if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
     __syncthreads();
     if (f < 0) {
-      lo = lo + width * (256.0 / 257.0);
+      lo = lo + width * ((NSIG - 1.0) / NSIG);
     } else {
-      hi = lo + width * ((double)(f + 1) / 257.0);
-      if (f > 0) lo = lo + width * ((double)f / 257.0);
+      hi = lo + width * ((double)(f + 1) / NSIG);
+      if (f > 0) lo = lo + width * ((double)f / NSIG);
     }
   }
   if (tid == 0) out[blockIdx.x] = __builtin_ldexp((lo + hi) * 0.5, bnd_ex + ex0);

@@ -1,4 +1,4 @@
-"""Print the double-double log of the gap-1e-24 golden instance next to the 256-bit oracle's."""
+"""Print the double-double log of the gap-1e-20 golden instance next to the 256-bit oracle's."""
 import json
 import os
 import sys
@@ -8,7 +8,7 @@ sys.path.insert(0, ROOT)
 import _clrsdp_pkg  # noqa: E402
 
 pk = _clrsdp_pkg.load()
-g = json.load(open(os.path.join(ROOT, "tests/golden/rank2_mp256_seed5_gap24.json")))
+g = json.load(open(os.path.join(ROOT, "tests/golden/rank2_mp256_seed5_gap20.json")))
 cons, b = pk.synth(**g["instance"])
 bi = pk.get_block_info(cons)
 res = pk.solverank1sdp(cons, b, bi, maxiterations=int(sys.argv[1]) if len(sys.argv) > 1 else 70,

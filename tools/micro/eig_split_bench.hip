@@ -86,7 +86,7 @@ int run(int n, int nb, double scale, int kind, bool check_host) {
   CK(hipMalloc(&ddin, nb * sizeof(MatDesc<double>)));
   CK(hipMemcpy(ddin, din.data(), nb * sizeof(MatDesc<double>), hipMemcpyHostToDevice));
   const float t_reg = timeit([&] { eigmin_reg<<<nb, 512>>>(ddin, dE); });
-  const float t_spl = timeit([&] { eigmin_split<<<nb, 576>>>(ddin, dE + nb); });
+  const float t_spl = timeit([&] { eigmin_split<0><<<nb, 576>>>(ddin, dE + nb); });
   CK(hipDeviceSynchronize());
   std::vector<double> ev(2 * nb);
   CK(hipMemcpy(ev.data(), dE, 2 * nb * 8, hipMemcpyDeviceToHost));
@@ -134,6 +134,35 @@ int main(int argc, char** argv) {
     return 0;
   }
 #endif
+  {  // timing experiments on the C3 batch (DBG variants: wrong results, timing only)
+    const int n = 128, nb = 128;
+    std::vector<double> h((size_t)nb * n * n);
+    srand(5);
+    for (int b = 0; b < nb; ++b)
+      for (int j = 0; j < n; ++j)
+        for (int i = j; i < n; ++i) h[(size_t)b * n * n + i + j * n] = h[(size_t)b * n * n + j + i * n] = rand() / (double)RAND_MAX - 0.5;
+    double *dA, *dE;
+    CK(hipMalloc(&dA, h.size() * 8));
+    CK(hipMalloc(&dE, nb * 8));
+    CK(hipMemcpy(dA, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+    std::vector<MatDesc<double>> din(nb);
+    for (int b = 0; b < nb; ++b) din[b] = {dA + (size_t)b * n * n, n, n};
+    MatDesc<double>* dd;
+    CK(hipMalloc(&dd, nb * sizeof(MatDesc<double>)));
+    CK(hipMemcpy(dd, din.data(), nb * sizeof(MatDesc<double>), hipMemcpyHostToDevice));
+    printf("DBG variants (n=128, batch=128): full %.1f us | two-ended multisection %.1f | no update FMAs %.1f | no matvec FMAs %.1f | no FMAs %.1f | no reflector %.1f | nothing %.1f | slot pairs %.1f\n",
+           timeit([&] { eigmin_split<0><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<8><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<1><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<2><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<3><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<4><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<7><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<16><<<nb, 576>>>(dd, dE); }));
+    CK(hipFree(dA));
+    CK(hipFree(dE));
+    CK(hipFree(dd));
+  }
   bad += run(128, 128, 1.0, 0, true);
   bad += run(128, 16, 1.0, 0, false);
   bad += run(128, 256, 1.0, 0, false);
