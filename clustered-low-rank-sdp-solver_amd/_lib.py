@@ -38,7 +38,7 @@ EXPORTS = ["clrsdp_version", "clrsdp_last_error", "clrsdp_create", "clrsdp_uploa
            "clrsdp_destroy", "clrsdp_set_control", "clrsdp_iterate_async", "clrsdp_iterate_wait",
            "clrsdp_comm_unique_id", "clrsdp_comm_init", "clrsdp_save_state",
            "clrsdp_restore_state", "clrsdp_step_length", "clrsdp_set_factorization",
-           "clrsdp_get_factorization", "clrsdp_set_graph", "clrsdp_comm_info"]
+           "clrsdp_get_factorization", "clrsdp_set_graph", "clrsdp_comm_info", "clrsdp_eigmin"]
 # clrsdp_set_factorization flags (include/clrsdp.h)
 FACT_FALLBACK, FACT_LU_SQ, FACT_LU_X = 1, 2, 4
 COMM_ID_BYTES = 128
@@ -125,6 +125,7 @@ def lib():
     L.clrsdp_get_factorization.argtypes = [C.c_void_p, P_i32]
     L.clrsdp_set_graph.argtypes = [C.c_void_p, C.c_int32]
     L.clrsdp_comm_info.argtypes = [C.c_void_p, P_i32, P_i32]
+    L.clrsdp_eigmin.argtypes = [C.c_int32, C.c_int32, C.c_int64, P_i64, P_f64, P_f64]
     L.clrsdp_step_length.argtypes = [C.c_int32, C.c_int64, P_i64, P_f64, P_f64, C.c_double, P_f64,
                                      P_f64]
     for name in EXPORTS:

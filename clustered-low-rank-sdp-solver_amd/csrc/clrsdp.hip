@@ -1826,7 +1826,7 @@ struct Solver final : HandleBase {
 
   // one-workgroup fixed-tree reduction of n <= 256 partials
   void vec_reduce_tree(const T* in, int n, int op, T* dst) {
-    vec_reduce<T><<<1, 1024, 0, stream>>>(in, in, n, op == 2 ? 2 : 3, dst);
+    vec_reduce<T><<<1, vec_reduce_threads<T>(), 0, stream>>>(in, in, n, op == 2 ? 2 : 3, dst);
   }
 
   // trace_A with the products U already in TX -> val (tval) -> aggregate
@@ -2072,7 +2072,7 @@ struct Solver final : HandleBase {
     // p partial = sum_j B_j^T x_j (slabs) ; local maxima of |P| and |d| into tmpsc[0..1]
     p_Btx.launch(stream, 1.0, 0.0);
     local_blk_reduce(P, nullptr, nullptr, nullptr, 2, tmpsc);
-    if (nx > 0) vec_reduce<T><<<1, 1024, 0, stream>>>(dvec, nullptr, nx, 2, tmpsc + 1);
+    if (nx > 0) vec_reduce<T><<<1, vec_reduce_threads<T>(), 0, stream>>>(dvec, nullptr, nx, 2, tmpsc + 1);
     else fill(tmpsc + 1, 0.0, 1);
   }
   void residuals_finish() {
@@ -2267,11 +2267,11 @@ struct Solver final : HandleBase {
   void objectives(const clrsdp_params* prm, int pd_feas, int which = 3) {
     zero_cy = !hasC;
     if (world == 1) {
-      if (nx > 0) vec_reduce<T><<<1, 1024, 0, stream>>>(cvec, x, nx, 0, sc + SC_DOT_CX);
+      if (nx > 0) vec_reduce<T><<<1, vec_reduce_threads<T>(), 0, stream>>>(cvec, x, nx, 0, sc + SC_DOT_CX);
       else fill(sc + SC_DOT_CX, 0.0, 1);
       if (hasC) local_blk_reduce(Cm, Y, nullptr, nullptr, 0, sc + SC_DOT_CY);
     } else {
-      if (nx > 0) vec_reduce<T><<<1, 1024, 0, stream>>>(cvec, x, nx, 0, xsend);
+      if (nx > 0) vec_reduce<T><<<1, vec_reduce_threads<T>(), 0, stream>>>(cvec, x, nx, 0, xsend);
       else fill(xsend, 0.0, 1);
       if (hasC) local_blk_reduce(Cm, Y, nullptr, nullptr, 0, xsend + 1);
       else fill(xsend + 1, 0.0, 1);
@@ -2279,7 +2279,7 @@ struct Solver final : HandleBase {
       reduce_ranks(2, 0, 0, SC_DOT_CX);
       reduce_ranks(2, 1, 0, SC_DOT_CY);
     }
-    vec_reduce<T><<<1, 1024, 0, stream>>>(bvec, y, n_y, 0, sc + SC_DOT_BY);
+    vec_reduce<T><<<1, vec_reduce_threads<T>(), 0, stream>>>(bvec, y, n_y, 0, sc + SC_DOT_BY);
     scalars(prm, pd_feas, which);
     zero_cy = false;
   }
@@ -2781,6 +2781,41 @@ struct DevBuf {
   }
 };
 
+// lambda_min of each symmetric block at the word type T (the eigenvalue part of
+// compute_step_length, MPMP.jl:1857-1870): planes in, planes out
+template <class T>
+void eigmin_words(int device, int64_t nblk, const int64_t* n, const double* Ap, double* ep) {
+  constexpr int W = Num<T>::W;
+  DeviceGuard dg(device);
+  std::vector<int64_t> off(nblk + 1, 0);
+  for (int64_t b = 0; b < nblk; ++b) {
+    if (n[b] <= 0 || n[b] > 4096) throw ClrsdpError{CLRSDP_E_ARG, "block size out of range"};
+    off[b + 1] = off[b] + n[b] * n[b];
+  }
+  const int64_t tot = off[nblk];
+  // planes -> interleaved limbs (the layout of T)
+  std::vector<double> h((size_t)tot * W);
+  for (int64_t e = 0; e < tot; ++e)
+    for (int q = 0; q < W; ++q) h[(size_t)e * W + q] = Ap[(size_t)q * tot + e];
+  DevBuf mem;
+  T* A = mem.alloc<T>(tot);
+  T* eig = mem.alloc<T>(nblk);
+  HIPCHK(hipMemcpy(A, h.data(), (size_t)tot * sizeof(T), hipMemcpyHostToDevice));
+  MatPlan<T> eg;
+  for (int64_t b = 0; b < nblk; ++b) eg.add(A + off[b], (int)n[b], (int)n[b]);
+  eg.finalize();
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  struct StreamGuard { hipStream_t s; ~StreamGuard() { (void)hipStreamDestroy(s); } } sg{s};
+  eg.eigmin(s, eig);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<double> he((size_t)nblk * W);
+  HIPCHK(hipMemcpy(he.data(), eig, (size_t)nblk * sizeof(T), hipMemcpyDeviceToHost));
+  for (int64_t b = 0; b < nblk; ++b)
+    for (int q = 0; q < W; ++q) ep[(size_t)q * nblk + b] = he[(size_t)b * W + q];
+}
+
 int step_length_f64(int device, int64_t nblk, const int64_t* n, const double* Mh, const double* dMh,
                     double gamma, double* alpha, double* min_eig, std::string& err) {
   DeviceGuard dg(device);
@@ -3039,6 +3074,24 @@ int32_t clrsdp_step_length(int32_t device, int64_t nblocks, const int64_t* n, co
     const int rc = step_length_f64(device, nblocks, n, M, dM, gamma, alpha, min_eig, err);
     if (rc) g_last_error = err;
     return rc;
+  } catch (const ClrsdpError& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return CLRSDP_E_HIP;
+  }
+}
+
+int32_t clrsdp_eigmin(int32_t device, int32_t words, int64_t nblocks, const int64_t* n,
+                      const double* A, double* min_eig) {
+  if (nblocks <= 0 || !n || !A || !min_eig) { g_last_error = "null argument or no blocks"; return CLRSDP_E_ARG; }
+  try {
+    if (words == 1) eigmin_words<double>(device, nblocks, n, A, min_eig);
+    else if (words == 2) eigmin_words<mw::dd>(device, nblocks, n, A, min_eig);
+    else if (words == 4) eigmin_words<mw::qd>(device, nblocks, n, A, min_eig);
+    else { g_last_error = "words must be 1, 2 or 4"; return CLRSDP_E_ARG; }
+    return CLRSDP_OK;
   } catch (const ClrsdpError& e) {
     g_last_error = e.msg;
     return e.code;

@@ -19,6 +19,7 @@
 namespace clrsdp {
 
 using mw::Num;
+using mw::sel;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -989,7 +990,10 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
       const int i = e % nb, j = e / nb;
       D[i + j * NB] = lat(i0 + i, i0 + j);
     }
-    if (tid < nb) rdg[tid] = UNIT ? T(1.0) : recip_fast(lat(i0 + tid, i0 + tid));
+    if (tid < nb) {
+      if (UNIT) rdg[tid] = T(1.0);
+      else rdg[tid] = recip_fast(lat(i0 + tid, i0 + tid));
+    }
     if constexpr (PS) {
       __syncthreads();
       for (int e = tid; e < nb * nb; e += blockDim.x) {
@@ -1014,7 +1018,8 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
     for (int cb = 0; cb < nc; cb += NT / 16) {  // uniform: NT/16 right-hand sides per pass
       const int r = tid & 15, c = cb + (tid >> 4), base = tid & 48;
       const bool act = r < nb && c < nc;
-      T v = act ? B[(i0 + r) + (size_t)c * d.ldb] : T(0.0);
+      T v = T(0.0);
+      if (act) v = B[(i0 + r) + (size_t)c * d.ldb];
       T xr = T(0.0);
       if constexpr (PS) {
         // v_q is final once the steps before q have run: broadcast it, scale it off the chain
@@ -1110,7 +1115,8 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave(const TrsmDesc<T>* __restri
   const int c = (blockIdx.x - d.tile0) * NW + (tid >> 6);
   if (c >= d.nrhs) return;  // (whole waves; no barrier follows)
   T* B = d.B + (size_t)c * d.ldb;
-  T v = lane < n ? B[lane] : T(0.0);
+  T v = T(0.0);
+  if (lane < n) v = B[lane];
   if (!TRANS) {
     for (int q = 0; q + 1 < n; ++q) {
       const T vq = readlane_t(v, q);
@@ -1144,8 +1150,9 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave128(const TrsmDesc<T>* __res
   const int c = (blockIdx.x - d.tile0) * NW + (tid >> 6);
   const bool act = c < d.nrhs;  // (wave-uniform; every wave stays for the barriers)
   T* B = d.B + (size_t)(act ? c : 0) * d.ldb;
-  T v0 = act && lane < n ? B[lane] : T(0.0);
-  T v1 = act && lane + 64 < n ? B[lane + 64] : T(0.0);
+  T v0 = T(0.0), v1 = T(0.0);
+  if (act && lane < n) v0 = B[lane];
+  if (act && lane + 64 < n) v1 = B[lane + 64];
   const int nch = (n + CH - 1) / CH;
   for (int ci = 0; ci < nch; ++ci) {
     const int q0 = (TRANS ? nch - 1 - ci : ci) * CH, qn = min(CH, n - q0);
@@ -1162,7 +1169,7 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave128(const TrsmDesc<T>* __res
     if (act) {
       for (int u = 0; u < qn; ++u) {
         const int qq = TRANS ? qn - 1 - u : u, q = q0 + qq;
-        const T vq = readlane_t(q < 64 ? v0 : v1, q & 63);
+        const T vq = readlane_t(sel(q < 64, v0, v1), q & 63);
         if (TRANS ? lane < q : (lane > q && lane < n)) v0 = v0 - Ls[lane + 128 * qq] * vq;
         if (TRANS ? lane + 64 < q : (lane + 64 > q && lane + 64 < n)) v1 = v1 - Ls[lane + 64 + 128 * qq] * vq;
       }
@@ -1337,7 +1344,8 @@ __global__ __launch_bounds__(256) void perm_rows(const PermDesc<T>* __restrict__
   for (long long e = blockIdx.x * 256LL + threadIdx.x; e < tot; e += 256LL * gridDim.x) {
     const int i = (int)(e % d.n), c = (int)(e / d.n);
     const int pi = d.perm[i];
-    d.out[i + (size_t)c * d.ldo] = ident ? (pi == c ? T(1.0) : T(0.0)) : d.in[pi + (size_t)c * d.ldi];
+    if (ident) d.out[i + (size_t)c * d.ldo] = T(pi == c ? 1.0 : 0.0);
+    else d.out[i + (size_t)c * d.ldo] = d.in[pi + (size_t)c * d.ldi];
   }
 }
 
@@ -1393,7 +1401,7 @@ __global__ __launch_bounds__(256) void eigmin_batched(const MatDesc<T>* __restri
     s = block_sum(s, red);
     const T x0 = v[0];
     const T nrm = Num<T>::sqrt_(s);
-    const T alpha = (x0 > T(0.0)) ? -nrm : nrm;
+    const T alpha = sel(x0 > T(0.0), -nrm, nrm);
     if (tid == 0) dg[k] = A[k + (size_t)k * lda];
     T tail = s - x0 * x0;
     if (!(tail > T(0.0))) {  // already tridiagonal in this column
@@ -2022,7 +2030,8 @@ __global__ void blk_axpby(const BlkDesc* __restrict__ bd, T* out, const T* X, co
                           double b, const T* sc, double sc_mult) {
   const BlkDesc B = bd[blockIdx.x];
   const int nn = B.n * B.n;
-  const T s = sc ? (*sc) * T(sc_mult) : T(0.0);
+  T s = T(0.0);
+  if (sc) s = (*sc) * T(sc_mult);
   for (int e = threadIdx.x; e < nn; e += blockDim.x) {
     T v = T(0.0);
     if (a != 0.0) v += X[B.off + e] * T(a);
@@ -2095,7 +2104,7 @@ __global__ void blk_identity(const BlkDesc* __restrict__ bd, T* out) {
   const BlkDesc B = bd[blockIdx.x];
   const int nn = B.n * B.n;
   for (int e = threadIdx.x; e < nn; e += blockDim.x)
-    out[B.off + e] = ((e % B.n) == (e / B.n)) ? T(1.0) : T(0.0);
+    out[B.off + e] = T(((e % B.n) == (e / B.n)) ? 1.0 : 0.0);
 }
 
 // out = (Z + Z^T)/2   (mode 0);  out = upper triangle mirrored (mode 1, Symmetric(.)) ;
@@ -2150,46 +2159,77 @@ __global__ __launch_bounds__(256) void blk_reduce(const BlkDesc* __restrict__ bd
   if (threadIdx.x == 0) partial[blockIdx.x] = r;
 }
 
-// vector reductions over [0, n): op 0 = sum a.*b, op 2 = max |a|; single workgroup
+// vector reductions over [0, n): op 0 = sum a.*b, op 2 = max |a|; single workgroup of
+// vec_reduce_threads<T>() threads.  Thread t owns elements t + NT (U u + q), combined q = 0..U-1
+// in order.  fp64: 1024 threads, U = 4.  Multi-word: 256 threads and U = 2 (dd) / 1 (qd), so a
+// lane has the registers of its multi-word products (at 1024 threads, 128 VGPRs per lane, the
+// accumulators and loads spilled to scratch: 160 B/lane at dd, 304 at qd); the remainder walks
+// the accumulators with compile-time indices
 template <class T>
-__global__ __launch_bounds__(1024) void vec_reduce(const T* a, const T* b, long long n, int op,
-                                                   T* __restrict__ out) {
-  __shared__ T red[1024];
-  // fixed assignment: thread t owns elements t + 1024 (4u + q), combined q = 0..3 in order
-  T acc[4] = {T(0.0), T(0.0), T(0.0), T(0.0)};
+__host__ __device__ constexpr int vec_reduce_threads() { return sizeof(T) == 8 ? 1024 : 256; }
+template <class T>
+__global__ __launch_bounds__(vec_reduce_threads<T>()) void vec_reduce(const T* a, const T* b, long long n, int op,
+                                                                      T* __restrict__ out) {
+  constexpr int U = sizeof(T) == 8 ? 4 : (sizeof(T) == 16 ? 2 : 1);
+  constexpr int NT = vec_reduce_threads<T>();
+  __shared__ T red[NT];
+  // (if/else throughout: a ternary on the struct types is lowered to a select of addresses,
+  // which keeps the operands in scratch; the accumulators are named variables, not an array)
+  auto elem = [&](long long f) {
+    T v;
+    if (op == 0) v = a[f] * b[f];
+    else if (op == 3) v = a[f];
+    else v = Num<T>::abs_(a[f]);
+    return v;
+  };
+  auto comb = [&](T& acc, const T& v) {
+    if (op == 2) {
+      if (v > acc) acc = v;
+    } else {
+      acc += v;
+    }
+  };
+  T a0(0.0), a1(0.0), a2(0.0), a3(0.0);
   long long e = threadIdx.x;
-  for (; e + 3 * 1024 < n; e += 4 * 1024) {
-    T v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const long long f = e + (long long)q * 1024;
-      v[q] = op == 0 ? a[f] * b[f] : (op == 3 ? a[f] : Num<T>::abs_(a[f]));
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (op == 2) acc[q] = (v[q] > acc[q]) ? v[q] : acc[q];
-      else acc[q] += v[q];
+  for (; e + (U - 1) * NT < n; e += U * NT) {
+    if constexpr (U == 4) {
+      const T v0 = elem(e), v1 = elem(e + NT), v2 = elem(e + 2 * NT), v3 = elem(e + 3 * NT);
+      comb(a0, v0);
+      comb(a1, v1);
+      comb(a2, v2);
+      comb(a3, v3);
+    } else if constexpr (U == 2) {
+      const T v0 = elem(e), v1 = elem(e + NT);
+      comb(a0, v0);
+      comb(a1, v1);
+    } else {
+      comb(a0, elem(e));
     }
   }
-  for (int q = 0; e < n; e += 1024, ++q) {
-    const T v = op == 0 ? a[e] * b[e] : (op == 3 ? a[e] : Num<T>::abs_(a[e]));
-    if (op == 2) acc[q] = (v > acc[q]) ? v : acc[q];
-    else acc[q] += v;
-  }
-  T t;
-  if (op == 2) {
-    t = acc[0];
-#pragma unroll
-    for (int q = 1; q < 4; ++q) t = (acc[q] > t) ? acc[q] : t;
-  } else {
-    t = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  // remainder: at most U - 1 more elements, in accumulator order
+  if (U > 1 && e < n) { comb(a0, elem(e)); e += NT; }
+  if (U > 2 && e < n) { comb(a1, elem(e)); e += NT; }
+  if (U > 3 && e < n) { comb(a2, elem(e)); e += NT; }
+  T t = a0;
+  if constexpr (U == 4) {
+    if (op == 2) {
+      if (a1 > t) t = a1;
+      if (a2 > t) t = a2;
+      if (a3 > t) t = a3;
+    } else {
+      t = (a0 + a1) + (a2 + a3);   // the pairwise order of the round-3 kernel
+    }
+  } else if constexpr (U == 2) {
+    comb(t, a1);
   }
   red[threadIdx.x] = t;
   __syncthreads();
   for (int s2 = blockDim.x / 2; s2 > 0; s2 >>= 1) {
     if ((int)threadIdx.x < s2) {
       const T o = red[threadIdx.x + s2];
-      red[threadIdx.x] = (op == 2) ? ((o > red[threadIdx.x]) ? o : red[threadIdx.x]) : red[threadIdx.x] + o;
+      T m = red[threadIdx.x];
+      comb(m, o);
+      red[threadIdx.x] = m;
     }
     __syncthreads();
   }
@@ -2204,8 +2244,8 @@ __global__ void ordered_reduce(const T* in, int cnt, long long stride, int op, T
   for (int i = 1; i < cnt; ++i) {
     const T v = in[(size_t)i * stride];
     if (op == 0) acc += v;
-    else if (op == 2) acc = (v > acc) ? v : acc;
-    else acc = (v < acc) ? v : acc;  // op 3: min
+    else if (op == 2) { if (v > acc) acc = v; }
+    else { if (v < acc) acc = v; }  // op 3: min
   }
   *out = acc;
 }
@@ -2552,12 +2592,16 @@ __device__ inline bool pd_feasible(const T* sc, const ScalarParams<T>& p) {
 // 1067-1078, 1147-1185); excl_b0: the initial gap of MPMP.jl:725 (compute_duality_gap has no b0)
 template <class T>
 __device__ inline void control_update(T* sc, const ScalarParams<T>& p, bool excl_b0) {
-  const T po = excl_b0 ? sc[SC_POBJ] - p.b0 : sc[SC_POBJ];
-  const T dob = excl_b0 ? sc[SC_DOBJ] - p.b0 : sc[SC_DOBJ];
-  const T den0 = Num<T>::abs_(po + dob);
-  const T den = den0 > T(1.0) ? den0 : T(1.0);
+  T po = sc[SC_POBJ], dob = sc[SC_DOBJ];
+  if (excl_b0) {
+    po = po - p.b0;
+    dob = dob - p.b0;
+  }
+  T den = Num<T>::abs_(po + dob);
+  if (!(den > T(1.0))) den = T(1.0);
   const T gap = Num<T>::abs_(po - dob) / den;
-  const T perr = sc[SC_ERR_PMAT] > sc[SC_ERR_PVEC] ? sc[SC_ERR_PMAT] : sc[SC_ERR_PVEC];
+  T perr = sc[SC_ERR_PVEC];
+  if (sc[SC_ERR_PMAT] > perr) perr = sc[SC_ERR_PMAT];
   const T derr = sc[SC_ERR_DVEC];
   const bool pf = perr < p.p_thr, df = derr < p.d_thr, go = gap < p.gap_thr;
   // sticky once set (a skipped body must not un-terminate the loop); reset by excl_b0 (initial)
@@ -2580,17 +2624,21 @@ __device__ T fold_wave(const FoldRed<T>& r, int lane) {
     if (r.op == 4) v = Num<T>::abs_(v);
     if (!have) { acc = v; have = true; }
     else if (sum) acc += v;
-    else if (mn) acc = (v < acc) ? v : acc;
-    else acc = (v > acc) ? v : acc;
+    else if (mn) { if (v < acc) acc = v; }
+    else { if (v > acc) acc = v; }
   }
   // lanes without elements hold the first element (neutral for min/max) or 0 (sum)
-  if (!have) acc = sum ? T(0.0) : (r.op == 4 ? Num<T>::abs_(r.src[0]) : r.src[0]);
+  if (!have) {
+    if (sum) acc = T(0.0);
+    else if (r.op == 4) acc = Num<T>::abs_(r.src[0]);
+    else acc = r.src[0];
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const T v = shfl_xor_t(acc, o);
     if (sum) acc += v;
-    else if (mn) acc = (v < acc) ? v : acc;
-    else acc = (v > acc) ? v : acc;
+    else if (mn) { if (v < acc) acc = v; }
+    else { if (v > acc) acc = v; }
   }
   return acc;
 }
@@ -2599,9 +2647,14 @@ template <class T>
 __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
   const int lane = threadIdx.x;
   for (int e = lane; e < p.zero_n; e += 64) p.zero_ptr[e] = 0;
-  for (int q = 0; q < p.nred; ++q) {
-    const T v = fold_wave(p.red[q], lane);
-    if (lane == 0) sc[p.red[q].dst] = v;
+  // compile-time indices into the by-value parameter block (a runtime index makes the
+  // compiler copy the whole block to scratch: 104 B/lane at quad-double)
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    if (q < p.nred) {
+      const T v = fold_wave(p.red[q], lane);
+      if (lane == 0) sc[p.red[q].dst] = v;
+    }
   }
   // any status word set (which == 3): the wave reads them strided, one ballot
   bool fl = false;
@@ -2618,7 +2671,7 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
       p.stamps[1] = p.stamps[3] = p.stamps[5] = 0ull;
     }
     sc[SC_MU] = sc[SC_DOT_XY] / dim;
-    sc[SC_MU_P] = pdf ? T(0.0) : p.beta_inf * sc[SC_MU];
+    sc[SC_MU_P] = sel(pdf, T(0.0), p.beta_inf * sc[SC_MU]);
   } else if (which == 1) {  // r, beta, beta_c, mu_c
     const T r = sc[SC_DOT_XDY] / (sc[SC_MU] * dim);
     const T beta = (r < T(1.0)) ? r * r : r;
@@ -2636,8 +2689,9 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     sc[SC_DMU] = sc[SC_MU_C] - sc[SC_MU_P];
   } else if (which == 2) {  // step lengths
     const T g = p.gamma;
-    T ap = (sc[SC_MINEIG_X] > -g) ? T(1.0) : -g / sc[SC_MINEIG_X];
-    T ad = (sc[SC_MINEIG_Y] > -g) ? T(1.0) : -g / sc[SC_MINEIG_Y];
+    T ap = T(1.0), ad = T(1.0);
+    if (!(sc[SC_MINEIG_X] > -g)) ap = -g / sc[SC_MINEIG_X];
+    if (!(sc[SC_MINEIG_Y] > -g)) ad = -g / sc[SC_MINEIG_Y];
     if (pd_feasible(sc, p)) {
       const T mn = (ad < ap) ? ad : ap;
       ap = mn;

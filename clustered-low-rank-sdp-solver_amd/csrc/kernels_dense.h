@@ -71,8 +71,9 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
 #pragma unroll
     for (int c = 0; c < TC; ++c) {
       const int gi = r0 + i, gc = c0 + c;
-      a[i][c] = (gi < n && gc < n && gc <= gi) ? d.A[gi + (size_t)gc * d.lda] : T(0.0);
-      x[i][c] = (gi == gc) ? T(1.0) : T(0.0);
+      a[i][c] = T(0.0);
+      if (gi < n && gc < n && gc <= gi) a[i][c] = d.A[gi + (size_t)gc * d.lda];
+      x[i][c] = T(gi == gc ? 1.0 : 0.0);
     }
   if (t == 0) {
     fail = 0;
@@ -119,7 +120,10 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
     if (r0 + TR - 1 > j) {
       T ci[TR];
 #pragma unroll
-      for (int i = 0; i < TR; ++i) ci[i] = (r0 + i > j && r0 + i < n) ? col[r0 + i] : T(0.0);
+      for (int i = 0; i < TR; ++i) {
+        ci[i] = T(0.0);
+        if (r0 + i > j && r0 + i < n) ci[i] = col[r0 + i];
+      }
       if (c0 + TC - 1 > j && c0 <= r0 + TR - 1) {
 #pragma unroll
         for (int c = 0; c < TC; ++c) {
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(GR * GC) void chol_inv_reg(const MatDesc<T>* __rest
 #pragma unroll
       for (int c = 0; c < TC; ++c) {
         const int gi = r0 + i, gc = c0 + c;
-        if (gi < n && gc < n) ol.A[gi + (size_t)gc * ol.lda] = (gc <= gi) ? a[i][c] : T(0.0);
+        if (gi < n && gc < n) ol.A[gi + (size_t)gc * ol.lda] = sel(gc <= gi, a[i][c], T(0.0));
       }
   }
 }
@@ -238,7 +242,8 @@ __global__ __launch_bounds__(NT) void chol_packed(const MatDesc<T>* __restrict__
     }
     ar[k] = r;
     ac[k] = c;
-    a[k] = c >= 0 ? d.A[r + (size_t)c * d.lda] : T(0.0);
+    a[k] = T(0.0);
+    if (c >= 0) a[k] = d.A[r + (size_t)c * d.lda];
     ahi[k] = wave_max(c);
     alo[k] = -wave_max(c >= 0 ? -c : -NMAX);
   }
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(NT) void chol_packed(const MatDesc<T>* __restrict__
       const bool v = tv && r < n && c < n;
       xr[k] = v ? r : -1;
       xc[k] = v ? c : NMAX;
-      x[k] = (v && r == c) ? T(1.0) : T(0.0);
+      x[k] = T((v && r == c) ? 1.0 : 0.0);
     }
   }
   // the pivot of column jp from its (updated) diagonal entry dn: sd = sqrt, rsd = 1/sqrt (LDL:
@@ -1393,7 +1398,7 @@ __device__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       dv[u] = dg[i + u] - sigma;
-      fv[u] = i + u > 0 ? e2[i + u - 1] : T(0.0);
+      fv[u] = sel(i + u > 0, e2[i + u > 0 ? i + u - 1 : 0], T(0.0));
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1414,7 +1419,7 @@ __device__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict
     }
   }
   for (; i < n; ++i) {
-    T pn = (dg[i] - sigma) * pc - (i > 0 ? e2[i - 1] : T(0.0)) * pm;
+    T pn = (dg[i] - sigma) * pc - sel(i > 0, e2[i > 0 ? i - 1 : 0], T(0.0)) * pm;
     if (Num<T>::hi(pn) == 0.0) pn = T(-__builtin_ldexp(fabs(Num<T>::hi(pc)), -300));
     neg = neg || (pn < T(0.0));
     pm = pc;
@@ -1727,7 +1732,7 @@ __global__ __launch_bounds__(512) void eigmin_lds(const MatDesc<T>* __restrict__
         } else {
           T nrm, rnrm;
           pivot_sqrt(s, nrm, rnrm);  // (dd: off the IEEE sqrt/division sequences)
-          const T alpha = (x0 > T(0.0)) ? -nrm : nrm;
+          const T alpha = sel(x0 > T(0.0), -nrm, nrm);
           const T v0 = x0 - alpha;
           e2[k] = alpha * alpha;
           v[0] = v0;
@@ -1876,7 +1881,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
     if (tail > T(0.0)) {
       T nrm, rnrm;
       pivot_sqrt(s, nrm, rnrm);
-      const T alpha = (x0 > T(0.0)) ? -nrm : nrm;
+      const T alpha = sel(x0 > T(0.0), -nrm, nrm);
       v0 = x0 - alpha;
       e2c = alpha * alpha;
       beta = recip_fast(tail + v0 * v0) * T(2.0);
@@ -1884,7 +1889,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int i = c + 1 + lane + 64 * h;
-      if (i < n) v[i] = (i == c + 1) ? v0 : x[h];
+      if (i < n) v[i] = sel(i == c + 1, v0, x[h]);
     }
     if (lane < c + 1 && lane < ld) v[lane] = T(0.0);
     if (NH > 1 && lane + 64 < c + 1) v[lane + 64] = T(0.0);
@@ -1903,7 +1908,8 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int i = 1 + lane + 64 * h;
-      x[h] = i < n ? A[i] : T(0.0);
+      x[h] = T(0.0);
+      if (i < n) x[h] = A[i];
     }
     reflector(0, x, A[0]);
   }
@@ -1930,7 +1936,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
       pi = pi + swap_mw<16>(pi);     // classes c ^ 2
       pi = pi + swap_mw<32>(pi);     // classes c ^ 4
       if (cls == 0 && i < n) {
-        p[i] = (i > k) ? pi : T(0.0);
+        p[i] = sel(i > k, pi, T(0.0));
         if (i > k) vp += v[i] * pi;
       }
     }

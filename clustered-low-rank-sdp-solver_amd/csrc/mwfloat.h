@@ -281,6 +281,16 @@ MW_HD qd sqrt_qd(const qd& a) {
   return a * r;
 }
 
+// ---- component-wise select ------------------------------------------------------------------
+// c ? a : b on the limbs.  A C++ ternary on the structs is lowered to a select of the operands'
+// addresses, which keeps them in memory (scratch on the device: eigmin_lds2<qd> spilled 172
+// B/lane, vec_reduce<qd> 304); selecting each limb keeps everything in registers.
+MW_HD double sel(bool c, double a, double b) { return c ? a : b; }
+MW_HD dd sel(bool c, const dd& a, const dd& b) { return dd(c ? a.hi : b.hi, c ? a.lo : b.lo); }
+MW_HD qd sel(bool c, const qd& a, const qd& b) {
+  return qd(c ? a.x[0] : b.x[0], c ? a.x[1] : b.x[1], c ? a.x[2] : b.x[2], c ? a.x[3] : b.x[3]);
+}
+
 // ---- word-type traits used by every kernel -------------------------------------------------
 template <class T> struct Num;
 
@@ -302,7 +312,7 @@ template <> struct Num<dd> {
   MW_HD static double hi(const dd& v) { return v.hi; }
   MW_HD static dd from(double v) { return dd(v); }
   MW_HD static dd sqrt_(const dd& v) { return sqrt_dd(v); }
-  MW_HD static dd abs_(const dd& v) { return v.hi < 0.0 ? -v : v; }
+  MW_HD static dd abs_(const dd& v) { return sel(v.hi < 0.0, -v, v); }
   MW_HD static double eps() { return 1.2325951644078309e-32; }
   static void pack(const double* planes, int64_t n, int64_t i, dd* out) {
     double e;
@@ -322,7 +332,7 @@ template <> struct Num<qd> {
   MW_HD static double hi(const qd& v) { return v.x[0]; }
   MW_HD static qd from(double v) { return qd(v); }
   MW_HD static qd sqrt_(const qd& v) { return sqrt_qd(v); }
-  MW_HD static qd abs_(const qd& v) { return v.x[0] < 0.0 ? -v : v; }
+  MW_HD static qd abs_(const qd& v) { return sel(v.x[0] < 0.0, -v, v); }
   MW_HD static double eps() { return 1.2154326714572501e-63; }  // 2^-209
   static void pack(const double* planes, int64_t n, int64_t i, qd* out) {
     *out = qd_renorm(planes[i], planes[n + i], planes[2 * n + i], planes[3 * n + i], 0.0);

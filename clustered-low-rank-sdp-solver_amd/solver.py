@@ -327,6 +327,27 @@ def compute_step_length(M, dM, gamma, device: int = 0, return_eigs: bool = False
     return alpha.value, False
 
 
+def eigmin(blocks, precision_words: int = 1, device: int = 0):
+    """lambda_min of each exactly symmetric block at fp64 / double-double / quad-double
+    (clrsdp_eigmin; the eigenvalue part of compute_step_length, MPMP.jl:1857-1870).  Blocks are
+    float arrays or object arrays of mpmath numbers (split exactly into limbs); returns floats
+    (words 1) or mpmath numbers (the exact limb sums)."""
+    w = int(precision_words)
+    mats = [np.asarray(b) for b in blocks]
+    for a in mats:
+        if a.ndim != 2 or a.shape[0] != a.shape[1] or a.shape[0] < 1:
+            raise ValueError("blocks must be square")
+    n = np.array([a.shape[0] for a in mats], dtype=np.int64)
+    flat = np.concatenate([a.reshape(-1, order="F") for a in mats])
+    planes = to_planes(flat, w)
+    out = np.zeros(w * len(mats))
+    _lib.check(_lib.lib().clrsdp_eigmin(device, w, len(mats), n.ctypes.data_as(_lib.P_i64),
+                                        _ptr(planes), _ptr(out)))
+    if w == 1:
+        return out
+    return from_planes(out, len(mats), w)
+
+
 def initial_point(bi: BlockInfo, omega_p, omega_d):
     """x = 0, X = omega_p I, y = 0, Y = omega_d I (MPMP.jl:660-686)."""
     x = np.zeros(sum(bi.dim_S))

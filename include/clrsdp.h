@@ -318,6 +318,14 @@ int32_t clrsdp_destroy(clrsdp_handle* h);
 int32_t clrsdp_step_length(int32_t device, int64_t nblocks, const int64_t* n, const double* M,
                            const double* dM, double gamma, double* alpha, double* min_eig);
 
+/* lambda_min of each symmetric block at fp64 (words 1), double-double (2) or quad-double (4):
+ * the eigenvalue part of compute_step_length (MPMP.jl:1857-1870, approx_eig_qr! of L^-1 dM L^-T),
+ * Householder tridiagonalisation + Sturm multisection (+ the multi-word Newton tail) as the
+ * loop body runs it.  A: the nblocks blocks of sizes n[] concatenated column-major, as `words`
+ * planes of doubles (hi limb first; the blocks must be exactly symmetric); min_eig: `words` planes of nblocks values. */
+int32_t clrsdp_eigmin(int32_t device, int32_t words, int64_t nblocks, const int64_t* n,
+                      const double* A, double* min_eig);
+
 #ifdef __cplusplus
 }
 #endif

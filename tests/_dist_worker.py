@@ -39,6 +39,28 @@ def main():
         ex.close()
         return
     P = pk.make_params("0.3", "0.1", "0.7", 0)
+    if len(sys.argv) > 3 and sys.argv[3] == "failone":
+        # Y of one cluster of rank 0 negative definite: its S_j Cholesky fails on rank 0 only;
+        # the failure bits travel with STEP's exchange, so both ranks must fall back to LU
+        # together and then report the reference's step-length error (cho!(Y) fails)
+        from clrsdp_amd import _lib as L
+        x, X, y, Y = pk.initial_point(bi, 10.0, 10.0)
+        bad = pk.partition_clusters(bi, world)[0][0]
+        Y[bad] = [-0.5 * yb for yb in Y[bad]]
+        dev.set_state(x, X, y, Y)
+        code = 0
+        try:
+            dev.iterate(P, False)
+        except L.ClrsdpError as e:
+            code = e.code
+        x2, X2, y2, Y2 = dev.get_state()
+        unchanged = bool((x2 == x).all() and (y2 == y).all())
+        json.dump({"rank": rank, "owned": owned, "bad": bad, "code": code,
+                   "fact": dev.factorization, "unchanged": unchanged},
+                  open(f"{out}.{rank}.json", "w"))
+        dev.close()
+        ex.close()
+        return
     dev.set_state(*pk.initial_point(bi, 10.0, 10.0))
     log = []
     for _ in range(iters):

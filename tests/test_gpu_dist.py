@@ -116,3 +116,41 @@ def test_native_rccl_one_rank_graph_equals_plain(pk):
         dev.close()
     assert runs[0][0] == runs[1][0]
     assert np.array_equal(runs[0][1], runs[1][1]) and np.array_equal(runs[0][2], runs[1][2])
+
+
+def test_two_ranks_one_sided_failure_fall_back_together(pk):
+    """Only rank 0's cluster has an indefinite Y, so only rank 0's S_j Cholesky fails.  The
+    failure bits are OR-ed over the ranks (status_bits / status_gather with STEP's exchange), so
+    both ranks skip the update, switch S_j and Q to the pivoted LU together, re-run the body and
+    report the same outcome -- the reference's step-length error (cho!(Y), MPMP.jl:1846-1882),
+    as the single-rank handle does on the same state."""
+    from clrsdp_amd import _lib as L
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "f")
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={_port()}",
+               os.path.join(HERE, "_dist_worker.py"), out, "1", "failone", "gloo"]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        res = [json.load(open(f"{out}.{k}.json")) for k in range(2)]
+    assert res[0]["bad"] in res[0]["owned"] and res[0]["bad"] not in res[1]["owned"]
+    for rr in res:
+        assert rr["code"] == L.E_STEP, rr
+        assert rr["fact"] == L.FACT_FALLBACK | L.FACT_LU_SQ, rr
+        assert rr["unchanged"], rr
+    # the single-rank handle on the same state ends the same way
+    cons, b = pk.synth(seed=12, J=5, delta=16, rank=1, n_y=9, m=1)
+    bi = pk.get_block_info(cons)
+    x, X, y, Y = pk.initial_point(bi, 10.0, 10.0)
+    bad = res[0]["bad"]
+    Y[bad] = [-0.5 * yb for yb in Y[bad]]
+    dev = pk.DeviceSolver(cons, b, bi)
+    try:
+        dev.set_state(x, X, y, Y)
+        with pytest.raises(L.ClrsdpError) as ei:
+            dev.iterate(pk.make_params("0.3", "0.1", "0.7", 0), False)
+        assert ei.value.code == L.E_STEP
+        assert dev.factorization == L.FACT_FALLBACK | L.FACT_LU_SQ
+    finally:
+        dev.close()

@@ -195,3 +195,28 @@ def test_lu_run_matches_golden(pk):
         for key, slot in (("mu", "mu"), ("alpha_p", "alpha_p"), ("alpha_d", "alpha_d"), ("beta", "beta_c")):
             r = mpmath.mpf(ref[key])
             assert abs(mpmath.mpf(sc[slot]) - r) <= 1e-24 * max(1, abs(r)), (it + 1, key)
+
+
+def test_pipelined_loop_falls_back_like_the_synchronous_one(pk):
+    """The real sphere-packing instance at quad-double with the reference's default thresholds:
+    the Cholesky of S_j fails mid-run (iteration ~43) and the LU fallback takes over.  In the
+    pipelined loop the failure is seen one body late, with the next body already in flight
+    (replayed from the graph that fallback() then drops): that body is waited for before the
+    graphs go, both are re-run with LU, and the run ends exactly as the synchronous one --
+    same iterations, same LU switch, same log and objectives."""
+    from clrsdp_amd import _lib as L
+    from clrsdp_amd import sphere_packing as S
+    runs = []
+    for pipe in (False, True):
+        res = S.Nsphere_packing_2point(3, 8, precision_words=4, maxiterations=200, verbose=False,
+                                       return_info=True, pipelined=pipe)
+        runs.append(res)
+    a, c = runs
+    ia, ic = a[-1], c[-1]
+    assert ia.status == ic.status == "terminated"
+    assert ia.factorization & L.FACT_LU_SQ and ic.factorization & L.FACT_LU_SQ
+    assert ia.lu_switch == ic.lu_switch > 30
+    assert ia.iterations == ic.iterations
+    for ra, rc in zip(ia.log, ic.log):
+        assert ra[2:] == rc[2:]
+    assert a[8] == c[8] and a[9] == c[9]

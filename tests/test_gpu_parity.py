@@ -517,3 +517,53 @@ def test_save_restore_state_replays_bitwise(pk):
     dev.close()
     assert runs[0][0] == runs[1][0]
     assert np.array_equal(runs[0][1], runs[1][1]) and np.array_equal(runs[0][2], runs[1][2])
+
+
+@pytest.mark.parametrize("words", [1, 2])
+def test_c2_c4_full_size_newton_identities(pk, oracle, words):
+    """Config 2 (fp64) and config 4 (the C2 instance at double-double) at their full size (16
+    clusters x 64x64 blocks, rank 2, n_y = 64): the size-independent identities of one GPU
+    iteration, as for C3 -- B^T dx = p, Tr(A_* dY) + B dy = d, dX = P + sum dx_i A_i, S
+    symmetric.  At double-double B^T dx = p is checked in extended precision (longdouble, all
+    limbs of dx) to 1e-16, below what an fp64 solve reaches; the trace and weighted-A identities
+    use the fp64 oracle."""
+    from clrsdp_amd import _lib as L
+    from clrsdp_amd import instance as inst
+    cons, b = pk.synth(seed=0, J=16, delta=64, rank=2, n_y=64)
+    bi = pk.get_block_info(cons)
+    dev = pk.DeviceSolver(cons, b, bi, precision_words=words)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    dev.set_state(*pk.initial_point(bi, 100.0, 100.0))
+    for _ in range(2):
+        dev.iterate(P, False)
+    for s in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR):
+        dev.run_stage(s, P, False)
+    S = dev.buffer(L.BUF_S)
+    D = bi.dim_S[0]
+    S0 = np.asarray(S[:D * D], dtype=float).reshape(D, D, order="F")
+    # (rank 2: the rank-group sums of the general pairing leave S symmetric to round-off, not
+    # bitwise as the fused rank-1 path of C3)
+    assert np.max(np.abs(S0 - S0.T)) <= 1e-14 * np.max(np.abs(S0))
+    for s in (L.STAGE_FACTOR, L.STAGE_RESIDUALS, L.STAGE_PREDICTOR):
+        dev.run_stage(s, P, False)
+    ar = oracle.Fp64()
+    dx, dy = dev.buffer(L.BUF_DX), dev.buffer(L.BUF_DY)
+    dY = inst.flat_to_blocks(dev.buffer(L.BUF_DYMAT), bi)
+    dX = inst.flat_to_blocks(dev.buffer(L.BUF_DXMAT), bi)
+    Pm = inst.flat_to_blocks(dev.buffer(L.BUF_P), bi)
+    p, d = dev.buffer(L.BUF_PVEC), dev.buffer(L.BUF_DVEC)
+    Bst = oracle.stack_B(cons)
+    assert rel_err(Bst.T @ dx, p, np.abs(b).max()) < 1e-9
+    if words > 1:
+        import mpmath
+        # (decimal strings: np.longdouble(mpf) would round through a double)
+        dxl = np.array([np.longdouble(mpmath.nstr(v, 30)) for v in dev.buffer(L.BUF_DX, exact=True)])
+        pl = np.array([np.longdouble(mpmath.nstr(v, 30)) for v in dev.buffer(L.BUF_PVEC, exact=True)])
+        r = Bst.astype(np.longdouble).T @ dxl - pl
+        assert float(np.max(np.abs(r))) / float(np.abs(b).max()) < 1e-16
+    lhs = oracle.trace_A(ar, cons, dY, bi) + Bst @ dy
+    assert rel_err(lhs, d, np.abs(oracle.stack_c(cons)).max()) < 1e-8
+    WA = oracle.compute_weighted_A(ar, cons, dx, bi)
+    for j in range(0, bi.J, 5):
+        assert rel_err(dX[j][0], WA[j][0] + Pm[j][0]) < 1e-12
+    dev.close()

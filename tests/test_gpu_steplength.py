@@ -122,3 +122,69 @@ def test_device_solver_all_1x1_blocks(pk):
                            maxiterations=60, verbose=False, return_info=True)
     assert out[-1].iterations > 0
     assert out[-1].status in ("terminated", "optimal", "maxiterations")
+
+
+def _mp_tridiag(n, d, e, prec=320):
+    import mpmath
+    with mpmath.workprec(prec):
+        A = np.empty((n, n), dtype=object)
+        for i in range(n):
+            for j in range(n):
+                A[i, j] = mpmath.mpf(0)
+        for i in range(n):
+            A[i, i] = mpmath.mpf(d[i])
+            if i + 1 < n:
+                A[i, i + 1] = A[i + 1, i] = mpmath.mpf(e[i])
+    return A
+
+
+def _mp_eigmin(A, prec=320):
+    import mpmath
+    with mpmath.workprec(prec):
+        M = mpmath.matrix(A.tolist())
+        ev = mpmath.eigsy(M, eigvals_only=True)
+        return min(ev)
+
+
+# (qd: measured 1.0e-54 on the decoupled n = 64 tridiagonal; the qd stage parity holds 1e-50)
+EIG_TOL = {1: 1e-13, 2: 1e-28, 4: 1e-50}
+
+
+@pytest.mark.parametrize("words,n", [(1, 18), (1, 64), (1, 128), (2, 18), (2, 64), (4, 18),
+                                     (4, 64)])
+def test_eigmin_decoupled_and_zero_minor_cases(pk, words, n):
+    """lambda_min at fp64 / dd / qd (clrsdp_eigmin) on blocks whose Sturm recurrences meet zero
+    couplings and exact zero minors (the zero-minor rule of the multi-word count and its fp64
+    twin, kernels_dense.h sturm_any_below / the multi-word eig_multisection): c I (every
+    coupling zero, every minor zero at sigma = c), a tridiagonal decoupled in the middle with
+    constant diagonal (d_i = sigma for the repeated eigenvalue of both halves), a tridiagonal with
+    alternating zero couplings (2x2 blocks) and a dense block with one decoupled row.  Against
+    320-bit mpmath eigenvalues, to the word's resolution times ||A||."""
+    import mpmath
+    rng = np.random.default_rng(1000 * words + n)
+    blocks = []
+    # c I
+    blocks.append(np.eye(n) * 0.75)
+    # decoupled in the middle, d_i = 1/2, couplings 1/4 except a zero one
+    e = [0.25] * (n - 1)
+    e[n // 2 - 1] = 0.0
+    blocks.append(_mp_tridiag(n, [0.5] * n, e))
+    # 2x2 blocks [[a, b], [b, a]] (zero coupling between them), eigenvalues a -/+ b, repeated
+    d = [0.5] * n
+    e = [(0.125 if i % 2 == 0 else 0.0) for i in range(n - 1)]
+    blocks.append(_mp_tridiag(n, d, e))
+    # dense random symmetric with row/column 0 decoupled (A[0, 0] is an eigenvalue)
+    G = rng.standard_normal((n, n))
+    S = (G + G.T) / 4
+    S[0, 1:] = 0.0
+    S[1:, 0] = 0.0
+    S[0, 0] = -3.0
+    blocks.append(S)
+    got = pk.eigmin(blocks, precision_words=words)
+    with mpmath.workprec(320):
+        for q, (B, g) in enumerate(zip(blocks, got)):
+            Bm = B if B.dtype == object else np.array([[mpmath.mpf(float(x)) for x in row] for row in B], dtype=object)
+            ref = _mp_eigmin(Bm)
+            nrm = max(abs(x) for x in Bm.reshape(-1))
+            err = abs(mpmath.mpf(g) - ref) / nrm
+            assert err <= EIG_TOL[words], (q, float(g), float(ref), float(err))
