@@ -2157,25 +2157,56 @@ struct Solver final : HandleBase {
       t_t.launch(stream, false);
     }
     p_Wt.launch(stream, 1.0, 0.0);
-    // r = p - sum_j W_j^T t_j  (-> uvec with the explicit Q^-1, -> dyv for the two solves)
-    T* rv = reg_Q ? uvec : dyv;
-    if (world == 1 && nc()) {  // one launch
-      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, rv, pvec, 1.0, -1.0);
-    } else {
-      if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
-      else fill(xsend, 0.0, n_y);
-      exchange(tag, n_y);
-      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, rv, pvec, 1.0, -1.0);
+    // fp64 with the explicit Q^-1: r = p - sum of the slabs and dy = Q^-1 r in one launch
+    // (slab_qsolve; CLRSDP_SLAB_QSOLVE=0 keeps slab_sum + the GEMV)
+    bool fused_done = false;
+    if constexpr (std::is_same<T, double>::value) {
+      static const bool fused_q = [] {
+        const char* e = std::getenv("CLRSDP_SLAB_QSOLVE");
+        return !(e && e[0] == '0');
+      }();
+      const size_t lds = ((size_t)n_y + 256) * sizeof(double);
+      if (reg_Q && fused_q && lds <= 64 * 1024) {
+        const double* src = pslab;
+        int cnt = nc();
+        if (!(world == 1 && nc())) {
+          if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+          else fill(xsend, 0.0, n_y);
+          exchange(tag, n_y);
+          src = xrecv;
+          cnt = world;
+        }
+        if (pending_q) {
+          HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
+          pending_q = false;
+        }
+        slab_qsolve<<<cdiv(n_y, 64), 256, lds, stream>>>(src, cnt, n_y, (int)n_y, pvec, 1.0, -1.0,
+                                                          Qinv, (int)n_y, dyv);
+        HIPCHK(hipGetLastError());
+        fused_done = true;
+      }
     }
-    if (pending_q) {  // L_Q^-1 and Q^-1 are being computed on the side stream (iterate)
-      HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
-      pending_q = false;
-    }
-    if (reg_Q) {
-      q_qdy.launch(stream, 1.0, 0.0);         // dy = Q^-1 r
-    } else {
-      t_Q.launch(stream, false);
-      t_Q.launch(stream, true);
+    if (!fused_done) {
+      // r = p - sum_j W_j^T t_j  (-> uvec with the explicit Q^-1, -> dyv for the two solves)
+      T* rv = reg_Q ? uvec : dyv;
+      if (world == 1 && nc()) {  // one launch
+        slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, rv, pvec, 1.0, -1.0);
+      } else {
+        if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+        else fill(xsend, 0.0, n_y);
+        exchange(tag, n_y);
+        slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, rv, pvec, 1.0, -1.0);
+      }
+      if (pending_q) {  // L_Q^-1 and Q^-1 are being computed on the side stream (iterate)
+        HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
+        pending_q = false;
+      }
+      if (reg_Q) {
+        q_qdy.launch(stream, 1.0, 0.0);         // dy = Q^-1 r
+      } else {
+        t_Q.launch(stream, false);
+        t_Q.launch(stream, true);
+      }
     }
     // dx_j = L_j^-T (t_j + W_j dy)
     if (reg_S) {

@@ -386,14 +386,20 @@ __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__
       const int i = TA ? (tid >> 4) : (tid & 15), k = TA ? (tid & 15) : (tid >> 4);
       const int gi = m0 + i, gk = k0 + k;
       T v = T(0.0);
-      if (gi < d.M && gk < d.K) v = TA ? d.A[gk + (size_t)gi * d.lda] : d.A[gi + (size_t)gk * d.lda];
+      if (gi < d.M && gk < d.K) {
+        if (TA) v = d.A[gk + (size_t)gi * d.lda];
+        else v = d.A[gi + (size_t)gk * d.lda];
+      }
       As[k][i] = v;
     }
     {  // B tile 16 x 16: j contiguous in memory iff TB
       const int j = TB ? (tid & 15) : (tid >> 4), k = TB ? (tid >> 4) : (tid & 15);
       const int gj = n0 + j, gk = k0 + k;
       T v = T(0.0);
-      if (gj < d.N && gk < d.K) v = TB ? d.B[gj + (size_t)gk * d.ldb] : d.B[gk + (size_t)gj * d.ldb];
+      if (gj < d.N && gk < d.K) {
+        if (TB) v = d.B[gj + (size_t)gk * d.ldb];
+        else v = d.B[gk + (size_t)gj * d.ldb];
+      }
       Bs[k][j] = v;
     }
     __syncthreads();
@@ -438,14 +444,20 @@ __global__ __launch_bounds__(256) void gemm_valu_ks(const GemmDesc<T>* __restric
       const int i = TA ? (tid >> 5) : (tid & 7), k = TA ? (tid & 31) : (tid >> 3);
       const int gi = m0 + i, gk = k0 + k;
       T v = T(0.0);
-      if (gi < d.M && gk < d.K) v = TA ? d.A[gk + (size_t)gi * d.lda] : d.A[gi + (size_t)gk * d.lda];
+      if (gi < d.M && gk < d.K) {
+        if (TA) v = d.A[gk + (size_t)gi * d.lda];
+        else v = d.A[gi + (size_t)gk * d.lda];
+      }
       As[k][i] = v;
     }
     {  // B tile 32 x 8
       const int j = TB ? (tid & 7) : (tid >> 5), k = TB ? (tid >> 3) : (tid & 31);
       const int gj = n0 + j, gk = k0 + k;
       T v = T(0.0);
-      if (gj < d.N && gk < d.K) v = TB ? d.B[gj + (size_t)gk * d.ldb] : d.B[gk + (size_t)gj * d.ldb];
+      if (gj < d.N && gk < d.K) {
+        if (TB) v = d.B[gj + (size_t)gk * d.ldb];
+        else v = d.B[gk + (size_t)gj * d.ldb];
+      }
       Bs[k][j] = v;
     }
     __syncthreads();
@@ -743,7 +755,7 @@ __global__ __launch_bounds__(256) void flat_reduce(const T* __restrict__ a, cons
   __syncthreads();
   for (int s = blockDim.x / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) {
-      if (op == 2) red[threadIdx.x] = (red[threadIdx.x + s] > red[threadIdx.x]) ? red[threadIdx.x + s] : red[threadIdx.x];
+      if (op == 2) { if (red[threadIdx.x + s] > red[threadIdx.x]) red[threadIdx.x] = red[threadIdx.x + s]; }
       else red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + s];
     }
     __syncthreads();
@@ -756,7 +768,7 @@ __global__ __launch_bounds__(256) void flat_reduce(const T* __restrict__ a, cons
 // Block reductions (deterministic: fixed tree over a fixed thread->element map)
 // ------------------------------------------------------------------------------------------
 template <class T>
-__device__ T block_sum(T v, T* red) {
+__device__ __forceinline__ T block_sum(T v, T* red) {
   const int tid = threadIdx.x;
   red[tid] = v;
   __syncthreads();
@@ -769,12 +781,12 @@ __device__ T block_sum(T v, T* red) {
   return r;
 }
 template <class T>
-__device__ T block_max(T v, T* red) {
+__device__ __forceinline__ T block_max(T v, T* red) {
   const int tid = threadIdx.x;
   red[tid] = v;
   __syncthreads();
   for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (tid < s) red[tid] = (red[tid + s] > red[tid]) ? red[tid + s] : red[tid];
+    if (tid < s) { if (red[tid + s] > red[tid]) red[tid] = red[tid + s]; }
     __syncthreads();
   }
   T r = red[0];
@@ -1036,7 +1048,7 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
           if (q < nb) {
-            if (r == q) xr = UNIT ? v : v * rdg[q];
+            if (r == q) { if (UNIT) xr = v; else xr = v * rdg[q]; }
             const T xq = shfl_t(xr, base + q);
             if (r > q) v = v - D[r + q * NB] * xq;
           }
@@ -1045,7 +1057,7 @@ __global__ __launch_bounds__(NT) void trsm_batched(const TrsmDesc<T>* __restrict
 #pragma unroll
         for (int q = NB - 1; q >= 0; --q) {
           if (q < nb) {
-            if (r == q) xr = UNIT ? v : v * rdg[q];
+            if (r == q) { if (UNIT) xr = v; else xr = v * rdg[q]; }
             const T xq = shfl_t(xr, base + q);
             if (r < q) v = v - D[q + r * NB] * xq;
           }
@@ -1357,7 +1369,7 @@ __global__ __launch_bounds__(256) void perm_rows(const PermDesc<T>* __restrict__
 // (mathematically symmetric) L^-1 dM L^-T.
 // ------------------------------------------------------------------------------------------
 template <class T>
-__device__ int sturm_count(const T* dg, const T* e2, int n, T sigma) {
+__device__ __forceinline__ int sturm_count(const T* dg, const T* e2, int n, T sigma) {
   int cnt = 0;
   T q = dg[0] - sigma;
   if (q < T(0.0)) ++cnt;
@@ -2271,6 +2283,50 @@ __global__ void slab_sum(const T* in, int cnt, long long stride, long long n, T*
   out[e] = acc;
 }
 
+// dy = Q^-1 r with r = cbase*base + csum*sum_{i<cnt} in[i*stride + .] (slab_sum's order): the
+// slab sum and the Q^-1 GEMV of the block solve (MPMP.jl:1758-1764) in one launch.  Every
+// workgroup forms all of r in LDS (n values, a few KB), then 64 rows of the product: 4 column
+// chunks per row (coalesced reads of the column-major Q^-1), summed in a fixed order.
+__global__ __launch_bounds__(256) void slab_qsolve(const double* __restrict__ in, int cnt,
+                                                   long long stride, int n,
+                                                   const double* __restrict__ base, double cbase,
+                                                   double csum, const double* __restrict__ Q,
+                                                   int ldq, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_sq[];
+  double* r = reinterpret_cast<double*>(smem_sq);  // n
+  double* part = r + n;                            // 4 x 64
+  for (int e = threadIdx.x; e < n; e += 256) {
+    double acc = in[e];
+    int i = 1;
+    for (; i + 7 < cnt; i += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = in[(size_t)(i + u) * stride + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; i < cnt; ++i) acc += in[(size_t)i * stride + e];
+    if (base) acc = base[e] * cbase + acc * csum;
+    r[e] = acc;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, ch = threadIdx.x >> 6;
+  const int row = blockIdx.x * 64 + lane;
+  const int j0 = (int)((long long)n * ch / 4), j1 = (int)((long long)n * (ch + 1) / 4);
+  double s0 = 0.0, s1 = 0.0;
+  if (row < n) {
+    int j = j0;
+    for (; j + 1 < j1; j += 2) {
+      s0 = fma(Q[row + (size_t)j * ldq], r[j], s0);
+      s1 = fma(Q[row + (size_t)(j + 1) * ldq], r[j + 1], s1);
+    }
+    if (j < j1) s0 = fma(Q[row + (size_t)j * ldq], r[j], s0);
+  }
+  part[ch * 64 + lane] = s0 + s1;
+  __syncthreads();
+  if (ch == 0 && row < n) out[row] = (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]);
+}
+
 // vector: out = a*x + b*y (+ c*z) over n
 template <class T>
 __global__ void vec_lin(T* out, const T* x, double a, const T* y, double b, const T* z, double c,
@@ -2591,7 +2647,7 @@ __device__ inline bool pd_feasible(const T* sc, const ScalarParams<T>& p) {
 // gap, pd_feas and terminate() of the current objectives and errors (MPMP.jl:942-945 and
 // 1067-1078, 1147-1185); excl_b0: the initial gap of MPMP.jl:725 (compute_duality_gap has no b0)
 template <class T>
-__device__ inline void control_update(T* sc, const ScalarParams<T>& p, bool excl_b0) {
+__device__ __forceinline__ void control_update(T* sc, const ScalarParams<T>& p, bool excl_b0) {
   T po = sc[SC_POBJ], dob = sc[SC_DOBJ];
   if (excl_b0) {
     po = po - p.b0;
@@ -2614,7 +2670,7 @@ __device__ inline void control_update(T* sc, const ScalarParams<T>& p, bool excl
 
 // one wave: lane l folds elements l, l+64, ... in order, then a fixed xor butterfly
 template <class T>
-__device__ T fold_wave(const FoldRed<T>& r, int lane) {
+__device__ __forceinline__ T fold_wave(const FoldRed<T>& r, int lane) {
   const bool sum = r.op == 0;
   const bool mn = r.op == 3;
   T acc;
@@ -2674,13 +2730,13 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     sc[SC_MU_P] = sel(pdf, T(0.0), p.beta_inf * sc[SC_MU]);
   } else if (which == 1) {  // r, beta, beta_c, mu_c
     const T r = sc[SC_DOT_XDY] / (sc[SC_MU] * dim);
-    const T beta = (r < T(1.0)) ? r * r : r;
+    const T beta = sel(r < T(1.0), r * r, r);
     T bc;
     if (pd_feasible(sc, p)) {
-      bc = (p.beta_feas > beta) ? p.beta_feas : beta;
+      bc = sel(p.beta_feas > beta, p.beta_feas, beta);
       if (bc > T(1.0)) bc = T(1.0);
     } else {
-      bc = (p.beta_inf > beta) ? p.beta_inf : beta;
+      bc = sel(p.beta_inf > beta, p.beta_inf, beta);
     }
     sc[SC_R] = r;
     sc[SC_BETA] = beta;
@@ -2693,9 +2749,8 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     if (!(sc[SC_MINEIG_X] > -g)) ap = -g / sc[SC_MINEIG_X];
     if (!(sc[SC_MINEIG_Y] > -g)) ad = -g / sc[SC_MINEIG_Y];
     if (pd_feasible(sc, p)) {
-      const T mn = (ad < ap) ? ad : ap;
-      ap = mn;
-      ad = mn;
+      if (ad < ap) ap = ad;
+      else ad = ap;
     }
     sc[SC_ALPHA_P] = ap;
     sc[SC_ALPHA_D] = ad;

@@ -13,7 +13,7 @@ namespace clrsdp {
 
 // Deterministic block reduction for 512 threads: wave butterfly, then 8 wave sums in order.
 template <class T>
-__device__ T wave_sum(T v) {
+__device__ __forceinline__ T wave_sum(T v) {
   for (int s = 32; s > 0; s >>= 1) {
     if constexpr (sizeof(T) == 8) {
       v += __shfl_xor(v, s);
@@ -29,7 +29,7 @@ __device__ T wave_sum(T v) {
   return v;
 }
 template <class T, int NW>
-__device__ T block_sum_w(T v, T* red) {
+__device__ __forceinline__ T block_sum_w(T v, T* red) {
   v = wave_sum(v);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) red[w] = v;
@@ -1255,12 +1255,14 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
     }
   }
   __syncthreads();
-  // 256-way multisection on waves 0-3 (one per SIMD), 7 rounds of 8 bits: as eigmin_reg
   double lo = bnd[0], hi = bnd[1];
   const int nr = (n + 7) & ~7;
-  constexpr int NCW = (DBG & 8) ? NWB : 4;         // counting waves (one per SIMD)
+  // 512-way on the 8 bulk waves (two per SIMD: the count is a latency-bound chain, so the second
+  // wave per SIMD costs little), 6 rounds of 9 bits (2^-54 of the span): 3 us less than 256-way
+  // on 4 waves in 7 rounds (DBG 64 keeps that, DBG 8 the two-ended count)
+  constexpr int NCW = (DBG & 64) ? 4 : NWB;        // counting waves
   constexpr double NSIG = 64.0 * NCW + 1.0;
-  for (int it = 0; it < ((DBG & 8) ? 6 : 7); ++it) {
+  for (int it = 0; it < ((DBG & 64) ? 7 : 6); ++it) {
     const double width = hi - lo;
     if (w < NCW) {
       const double sigma = lo + width * ((double)(tid + 1) / NSIG);
@@ -1386,7 +1388,7 @@ template <> struct HalfWord<mw::qd> {
 // form (sturm_count), whose fp64 division sequences made the multi-word rounds of the
 // multisection 56 % of eigmin_lds<dd>.
 template <class T>
-__device__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict__ e2, int n,
+__device__ __forceinline__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict__ e2, int n,
                                    const T& sigma) {
   T pm = T(0.0), pc = T(1.0);
   bool neg = false;
@@ -1438,7 +1440,7 @@ __device__ bool sturm_any_below_mw(const T* __restrict__ dg, const T* __restrict
 // tridiagonal (dg, e2 = squared off-diagonals) in LDS to the word's precision, into
 // out[blockIdx.x].  A is LDS scratch (>= 2n + 14 doubles), Wv one word of LDS scratch.
 template <class T, bool NEWTON>
-__device__ void eig_multisection(const T* __restrict__ dg, const T* __restrict__ e2, int n,
+__device__ __forceinline__ void eig_multisection(const T* __restrict__ dg, const T* __restrict__ e2, int n,
                                  T* __restrict__ A, T* __restrict__ Wv, T* __restrict__ out) {
   constexpr int NT = 512, NW = 8;
   const int tid = threadIdx.x;

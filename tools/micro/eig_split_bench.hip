@@ -150,7 +150,7 @@ int main(int argc, char** argv) {
     MatDesc<double>* dd;
     CK(hipMalloc(&dd, nb * sizeof(MatDesc<double>)));
     CK(hipMemcpy(dd, din.data(), nb * sizeof(MatDesc<double>), hipMemcpyHostToDevice));
-    printf("DBG variants (n=128, batch=128): full %.1f us | two-ended multisection %.1f | no update FMAs %.1f | no matvec FMAs %.1f | no FMAs %.1f | no reflector %.1f | nothing %.1f | slot pairs %.1f\n",
+    printf("DBG variants (n=128, batch=128): full %.1f us | two-ended multisection %.1f | no update FMAs %.1f | no matvec FMAs %.1f | no FMAs %.1f | no reflector %.1f | nothing %.1f | slot pairs %.1f | 256-way 4 waves %.1f\n",
            timeit([&] { eigmin_split<0><<<nb, 576>>>(dd, dE); }),
            timeit([&] { eigmin_split<8><<<nb, 576>>>(dd, dE); }),
            timeit([&] { eigmin_split<1><<<nb, 576>>>(dd, dE); }),
@@ -158,7 +158,8 @@ int main(int argc, char** argv) {
            timeit([&] { eigmin_split<3><<<nb, 576>>>(dd, dE); }),
            timeit([&] { eigmin_split<4><<<nb, 576>>>(dd, dE); }),
            timeit([&] { eigmin_split<7><<<nb, 576>>>(dd, dE); }),
-           timeit([&] { eigmin_split<16><<<nb, 576>>>(dd, dE); }));
+           timeit([&] { eigmin_split<16><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<64><<<nb, 576>>>(dd, dE); }));
     CK(hipFree(dA));
     CK(hipFree(dE));
     CK(hipFree(dd));

@@ -17,5 +17,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -
   python3 bench.py --steps 5 --warmup 1 --no-cpu > $OUT/bench_write.log 2>&1
 python3 tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv \
   $OUT/write/run_counter_collection.csv $OUT/schur_pmc.json > /dev/null
-python3 tools/prof_summary.py $OUT/kt/run_kernel_stats.csv 33 > $OUT/kernel_summary.txt
+python3 tools/prof_summary.py $OUT/kt/run_kernel_stats.csv > $OUT/kernel_summary.txt
+python3 tools/copy_census.py $OUT/kt/run_kernel_trace.csv > $OUT/copy_census.txt
+python3 tools/iter_trace.py $OUT/kt/run_kernel_trace.csv > $OUT/body_trace.txt
 echo done
