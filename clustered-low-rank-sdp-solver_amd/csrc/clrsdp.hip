@@ -657,6 +657,18 @@ struct MatPlan : PlanBase {  // potrf / eigmin
       const char* e = std::getenv("CLRSDP_EIG_NEWTON");
       return !(e && e[0] == '0');
     }();
+    // multi-word, n <= 64, with CLRSDP_EIG_MX=1: an fp64 eigenpair refined at the word's width
+    // (eigmin_mx, which falls back to eigmin_lds2's path per block; experimental, off by default)
+    static const bool mx = env_on("CLRSDP_EIG_MX");
+    if constexpr (!std::is_same<T, double>::value) {
+      if (mx && newton && nmax <= 64 && eigmx_lds_bytes<T>(nmax) <= LDS_MAX) {
+        static std::atomic<unsigned long long> attrm{0};
+        lds_attr_once(attrm, (const void*)eigmin_mx<T>, (int)LDS_MAX);
+        eigmin_mx<T><<<(unsigned)h.size(), 512, eigmx_lds_bytes<T>(nmax), s>>>(d, out);
+        HIPCHK(hipGetLastError());
+        return;
+      }
+    }
     // multi-word: eigmin_lds2 (two barriers per column) unless CLRSDP_EIG_LDS1=1
     static const bool lds1 = env_on("CLRSDP_EIG_LDS1");
     if (!std::is_same<T, double>::value && !lds1 && eig2_lds_bytes<T>(nmax) <= LDS_MAX &&

@@ -1836,37 +1836,21 @@ template <class T> size_t eig2_lds_bytes(int n) {
   // A (n x ld), v (2 x ld), p (ld), dg, e2, scal (4), redw (2 x 8), + the tail's fp64 scratch
   return sizeof(T) * ((size_t)n * eig2_ld<T>(n) + 3 * (size_t)eig2_ld<T>(n) + 2 * (size_t)n + 4 + 16) + 64;
 }
-// DBG (timing experiments, tools/micro/eig2_mw.hip): 1 = stop after the tridiagonalisation
-template <class T, bool NEWTON = true, int DBG = 0>
-__global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict__ descs,
-                                                   T* __restrict__ out) {
-  constexpr int NT = 512;
+// The tridiagonalisation loop of eigmin_lds2 on the symmetric image A (n x ld in LDS, n >= 2,
+// 512 threads): dg, e2 (and the last diagonal entry) when it returns.  KEEPV (fp64, eigmin_mx)
+// also keeps every reflector: v_c in column c of V (n x n, rows c+1..n-1), beta_c in bet[c] and
+// the signed off-diagonal T(c+1, c) in eo[c], so that A = Q T Q^T with Q = H_0 H_1 ... H_{n-3}.
+template <class T, bool KEEPV>
+__device__ __forceinline__ void tridiag_lds2(T* __restrict__ A, int ld, int n, T* __restrict__ vb,
+                                             T* __restrict__ p, T* __restrict__ dg,
+                                             T* __restrict__ e2, T* __restrict__ scal,
+                                             T* __restrict__ redw, T* __restrict__ V,
+                                             T* __restrict__ bet, T* __restrict__ eo) {
   // column slots per lane (j = cls + 8 t) and rows per lane in the reflector: a quad-double
   // image fits LDS only for n <= 64 (the launch checks it), so qd carries 8 slots and one row,
   // which keeps its per-lane words out of scratch
   constexpr int NSL = sizeof(T) > 16 ? 8 : 16, NH = sizeof(T) > 16 ? 1 : 2;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const MatDesc<T> d = descs[blockIdx.x];
-  const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ld = eig2_ld<T>(n);
-  T* A = reinterpret_cast<T*>(smem_raw);      // n x ld, column-major
-  T* vb = A + (size_t)n * ld;                 // 2 x ld: v of step k in vb[(k & 1) * ld]
-  T* p = vb + 2 * ld;                          // ld
-  T* dg = p + ld;                              // n
-  T* e2 = dg + n;                              // n
-  T* scal = e2 + n;                            // [0..1] beta of the two v buffers
-  T* redw = scal + 4;                          // 2 x 8 per-wave parts of v^T p
-  // coalesced load, then symmetrise: A = (A + A^T)/2
-  for (int j = tid >> 6; j < n; j += NT / 64)
-    for (int i = lane; i < n; i += 64) A[i + (size_t)j * ld] = d.A[i + (size_t)j * d.lda];
-  __syncthreads();
-  for (int j = tid >> 6; j < n; j += NT / 64)
-    for (int i = lane; i < j; i += 64) {
-      const T sv = (A[i + (size_t)j * ld] + A[j + (size_t)i * ld]) * T(0.5);
-      A[i + (size_t)j * ld] = sv;
-      A[j + (size_t)i * ld] = sv;
-    }
-  __syncthreads();
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 7, cls = lane >> 3;
   const int npass = (n + 63) / 64;
   // reflector of column c from its entries x_i = col[i] (i > c; lane l holds rows c+1+l and
@@ -1879,19 +1863,24 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
     const T x0 = shfl_t(x[0], 0);  // row c+1
     const T tail = s - x0 * x0;
     T* v = vb + (c & 1) * ld;
-    T beta = T(0.0), v0 = x0, e2c = x0 * x0;
+    T beta = T(0.0), v0 = x0, e2c = x0 * x0, offd = x0;
     if (tail > T(0.0)) {
       T nrm, rnrm;
       pivot_sqrt(s, nrm, rnrm);
       const T alpha = sel(x0 > T(0.0), -nrm, nrm);
       v0 = x0 - alpha;
       e2c = alpha * alpha;
+      offd = alpha;
       beta = recip_fast(tail + v0 * v0) * T(2.0);
     }
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int i = c + 1 + lane + 64 * h;
-      if (i < n) v[i] = sel(i == c + 1, v0, x[h]);
+      if (i < n) {
+        const T vi = sel(i == c + 1, v0, x[h]);
+        v[i] = vi;
+        if constexpr (KEEPV) V[i + (size_t)c * n] = vi;
+      }
     }
     if (lane < c + 1 && lane < ld) v[lane] = T(0.0);
     if (NH > 1 && lane + 64 < c + 1) v[lane + 64] = T(0.0);
@@ -1899,12 +1888,12 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
       dg[c] = diag;
       e2[c] = e2c;
       scal[c & 1] = beta;
+      if constexpr (KEEPV) {
+        bet[c] = beta;
+        eo[c] = offd;
+      }
     }
   };
-  if (n == 1) {
-    if (tid == 0) out[blockIdx.x] = A[0];
-    return;
-  }
   if (w == 0) {  // the reflector of column 0 from the input
     T x[NH];
 #pragma unroll
@@ -2001,13 +1990,435 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
   // the last diagonal entry (updated by the last step's (D))
   if (tid == 0) dg[n - 1] = A[(n - 1) + (size_t)(n - 1) * ld];
   __syncthreads();
+}
+
+// DBG (timing experiments, tools/micro/eig2_mw.hip): 1 = stop after the tridiagonalisation
+template <class T, bool NEWTON, int DBG>
+__device__ __forceinline__ void eigmin_lds2_dev(const MatDesc<T>& d, T* __restrict__ out,
+                                                char* __restrict__ smem_raw) {
+  constexpr int NT = 512;
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63;
+  const int ld = eig2_ld<T>(n);
+  T* A = reinterpret_cast<T*>(smem_raw);      // n x ld, column-major
+  T* vb = A + (size_t)n * ld;                 // 2 x ld: v of step k in vb[(k & 1) * ld]
+  T* p = vb + 2 * ld;                          // ld
+  T* dg = p + ld;                              // n
+  T* e2 = dg + n;                              // n
+  T* scal = e2 + n;                            // [0..1] beta of the two v buffers
+  T* redw = scal + 4;                          // 2 x 8 per-wave parts of v^T p
+  // coalesced load, then symmetrise: A = (A + A^T)/2
+  for (int j = tid >> 6; j < n; j += NT / 64)
+    for (int i = lane; i < n; i += 64) A[i + (size_t)j * ld] = d.A[i + (size_t)j * d.lda];
+  __syncthreads();
+  for (int j = tid >> 6; j < n; j += NT / 64)
+    for (int i = lane; i < j; i += 64) {
+      const T sv = (A[i + (size_t)j * ld] + A[j + (size_t)i * ld]) * T(0.5);
+      A[i + (size_t)j * ld] = sv;
+      A[j + (size_t)i * ld] = sv;
+    }
+  __syncthreads();
+  if (n == 1) {
+    if (tid == 0) out[blockIdx.x] = A[0];
+    return;
+  }
+  tridiag_lds2<T, false>(A, ld, n, vb, p, dg, e2, scal, redw, nullptr, nullptr, nullptr);
   if constexpr (DBG == 1) {
     if (tid == 0) out[blockIdx.x] = dg[n - 1] + e2[0];
     return;
   }
   eig_multisection<T, NEWTON>(dg, e2, n, A, p, out);
 }
+
+template <class T, bool NEWTON = true, int DBG = 0>
+__global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict__ descs,
+                                                   T* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  eigmin_lds2_dev<T, NEWTON, DBG>(descs[blockIdx.x], out, smem_raw);
+}
 #undef ANY_BELOW
+
+// ------------------------------------------------------------------------------------------
+// eigmin_mx (round 4): multi-word lambda_min (n <= 64) from an fp64 eigenpair refined at the
+// word's width, instead of a multi-word tridiagonalisation.  The reference computes lambda_min
+// of L^-1 dM L^-T at BigFloat precision (compute_step_length, MPMP.jl:1857-1870); eigmin_lds2
+// does so in double-double / quad-double arithmetic throughout, where every one of the n - 2
+// columns is a chain of multi-word reductions, square roots and reciprocals (~5 us per column
+// at dd).  Here:
+//   1. A_h = the leading words of A_s = (A + A^T)/2, tridiagonalised in fp64 (tridiag_lds2,
+//      keeping the reflectors): A_h = Q T Q^T.  T is rescaled by a power of two (|T| < 1).
+//   2. fp64 lambda of T (512-way multisection) and a lower bound of its second eigenvalue: one
+//      512-way round of full Sturm counts at lambda + span 2^(-t/8) (count <= 1 => lambda_2 >= ..).
+//   3. z = its eigenvector (inverse iteration, tridiagonal LU with partial pivoting), x = Q z.
+//   4. R refinement steps (1 at dd, 2 at qd): r = A_s x - rho x with rho = x^T A_s x / x^T x at
+//      the full width (the only multi-word work: two or three n^2 matrix-vector products), then
+//      the Newton correction (A - rho I) d = -r, d orthogonal to x, solved in fp64 through the
+//      same Q and T: d = Q P (T - lambda I)^-1 P Q^T (-r), P = I - z z^T; x <- x + d (each step
+//      multiplies the eigenvector error by ~eps64 ||A|| / gap).
+//   5. rho of the final x.  Temple's bound: with ||r||^2 / ||x||^2 = eta and lambda_2 > rho,
+//      rho - eta / (lambda_2 - rho) <= lambda_min <= rho.  rho is accepted when that width is
+//      below 2^-(BITS+2) of the spectrum's magnitude; otherwise (a multiple or tightly
+//      clustered lambda_min, or no separated lambda_2) the workgroup runs eigmin_lds2's
+//      multi-word path on the same block (eigmx_fallbacks counts those).
+// ------------------------------------------------------------------------------------------
+__device__ unsigned int g_eigmx_fallbacks = 0;
+template <class T> __host__ __device__ constexpr int eigmx_refine() { return sizeof(T) > 16 ? 2 : 1; }
+template <class T> size_t eigmx_own_bytes(int n) {
+  const size_t ld = eig2_ld<double>(n), W = sizeof(T) / 8;
+  return 8 * ((size_t)n * ld + 3 * ld + 2 * (size_t)n + 4 + 16 + (size_t)n * n + 2 * (size_t)n +
+              6 * (size_t)n + 64 + 8 + W * (size_t)n + 8 * W * (size_t)n) + 64;
+}
+template <class T> size_t eigmx_lds_bytes(int n) {
+  const size_t a = eigmx_own_bytes<T>(n), b = eig2_lds_bytes<T>(n);
+  return a > b ? a : b;
+}
+// Sturm count of the (scaled, |T| < 1) tridiagonal in pivot form, pivots floored at 2^-900
+__device__ __forceinline__ int sturm_count_piv(const double* __restrict__ dg,
+                                               const double* __restrict__ e2, int n, double sigma) {
+  constexpr double PIVMIN = 0x1p-900;
+  int cnt = 0;
+  double q = dg[0] - sigma;
+  if (fabs(q) < PIVMIN) q = -PIVMIN;
+  cnt += q < 0.0;
+  for (int i = 1; i < n; ++i) {
+    q = (dg[i] - sigma) - e2[i - 1] / q;
+    if (fabs(q) < PIVMIN) q = -PIVMIN;
+    cnt += q < 0.0;
+  }
+  return cnt;
+}
+// LU with partial pivoting of the tridiagonal T - lam I (diagonal dg, off-diagonal eo; LAPACK
+// dgttrf's elimination order), one thread, the modified row carried in registers; pivots
+// floored at 2^-900, rfd = the reciprocals of U's diagonal, fpv = 1 where rows i, i+1 swapped.
+__device__ __forceinline__ void tri_lu(const double* __restrict__ dg, const double* __restrict__ eo,
+                                       int n, double lam, double* __restrict__ rfd,
+                                       double* __restrict__ fdu, double* __restrict__ fdu2,
+                                       double* __restrict__ fdl, double* __restrict__ fpv) {
+  constexpr double PIVMIN = 0x1p-900;
+  double di = dg[0] - lam, dui = eo[0];
+#pragma unroll 4
+  for (int i = 0; i + 1 < n; ++i) {
+    const double li = eo[i];
+    const double dn = dg[i + 1] - lam;
+    const double dun = i + 2 < n ? eo[i + 1] : 0.0;
+    if (fabs(di) >= fabs(li)) {
+      if (fabs(di) < PIVMIN) di = PIVMIN;
+      const double r = 1.0 / di, f = li * r;
+      rfd[i] = r;
+      fdu[i] = dui;
+      fdu2[i] = 0.0;
+      fdl[i] = f;
+      fpv[i] = 0.0;
+      di = dn - f * dui;
+      dui = dun;
+    } else {
+      const double r = 1.0 / li, f = di * r;
+      rfd[i] = r;
+      fdu[i] = dn;
+      fdu2[i] = dun;
+      fdl[i] = f;
+      fpv[i] = 1.0;
+      di = dui - f * dn;
+      dui = -f * dun;
+    }
+  }
+  if (fabs(di) < PIVMIN) di = PIVMIN;
+  rfd[n - 1] = 1.0 / di;
+}
+// b <- (T - lam I)^-1 b with tri_lu's factors (dgttrs's order), one thread
+__device__ __forceinline__ void tri_solve(const double* __restrict__ rfd,
+                                          const double* __restrict__ fdu,
+                                          const double* __restrict__ fdu2,
+                                          const double* __restrict__ fdl,
+                                          const double* __restrict__ fpv, int n,
+                                          double* __restrict__ b) {
+  double bi = b[0];
+#pragma unroll 4
+  for (int i = 0; i + 1 < n; ++i) {
+    const double bn = b[i + 1], l = fdl[i];
+    if (fpv[i] == 0.0) {
+      b[i] = bi;
+      bi = bn - l * bi;
+    } else {
+      b[i] = bn;
+      bi = bi - l * bn;
+    }
+  }
+  double x1 = bi * rfd[n - 1], x2 = 0.0;
+  b[n - 1] = x1;
+#pragma unroll 4
+  for (int i = n - 2; i >= 0; --i) {
+    const double x = (b[i] - fdu[i] * x1 - fdu2[i] * x2) * rfd[i];
+    b[i] = x;
+    x2 = x1;
+    x1 = x;
+  }
+}
+// DBG: per-block diagnostics and phase stamps (s_memtime) in g_eigmx_dbg[block * 24 + slot]
+__device__ double g_eigmx_dbg[256 * 24];
+// DBG 2: block 0's fp64 data for a host check (V n x n, then dg, eo, bet, z, x, r, s, d', d by n)
+__device__ double g_eigmx_dump[64 * 64 + 12 * 64];
+template <class T, int DBG = 0>
+__global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ descs,
+                                                 T* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  constexpr int NT = 512, NW = 8, R = eigmx_refine<T>();
+  const MatDesc<T> d = descs[blockIdx.x];
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double* dbg = DBG ? g_eigmx_dbg + (size_t)(blockIdx.x & 255) * 24 : nullptr;
+  unsigned long long t_prev = DBG ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto stamp = [&](int slot) {
+    if constexpr (DBG != 0) {
+      if (tid == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        dbg[slot] = (double)(t - t_prev);
+        t_prev = t;
+      }
+    }
+  };
+  bool ok = n >= 3;
+  if (ok) {
+    const int ld = eig2_ld<double>(n);
+    double* A = reinterpret_cast<double*>(smem_raw);  // n x ld
+    double* vb = A + (size_t)n * ld;                  // 2 x ld
+    double* p = vb + 2 * ld;                           // ld
+    double* dg = p + ld;                               // n
+    double* e2 = dg + n;                               // n
+    double* scal = e2 + n;                             // 4
+    double* redw = scal + 4;                           // 16
+    double* V = redw + 16;                             // n x n reflectors
+    double* bet = V + (size_t)n * n;                   // n
+    double* eo = bet + n;                              // n signed off-diagonal
+    double* rfd = eo + n;                              // n  1 / U's diagonal
+    double* fdu = rfd + n;                             // n  U first superdiagonal
+    double* fdu2 = fdu + n;                            // n  U second superdiagonal
+    double* fdl = fdu2 + n;                            // n  L multipliers
+    double* fpv = fdl + n;                             // n  interchange flags
+    double* wv = fpv + n;                              // n  right-hand side / solution
+    double* sc = wv + n;                               // 64 scalars
+    unsigned long long* masks = reinterpret_cast<unsigned long long*>(sc + 64);  // 8
+    T* xv = reinterpret_cast<T*>(masks + 8);           // n   the eigenvector estimate
+    T* part = xv + n;                                  // 8 x n  row partials of A_s x
+    // (1) leading words of the symmetrised block, then the fp64 tridiagonalisation
+    for (int j = w; j < n; j += NW)
+      for (int i = lane; i < n; i += 64) {
+        if (i < j) continue;
+        const T s = (d.A[i + (size_t)j * d.lda] + d.A[j + (size_t)i * d.lda]) * T(0.5);
+        A[i + (size_t)j * ld] = Num<T>::hi(s);
+        A[j + (size_t)i * ld] = Num<T>::hi(s);
+      }
+    __syncthreads();
+    stamp(0);
+    tridiag_lds2<double, true>(A, ld, n, vb, p, dg, e2, scal, redw, V, bet, eo);
+    stamp(1);
+    // Gershgorin bracket of T and the power of two that scales it below 1
+    if (tid == 0) {
+      double glo = 0.0, ghi = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const double rr = (i > 0 ? fabs(eo[i - 1]) : 0.0) + (i + 1 < n ? fabs(eo[i]) : 0.0);
+        const double a = dg[i] - rr, b = dg[i] + rr;
+        if (i == 0 || a < glo) glo = a;
+        if (i == 0 || b > ghi) ghi = b;
+      }
+      const double mag = fmax(fabs(glo), fabs(ghi));
+      const bool fin = mag > 0.0 && mag < INFINITY;
+      const int ex = fin ? __builtin_amdgcn_frexp_exp(mag) : 0;
+      sc[0] = fin ? 1.0 : 0.0;
+      sc[1] = (double)ex;
+      const double span = ldexp(ghi - glo, -ex);
+      sc[2] = ldexp(glo, -ex) - span * 1e-3 - 1e-300;
+      sc[3] = ldexp(ghi, -ex) + span * 1e-3 + 1e-300;
+    }
+    __syncthreads();
+    ok = sc[0] != 0.0;
+    if (ok) {
+      const int ex = (int)sc[1];
+      for (int i = tid; i < n; i += NT) {
+        dg[i] = ldexp(dg[i], -ex);
+        e2[i] = ldexp(e2[i], -2 * ex);
+        eo[i] = ldexp(eo[i], -ex);
+      }
+      __syncthreads();
+      auto first_hit = [&](bool hit) -> int {
+        const unsigned long long mk = __ballot(hit);
+        if (lane == 0) masks[w] = mk;
+        __syncthreads();
+        int f = -1;
+        for (int q = 0; q < NW && f < 0; ++q)
+          if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
+        __syncthreads();
+        return f;
+      };
+      // (2) lambda of T: 6 rounds of 512 division-free counts (54 bits of the span)
+      double lo = sc[2], hi = sc[3];
+      for (int it = 0; it < 6; ++it) {
+        const double width = hi - lo;
+        const bool hit = sturm_any_below_mw<double>(dg, e2, n, lo + width * ((double)(tid + 1) / 513.0));
+        const int f = first_hit(hit);
+        if (f < 0) {
+          lo = lo + width * (512.0 / 513.0);
+        } else {
+          hi = lo + width * ((double)(f + 1) / 513.0);
+          if (f > 0) lo = lo + width * ((double)f / 513.0);
+        }
+      }
+      const double lam = 0.5 * (lo + hi), span = sc[3] - sc[2];
+      // lower bound of lambda_2: the largest lam + span 2^(-t/8) with at most one eigenvalue below
+      const double gt = span * exp2(-(double)tid * 0.125);
+      const int f2 = first_hit(sturm_count_piv(dg, e2, n, lam + gt) <= 1);
+      // the fp64 tridiagonal is within ~n eps64 |T| of A_s (backward stable, plus the rounding
+      // of A_s to its leading words): a margin of 2^-40 of the scaled magnitude
+      const double lam2 = f2 < 0 ? -INFINITY : lam + span * exp2(-(double)f2 * 0.125) - 0x1p-40;
+      stamp(2);
+      // (3) LU of T - lam I and two inverse-iteration solves from the all-ones vector (thread 0)
+      if (tid == 0) {
+        tri_lu(dg, eo, n, lam, rfd, fdu, fdu2, fdl, fpv);
+        for (int i = 0; i < n; ++i) wv[i] = 1.0;
+        for (int rep = 0; rep < 2; ++rep) {
+          tri_solve(rfd, fdu, fdu2, fdl, fpv, n, wv);
+          double mx = 0.0;
+          for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(wv[i]));
+          const double s = mx > 0.0 && mx < INFINITY ? 1.0 / mx : 0.0;
+          for (int i = 0; i < n; ++i) wv[i] *= s;
+        }
+      }
+      __syncthreads();
+      stamp(3);
+      // (3') wave 0: z = wv / ||wv||, x = Q z (reflectors n-3 .. 0), x / ||x||
+      double zl = 0.0;  // (wave 0, lane l < n: z_l; kept in the register for the projections)
+      // x <- Q x (H_{n-3} first) or Q^T x (H_0 first), lane l holding x_l: the next reflector's
+      // entry is loaded ahead of the current one's wave sum
+      auto apply_q = [&](double xl, bool transpose) -> double {
+        const int m = n - 2, dk = transpose ? 1 : -1;
+        int k = transpose ? 0 : n - 3;
+        double vk = lane > k && lane < n ? V[lane + (size_t)k * n] : 0.0, bk = bet[k];
+        for (int s = 0; s < m; ++s) {
+          const int kn = k + dk;
+          double vn = 0.0, bn = 0.0;
+          if (s + 1 < m) {
+            vn = lane > kn && lane < n ? V[lane + (size_t)kn * n] : 0.0;
+            bn = bet[kn];
+          }
+          const double t = wave_sum_mw<double>(vk * xl);
+          xl -= (bk * t) * vk;
+          vk = vn;
+          bk = bn;
+          k = kn;
+        }
+        return xl;
+      };
+      if (w == 0) {
+        double zz = lane < n ? wv[lane] : 0.0;
+        const double nz = sqrt(wave_sum_mw<double>(zz * zz));
+        zl = nz > 0.0 ? zz / nz : 0.0;
+        double xl = apply_q(zl, false);
+        const double nx = sqrt(wave_sum_mw<double>(xl * xl));
+        xl = nx > 0.0 ? xl / nx : 0.0;
+        if (lane < n) xv[lane] = T(xl);
+        if constexpr (DBG == 2) {
+          if (blockIdx.x == 0 && lane < n) {
+            double* dm = g_eigmx_dump + (size_t)n * n;
+            dm[lane] = dg[lane];
+            dm[n + lane] = eo[lane];
+            dm[2 * n + lane] = bet[lane];
+            dm[3 * n + lane] = zl;
+            dm[4 * n + lane] = xl;
+            for (int k = 0; k < n; ++k) g_eigmx_dump[lane + (size_t)k * n] = V[lane + (size_t)k * n];
+            if (lane == 0) { dm[10 * n] = lam; dm[10 * n + 1] = sc[1]; }
+          }
+        }
+        if (lane == 0) sc[4] = nz > 0.0 && nx > 0.0 ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      stamp(4);
+      ok = sc[4] != 0.0;
+      // (4) R refinement steps, then (5) the accepted Rayleigh quotient
+      for (int it = 0; ok && it <= R; ++it) {
+        // row partials of y = A_s x: row lane, columns j = w (mod 8)
+        if (lane < n) {
+          T acc = T(0.0);
+          for (int j = w; j < n; j += NW) {
+            const T s = (d.A[lane + (size_t)j * d.lda] + d.A[j + (size_t)lane * d.lda]) * T(0.5);
+            acc = acc + s * xv[j];
+          }
+          part[w * n + lane] = acc;
+        }
+        __syncthreads();
+        stamp(5 + 3 * it);
+        if (w == 0) {
+          T y = T(0.0), xl = T(0.0);
+          if (lane < n) {
+            xl = xv[lane];
+            y = ((part[lane] + part[n + lane]) + (part[2 * n + lane] + part[3 * n + lane])) +
+                ((part[4 * n + lane] + part[5 * n + lane]) + (part[6 * n + lane] + part[7 * n + lane]));
+          }
+          const T num = wave_sum_mw<T>(xl * y), den = wave_sum_mw<T>(xl * xl);
+          const T rho = num / den;
+          const T rr = y - rho * xl;
+          const double rh = ldexp(Num<T>::hi(rr), -(int)sc[1]);  // scaled residual
+          const double eta = wave_sum_mw<double>(rh * rh) / Num<T>::hi(den);
+          if constexpr (DBG != 0) {
+            if (lane == 0) dbg[16 + it] = eta;
+          }
+          if (it == R) {
+            const double rhs = ldexp(Num<T>::hi(rho), -(int)sc[1]);
+            const double tw = lam2 > rhs ? eta / (lam2 - rhs) : INFINITY;
+            const bool acc = tw <= 0x1p-3 * Num<T>::eps();  // 2^-(BITS+2) of |T| < 1
+            if (lane == 0) {
+              sc[5] = acc ? 1.0 : 0.0;
+              if (acc) out[blockIdx.x] = rho;
+              if constexpr (DBG != 0) {
+                dbg[20] = lam;
+                dbg[21] = lam2;
+                dbg[22] = rhs;
+                dbg[23] = tw;
+              }
+            }
+          } else {
+            // s = P Q^T (-r) in fp64 (scaled) -> wv for the solve
+            double s = apply_q(-rh, true);
+            s -= wave_sum_mw<double>(zl * s) * zl;
+            if (lane < n) wv[lane] = s;
+            if constexpr (DBG == 2) {
+              if (blockIdx.x == 0 && it == 0 && lane < n) {
+                double* dm = g_eigmx_dump + (size_t)n * n;
+                dm[5 * n + lane] = rh;
+                dm[6 * n + lane] = s;
+              }
+            }
+          }
+        }
+        __syncthreads();
+        if (it == R) {
+          ok = sc[5] != 0.0;
+          break;
+        }
+        if (tid == 0) tri_solve(rfd, fdu, fdu2, fdl, fpv, n, wv);  // (T - lam I) d' = s
+        __syncthreads();
+        stamp(6 + 3 * it);
+        if (w == 0) {  // x += Q P d' (unscaled: the residual was scaled by 2^-ex)
+          double dl = lane < n ? wv[lane] : 0.0;
+          dl -= wave_sum_mw<double>(zl * dl) * zl;
+          dl = apply_q(dl, false);
+          if constexpr (DBG == 2) {
+            if (blockIdx.x == 0 && it == 0 && lane < n) {
+              double* dm = g_eigmx_dump + (size_t)n * n;
+              dm[7 * n + lane] = wv[lane];
+              dm[8 * n + lane] = dl;
+            }
+          }
+          if (lane < n) xv[lane] = xv[lane] + T(dl);
+        }
+        __syncthreads();
+        stamp(7 + 3 * it);
+      }
+    }
+  }
+  if (ok) return;
+  // the multi-word path on this block (a clustered lambda_min, or n < 3)
+  if (tid == 0 && n >= 3) atomicAdd(&g_eigmx_fallbacks, 1u);
+  __syncthreads();
+  eigmin_lds2_dev<T, true, 0>(d, out, smem_raw);
+}
 
 }  // namespace clrsdp
 

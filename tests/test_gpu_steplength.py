@@ -188,3 +188,44 @@ def test_eigmin_decoupled_and_zero_minor_cases(pk, words, n):
             nrm = max(abs(x) for x in Bm.reshape(-1))
             err = abs(mpmath.mpf(g) - ref) / nrm
             assert err <= EIG_TOL[words], (q, float(g), float(ref), float(err))
+
+
+@pytest.mark.parametrize("words,n", [(2, 18), (2, 40), (2, 64), (4, 18), (4, 40)])
+def test_eigmin_refined_fp64_eigenpair(pk, words, n):
+    """The multi-word lambda_min of blocks up to 64 (eigmin_mx: fp64 tridiagonalisation and
+    eigenpair, refined at the word's width, accepted by Temple's bound, else the multi-word
+    tridiagonalisation) on blocks whose leading words alone would give the wrong answer:
+    Q diag(lam) Q^T at 320 bits with lambda_2 - lambda_1 = 2^-g (g = 3, 30, 60; 2^-60 is below
+    the fp64 resolution, so that block takes the multi-word path) and a random symmetric block
+    with entries carrying lower words.  Against 320-bit mpmath eigenvalues, to the word's
+    resolution times ||A|| (the limb split of the 320-bit entries moves lambda_min by about
+    2^-BITS ||A||, far inside the tolerance)."""
+    import mpmath
+    rng = np.random.default_rng(7000 + 100 * words + n)
+    blocks = []
+    with mpmath.workprec(320):
+        for g in (3, 30, 60):
+            Qf, _ = np.linalg.qr(rng.standard_normal((n, n)))
+            lam = [mpmath.mpf(-0.5), mpmath.mpf(-0.5) + mpmath.ldexp(1, -g)]
+            lam += [mpmath.mpf(-0.4) + mpmath.mpf(0.8) * i / n for i in range(2, n)]
+            Qm = [[mpmath.mpf(float(Qf[i, k])) for k in range(n)] for i in range(n)]
+            B = np.empty((n, n), dtype=object)
+            for i in range(n):
+                for j in range(i + 1):
+                    s = mpmath.fsum(Qm[i][k] * Qm[j][k] * lam[k] for k in range(n))
+                    B[i, j] = B[j, i] = s
+            blocks.append(B)
+        G = rng.standard_normal((n, n))
+        L = rng.standard_normal((n, n)) * 2.0 ** -60
+        B = np.empty((n, n), dtype=object)
+        for i in range(n):
+            for j in range(i + 1):
+                B[i, j] = B[j, i] = mpmath.mpf(float(G[i, j] + G[j, i])) / 4 + mpmath.mpf(float(L[i, j]))
+        blocks.append(B)
+    got = pk.eigmin(blocks, precision_words=words)
+    with mpmath.workprec(320):
+        for q, (B, g) in enumerate(zip(blocks, got)):
+            ref = _mp_eigmin(B)
+            nrm = max(abs(x) for x in B.reshape(-1))
+            err = abs(mpmath.mpf(g) - ref) / nrm
+            assert err <= EIG_TOL[words], (q, float(g), float(ref), float(err))

@@ -1,0 +1,12 @@
+set -o pipefail
+mkdir -p gpurun_out/r4g
+timeout -k 10 120 microbin/eig_mx_bench 64 32 > gpurun_out/r4g/eigmx.log 2>&1; echo "eigmx rc=$?"; cat gpurun_out/r4g/eigmx.log
+timeout -k 10 200 python3 tools/probe_c8.py 8 80 > gpurun_out/r4g/probe_a.log 2>&1; echo "probe rc=$?"; tail -4 gpurun_out/r4g/probe_a.log
+CLRSDP_SLAB_QSOLVE=0 timeout -k 10 200 python3 tools/probe_c8.py 8 80 > gpurun_out/r4g/probe_b.log 2>&1; tail -3 gpurun_out/r4g/probe_b.log
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_steplength.py tests/test_gpu_keywords.py > gpurun_out/r4g/t_eig.log 2>&1; echo "tests rc=$?"; tail -5 gpurun_out/r4g/t_eig.log
+for a in "--config c2 --precision 2" "--config c5 --precision 4"; do
+  for mx in 1 0; do
+    CLRSDP_EIG_MX=$mx timeout -k 10 200 python3 bench.py --no-cpu --steps 100 $a > gpurun_out/r4g/b.log 2>&1 || { echo "bench failed: $a"; tail -5 gpurun_out/r4g/b.log; exit 1; }
+    tail -1 gpurun_out/r4g/b.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("mx='$mx'", d["config"]["workload"][:40], d["dtype"], round(d["value"],1), "it/s")'
+  done
+done
