@@ -603,9 +603,11 @@ struct MatPlan : PlanBase {  // potrf / eigmin
   // falls back to chol_inv_reg with CLRSDP_CHOL_PACKED=0).  Set before finalize();
   // CLRSDP_REG_POTRF=0 keeps potrf_batched.
   bool reg_potrf = false;
+  int* redo = nullptr;  // eigmin_mx's per-block fallback flags
   void finalize() {
     if (h.empty()) return;
     d = own(h);
+    if (!std::is_same<T, double>::value) redo = own(std::vector<int>(h.size(), 1));
     const char* e = std::getenv("CLRSDP_REG_POTRF");
     // (double-double blocks 65..128: chol_packed only, CLRSDP_CHOL_PACKED128=0 keeps
     // potrf_batched there; quad-double would spill at nine slots per thread)
@@ -661,10 +663,15 @@ struct MatPlan : PlanBase {  // potrf / eigmin
     // (eigmin_mx, which falls back to eigmin_lds2's path per block; experimental, off by default)
     static const bool mx = env_on("CLRSDP_EIG_MX");
     if constexpr (!std::is_same<T, double>::value) {
-      if (mx && newton && nmax <= 64 && eigmx_lds_bytes<T>(nmax) <= LDS_MAX) {
-        static std::atomic<unsigned long long> attrm{0};
+      if (mx && newton && redo && nmax <= 64 && eigmx_lds_bytes<T>(nmax) + EIGMX_STATIC_LDS <= LDS_MAX &&
+          eig2_lds_bytes<T>(nmax) <= LDS_MAX && (sizeof(T) <= 16 || nmax <= 64)) {
+        static std::atomic<unsigned long long> attrm{0}, attr2r{0};
         lds_attr_once(attrm, (const void*)eigmin_mx<T>, (int)LDS_MAX);
-        eigmin_mx<T><<<(unsigned)h.size(), 512, eigmx_lds_bytes<T>(nmax), s>>>(d, out);
+        eigmin_mx<T><<<(unsigned)h.size(), 576, eigmx_lds_bytes<T>(nmax), s>>>(d, out, redo);
+        HIPCHK(hipGetLastError());
+        // the flagged blocks (clustered lambda_min) at the full width; the others exit at once
+        lds_attr_once(attr2r, (const void*)eigmin_lds2<T, true>, (int)LDS_MAX);
+        eigmin_lds2<T, true><<<(unsigned)h.size(), 512, eig2_lds_bytes<T>(nmax), s>>>(d, out, redo);
         HIPCHK(hipGetLastError());
         return;
       }
@@ -713,9 +720,11 @@ struct LuPlan : PlanBase {
   }
   size_t lds = 0;
   // (outside any graph capture: the LDS attribute is set here, not at launch)
+  int* redo = nullptr;  // eigmin_mx's per-block fallback flags
   void finalize() {
     if (h.empty()) return;
     d = own(h);
+    if (!std::is_same<T, double>::value) redo = own(std::vector<int>(h.size(), 1));
     lds = getrf_lds_bytes<T, NB>(nmax);
     // the static LDS of the kernel (pivot search, pivots) comes on top of the dynamic panel
     if (lds > LDS_MAX - 4096) throw ClrsdpError{CLRSDP_E_ARG, "LU fallback: matrix too large for the on-chip panel"};

@@ -1839,7 +1839,7 @@ template <class T> size_t eig2_lds_bytes(int n) {
 // The tridiagonalisation loop of eigmin_lds2 on the symmetric image A (n x ld in LDS, n >= 2,
 // 512 threads): dg, e2 (and the last diagonal entry) when it returns.  KEEPV (fp64, eigmin_mx)
 // also keeps every reflector: v_c in column c of V (n x n, rows c+1..n-1), beta_c in bet[c] and
-// the signed off-diagonal T(c+1, c) in eo[c], so that A = Q T Q^T with Q = H_0 H_1 ... H_{n-3}.
+// the signed off-diagonal T(c+1, c) in eo[c], so that A = Q T Q^T with Q = H_0 H_1 ... H_{n-2}.
 template <class T, bool KEEPV>
 __device__ __forceinline__ void tridiag_lds2(T* __restrict__ A, int ld, int n, T* __restrict__ vb,
                                              T* __restrict__ p, T* __restrict__ dg,
@@ -1860,18 +1860,37 @@ __device__ __forceinline__ void tridiag_lds2(T* __restrict__ A, int ld, int n, T
 #pragma unroll
     for (int h = 0; h < NH; ++h) s += x[h] * x[h];
     s = lane0_sum_mw(s, n - c - 1);  // (only lane 0 uses s: beta, v0, e2[c])
-    const T x0 = shfl_t(x[0], 0);  // row c+1
+    const T x0 = x[0];  // row c+1 (lane 0 is the only lane that uses x0, s and tail)
     const T tail = s - x0 * x0;
     T* v = vb + (c & 1) * ld;
     T beta = T(0.0), v0 = x0, e2c = x0 * x0, offd = x0;
     if (tail > T(0.0)) {
       T nrm, rnrm;
-      pivot_sqrt(s, nrm, rnrm);
+      if constexpr (std::is_same<T, double>::value) {  // (eigmin_mx) as eigmin_split's reflector
+        if (s > 0x1p-900) {
+          double rs = __builtin_amdgcn_rsq(s);
+          rs = rs * fma(-0.5 * s, rs * rs, 1.5);
+          nrm = s * rs;
+          nrm = fma(fma(-nrm, nrm, s), 0.5 * rs, nrm);
+        } else {
+          nrm = sqrt(s);
+        }
+      } else {
+        pivot_sqrt(s, nrm, rnrm);
+      }
       const T alpha = sel(x0 > T(0.0), -nrm, nrm);
       v0 = x0 - alpha;
       e2c = alpha * alpha;
       offd = alpha;
-      beta = recip_fast(tail + v0 * v0) * T(2.0);
+      if constexpr (std::is_same<T, double>::value) {
+        const double q = fma(v0, v0, tail);
+        double rc = __builtin_amdgcn_rcp(q);
+        rc = fma(fma(-q, rc, 1.0), rc, rc);
+        rc = fma(fma(-q, rc, 1.0), rc, rc);
+        beta = 2.0 * rc;
+      } else {
+        beta = recip_fast(tail + v0 * v0) * T(2.0);
+      }
     }
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
@@ -2029,10 +2048,13 @@ __device__ __forceinline__ void eigmin_lds2_dev(const MatDesc<T>& d, T* __restri
   eig_multisection<T, NEWTON>(dg, e2, n, A, p, out);
 }
 
+// redo (eigmin_mx's fallback launch): only the blocks with redo[block] != 0
 template <class T, bool NEWTON = true, int DBG = 0>
 __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict__ descs,
-                                                   T* __restrict__ out) {
+                                                   T* __restrict__ out,
+                                                   const int* __restrict__ redo = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if (redo && redo[blockIdx.x] == 0) return;
   eigmin_lds2_dev<T, NEWTON, DBG>(descs[blockIdx.x], out, smem_raw);
 }
 #undef ANY_BELOW
@@ -2057,20 +2079,20 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
 //   5. rho of the final x.  Temple's bound: with ||r||^2 / ||x||^2 = eta and lambda_2 > rho,
 //      rho - eta / (lambda_2 - rho) <= lambda_min <= rho.  rho is accepted when that width is
 //      below 2^-(BITS+2) of the spectrum's magnitude; otherwise (a multiple or tightly
-//      clustered lambda_min, or no separated lambda_2) the workgroup runs eigmin_lds2's
-//      multi-word path on the same block (eigmx_fallbacks counts those).
+//      clustered lambda_min, or no separated lambda_2) the block is flagged and the launch
+//      that follows (eigmin_lds2 with the flags) runs the multi-word path on it alone
+//      (g_eigmx_fallbacks counts those).
 // ------------------------------------------------------------------------------------------
 __device__ unsigned int g_eigmx_fallbacks = 0;
-template <class T> __host__ __device__ constexpr int eigmx_refine() { return sizeof(T) > 16 ? 2 : 1; }
+template <class T> __host__ __device__ constexpr int eigmx_refine() { return sizeof(T) > 16 ? 4 : 3; }
 template <class T> size_t eigmx_own_bytes(int n) {
   const size_t ld = eig2_ld<double>(n), W = sizeof(T) / 8;
-  return 8 * ((size_t)n * ld + 3 * ld + 2 * (size_t)n + 4 + 16 + (size_t)n * n + 2 * (size_t)n +
-              6 * (size_t)n + 64 + 8 + W * (size_t)n + 8 * W * (size_t)n) + 64;
+  return 8 * (128 + (size_t)n * ld + 3 * ld + 2 * (size_t)n + 4 + 16 + (size_t)n * n +
+              2 * (size_t)n + 6 * (size_t)n + 64 + 8 + W * (size_t)n + 8 * W * (size_t)n) + 64;
 }
-template <class T> size_t eigmx_lds_bytes(int n) {
-  const size_t a = eigmx_own_bytes<T>(n), b = eig2_lds_bytes<T>(n);
-  return a > b ? a : b;
-}
+// static LDS of split_tridiag_keepv (rowb, pb, vb, redw, betab, amaxw), on top of the dynamic size
+constexpr size_t EIGMX_STATIC_LDS = 6400;
+template <class T> size_t eigmx_lds_bytes(int n) { return eigmx_own_bytes<T>(n); }
 // Sturm count of the (scaled, |T| < 1) tridiagonal in pivot form, pivots floored at 2^-900
 __device__ __forceinline__ int sturm_count_piv(const double* __restrict__ dg,
                                                const double* __restrict__ e2, int n, double sigma) {
@@ -2086,80 +2108,274 @@ __device__ __forceinline__ int sturm_count_piv(const double* __restrict__ dg,
   }
   return cnt;
 }
-// LU with partial pivoting of the tridiagonal T - lam I (diagonal dg, off-diagonal eo; LAPACK
-// dgttrf's elimination order), one thread, the modified row carried in registers; pivots
-// floored at 2^-900, rfd = the reciprocals of U's diagonal, fpv = 1 where rows i, i+1 swapped.
-__device__ __forceinline__ void tri_lu(const double* __restrict__ dg, const double* __restrict__ eo,
-                                       int n, double lam, double* __restrict__ rfd,
-                                       double* __restrict__ fdu, double* __restrict__ fdu2,
-                                       double* __restrict__ fdl, double* __restrict__ fpv) {
-  constexpr double PIVMIN = 0x1p-900;
-  double di = dg[0] - lam, dui = eo[0];
-#pragma unroll 4
-  for (int i = 0; i + 1 < n; ++i) {
-    const double li = eo[i];
-    const double dn = dg[i + 1] - lam;
-    const double dun = i + 2 < n ? eo[i + 1] : 0.0;
-    if (fabs(di) >= fabs(li)) {
-      if (fabs(di) < PIVMIN) di = PIVMIN;
-      const double r = 1.0 / di, f = li * r;
-      rfd[i] = r;
-      fdu[i] = dui;
-      fdu2[i] = 0.0;
-      fdl[i] = f;
-      fpv[i] = 0.0;
-      di = dn - f * dui;
-      dui = dun;
-    } else {
-      const double r = 1.0 / li, f = di * r;
-      rfd[i] = r;
-      fdu[i] = dn;
-      fdu2[i] = dun;
-      fdl[i] = f;
-      fpv[i] = 1.0;
-      di = dui - f * dn;
-      dui = -f * dun;
-    }
-  }
-  if (fabs(di) < PIVMIN) di = PIVMIN;
-  rfd[n - 1] = 1.0 / di;
+// T - mu I = L D L^T for the (scaled) tridiagonal with mu just below lambda_1, so every pivot is
+// positive in exact arithmetic (floored at 2^-900 against rounding): one thread, the pivot
+// chain in registers, reciprocals by the hardware rcp and two Newton steps.  rd = 1 / D,
+// ll = the subdiagonal of L.
+__device__ __forceinline__ double rcp_nr(double q) {
+  double r = __builtin_amdgcn_rcp(q);
+  r = fma(fma(-q, r, 1.0), r, r);
+  return fma(fma(-q, r, 1.0), r, r);
 }
-// b <- (T - lam I)^-1 b with tri_lu's factors (dgttrs's order), one thread
-__device__ __forceinline__ void tri_solve(const double* __restrict__ rfd,
-                                          const double* __restrict__ fdu,
-                                          const double* __restrict__ fdu2,
-                                          const double* __restrict__ fdl,
-                                          const double* __restrict__ fpv, int n,
-                                          double* __restrict__ b) {
-  double bi = b[0];
-#pragma unroll 4
+__device__ __forceinline__ void tri_ldl(const double* __restrict__ dg, const double* __restrict__ eo,
+                                        int n, double mu, double* __restrict__ rd,
+                                        double* __restrict__ ll) {
+  constexpr double PIVMIN = 0x1p-900;
+  double dcur = dg[0] - mu;
+#pragma unroll 8
   for (int i = 0; i + 1 < n; ++i) {
-    const double bn = b[i + 1], l = fdl[i];
-    if (fpv[i] == 0.0) {
-      b[i] = bi;
-      bi = bn - l * bi;
-    } else {
-      b[i] = bn;
-      bi = bi - l * bn;
+    const double e = eo[i], an = dg[i + 1] - mu;
+    const double r = rcp_nr(fmax(dcur, PIVMIN)), l = e * r;
+    rd[i] = r;
+    ll[i] = l;
+    dcur = fma(-l, e, an);
+  }
+  rd[n - 1] = rcp_nr(fmax(dcur, PIVMIN));
+}
+// b <- (L D L^T)^-1 b, one thread
+__device__ __forceinline__ void tri_ldl_solve(const double* __restrict__ rd,
+                                              const double* __restrict__ ll, int n,
+                                              double* __restrict__ b) {
+  double y = b[0];
+#pragma unroll 8
+  for (int i = 1; i < n; ++i) {
+    y = fma(-ll[i - 1], y, b[i]);
+    b[i] = y;
+  }
+  double x = y * rd[n - 1];
+  b[n - 1] = x;
+#pragma unroll 8
+  for (int i = n - 2; i >= 0; --i) {
+    x = fma(b[i], rd[i], -ll[i] * x);
+    b[i] = x;
+  }
+}
+// eigmin_split's register-resident tridiagonalisation (576 threads: 8 bulk waves holding the
+// matrix, one chain wave building each reflector once) on the fp64 image Ah (n x ld in LDS,
+// n <= 128), keeping the reflectors for eigmin_mx: v_r in column r of V (n x n), beta_r in
+// bet[r], the signed coupling T(r+1, r) in eo[r] and the diagonal in dg.  The image is scaled by
+// 2^-ex0 (its largest entry below 1, as eigmin_split) and T comes out scaled alike; returns ex0.
+// The DBG knobs and stamps of eigmin_split are left out; the arithmetic is the same.
+__device__ __forceinline__ int split_tridiag_keepv(const double* __restrict__ Ah, int ld, int n,
+                                                   double* __restrict__ dg, double* __restrict__ V,
+                                                   double* __restrict__ bet,
+                                                   double* __restrict__ eo) {
+  constexpr int NS = 16, NWB = 8, GS = 4;
+  __shared__ __attribute__((aligned(16))) double rowb[2][128];
+  __shared__ __attribute__((aligned(16))) double pb[2][128];
+  __shared__ __attribute__((aligned(16))) double vb[2][128];
+  __shared__ __attribute__((aligned(16))) double redw[2][NWB];
+  __shared__ double betab[2];
+  __shared__ double amaxw[NWB];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const bool chain = w == NWB;
+  const int blk = w < 4 ? w : 11 - w;
+  const int c = lane >> 4, t16 = lane & 15;
+  const int i = blk * 16 + t16;
+  const int j0 = 2 * c + 8 * t16;
+  double a[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) a[s][0] = a[s][1] = 0.0;
+  if (!chain) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * c + 8 * s + e;
+        const int ic = min(i, n - 1), jc = min(j, n - 1);
+        const double v = Ah[ic + (size_t)jc * ld];
+        a[s][e] = (i < n && j < n) ? v : 0.0;
+      }
+    double amax = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) amax = fmax(amax, fmax(fabs(a[s][0]), fabs(a[s][1])));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
+    if (lane == 0) amaxw[w] = amax;
+  }
+  __syncthreads();
+  int ex0;
+  {
+    double amax = amaxw[0];
+#pragma unroll
+    for (int r = 1; r < NWB; ++r) amax = fmax(amax, amaxw[r]);
+    ex0 = (amax > 0.0 && amax < INFINITY) ? __builtin_amdgcn_frexp_exp(amax) : 0;
+  }
+  if (!chain) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      a[s][0] = __builtin_ldexp(a[s][0], -ex0);
+      a[s][1] = __builtin_ldexp(a[s][1], -ex0);
     }
   }
-  double x1 = bi * rfd[n - 1], x2 = 0.0;
-  b[n - 1] = x1;
-#pragma unroll 4
-  for (int i = n - 2; i >= 0; --i) {
-    const double x = (b[i] - fdu[i] * x1 - fdu2[i] * x2) * rfd[i];
-    b[i] = x;
-    x2 = x1;
-    x1 = x;
+  auto publish_row = [&](int r, double* dst) {
+    if (!chain && blk == (r >> 4) && t16 == (r & 15)) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        *reinterpret_cast<double2*>(dst + 2 * c + 8 * s) = make_double2(a[s][0], a[s][1]);
+    }
+  };
+  double cx = 0.0, cy = 0.0, beta = 0.0, vi = 0.0;
+  auto reflector = [&](int r, double xj0, double xj1, double xr, double x0) {
+    double tl = (j0 >= r + 2 ? xj0 * xj0 : 0.0);
+    tl = fma(j0 + 1 >= r + 2 ? xj1 : 0.0, xj1, tl);
+    tl = xsum32(xsum16(row16_sum(tl)));
+    double bt = 0.0, v0 = x0, offd = x0;
+    if (tl > 0.0) {
+      const double ss = fma(x0, x0, tl);
+      double nrm;
+      if (ss > 0x1p-900) {
+        double rs = __builtin_amdgcn_rsq(ss);
+        rs = rs * fma(-0.5 * ss, rs * rs, 1.5);
+        nrm = ss * rs;
+        nrm = fma(fma(-nrm, nrm, ss), 0.5 * rs, nrm);
+      } else {
+        nrm = sqrt(ss);
+      }
+      const double alpha = x0 > 0.0 ? -nrm : nrm;
+      v0 = x0 - alpha;
+      const double q = fma(v0, v0, tl);
+      double rc = __builtin_amdgcn_rcp(q);
+      rc = fma(fma(-q, rc, 1.0), rc, rc);
+      rc = fma(fma(-q, rc, 1.0), rc, rc);
+      bt = 2.0 * rc;
+      offd = alpha;
+    }
+    cx = j0 <= r ? 0.0 : (j0 == r + 1 ? v0 : xj0);
+    cy = j0 + 1 <= r ? 0.0 : (j0 + 1 == r + 1 ? v0 : xj1);
+    beta = bt;
+    *reinterpret_cast<double2*>(&vb[r & 1][j0]) = make_double2(cx, cy);
+    if (j0 < n) V[j0 + (size_t)r * n] = cx;
+    if (j0 + 1 < n) V[j0 + 1 + (size_t)r * n] = cy;
+    if (lane == 0) {
+      dg[r] = xr;
+      betab[r & 1] = bt;
+      bet[r] = bt;
+      eo[r] = offd;
+    }
+  };
+  publish_row(0, rowb[0]);
+  publish_row(1, rowb[1]);
+  __syncthreads();
+  if (chain) {
+    __builtin_amdgcn_s_setprio(3);
+    const double2 xr = *reinterpret_cast<const double2*>(&rowb[0][j0]);
+    reflector(0, xr.x, xr.y, rowb[0][0], rowb[0][1]);
   }
+  __syncthreads();
+  if (!chain) {
+    const double2 v2 = *reinterpret_cast<const double2*>(&vb[0][j0]);
+    cx = v2.x;
+    cy = v2.y;
+    vi = vb[0][i];
+    beta = betab[0];
+  }
+  for (int k = 0; k + 2 < n; ++k) {
+    const int lo = (k + 1) >> 3;
+    const int r = k + 1;
+    double pp = 0.0;
+    if (!chain) {
+      const bool live = blk * 16 + 15 > k && blk * 16 < n;
+      double pa[4] = {0.0, 0.0, 0.0, 0.0};
+      if (live) {
+        static_for<0, NS / GS>([&](auto G) {
+          constexpr int g = decltype(G)::value;
+          if (GS * g + GS - 1 >= lo) {
+            static_for<GS * g, GS * g + GS>([&](auto S) {
+              constexpr int s = decltype(S)::value;
+              fmac_bcast<s, s == GS * g>(pa[2 * (s & 1)], cx, a[s][0]);
+              fmac_bcast<s, false>(pa[2 * (s & 1) + 1], cy, a[s][1]);
+            });
+          }
+        });
+      }
+      pp = xsum32(xsum16((pa[0] + pa[1]) + (pa[2] + pa[3])));
+      double t = 0.0;
+      if (c == 0) {
+        pb[k & 1][i] = i > k ? pp : 0.0;
+        t = vi * pp;
+      }
+      t = row16_sum(t);
+      if (lane == 0) redw[k & 1][w] = t;
+    }
+    __syncthreads();
+    if (chain) {
+      double rw[NWB];
+#pragma unroll
+      for (int q = 0; q < NWB; q += 2) {
+        const double2 v2 = *reinterpret_cast<const double2*>(&redw[k & 1][q]);
+        rw[q] = v2.x;
+        rw[q + 1] = v2.y;
+      }
+      const double* old = rowb[r & 1];
+      const double2 pj = *reinterpret_cast<const double2*>(&pb[k & 1][j0]);
+      const double2 o = *reinterpret_cast<const double2*>(old + j0);
+      const double orr = old[r], or1 = old[r + 1];
+      const double vr = vb[k & 1][r], vr1 = vb[k & 1][r + 1];
+      const double pr = pb[k & 1][r], pr1 = pb[k & 1][r + 1];
+      const double tot = ((rw[0] + rw[1]) + (rw[2] + rw[3])) + ((rw[4] + rw[5]) + (rw[6] + rw[7]));
+      const double Kc = beta * beta * tot * 0.5;
+      const double wr = fma(beta, pr, -(Kc * vr));
+      const double gr = fma(Kc, vr, -wr), mhr = -(beta * vr);
+      const double xj0 = fma(cx, gr, fma(pj.x, mhr, o.x));
+      const double xj1 = fma(cy, gr, fma(pj.y, mhr, o.y));
+      const double xr = fma(vr, gr, fma(pr, mhr, orr));
+      const double x0 = fma(vr1, gr, fma(pr1, mhr, or1));
+      reflector(r, xj0, xj1, xr, x0);
+    } else if (blk * 16 + 15 > k + 1 && blk * 16 < n) {
+      double rw[NWB];
+#pragma unroll
+      for (int q = 0; q < NWB; q += 2) {
+        const double2 v2 = *reinterpret_cast<const double2*>(&redw[k & 1][q]);
+        rw[q] = v2.x;
+        rw[q + 1] = v2.y;
+      }
+      const double2 pv = *reinterpret_cast<const double2*>(&pb[k & 1][j0]);
+      const double tot = ((rw[0] + rw[1]) + (rw[2] + rw[3])) + ((rw[4] + rw[5]) + (rw[6] + rw[7]));
+      const double Kc = beta * beta * tot * 0.5;
+      const double wi = fma(beta, pp, -(Kc * vi));
+      const double gi = fma(Kc, vi, -wi), mhi = -(beta * vi);
+      static_for<0, NS / GS>([&](auto G) {
+        constexpr int g = decltype(G)::value;
+        if (GS * g + GS - 1 >= lo) {
+          static_for<GS * g, GS * g + GS>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            fmac_bcast<s, s == GS * g>(a[s][0], pv.x, mhi);
+            fmac_bcast<s, false>(a[s][1], pv.y, mhi);
+          });
+          static_for<GS * g, GS * g + GS>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            fmac_bcast<s, false>(a[s][0], cx, gi);
+            fmac_bcast<s, false>(a[s][1], cy, gi);
+          });
+        }
+      });
+      publish_row(k + 2, rowb[k & 1]);
+    }
+    __syncthreads();
+    if (!chain) {
+      const double2 v2 = *reinterpret_cast<const double2*>(&vb[r & 1][j0]);
+      cx = v2.x;
+      cy = v2.y;
+      vi = vb[r & 1][i];
+      beta = betab[r & 1];
+    }
+  }
+  if (chain) __builtin_amdgcn_s_setprio(0);
+  if (tid == 0) dg[n - 1] = rowb[(n - 1) & 1][n - 1];
+  __syncthreads();
+  return ex0;
 }
 // DBG: per-block diagnostics and phase stamps (s_memtime) in g_eigmx_dbg[block * 24 + slot]
 __device__ double g_eigmx_dbg[256 * 24];
 // DBG 2: block 0's fp64 data for a host check (V n x n, then dg, eo, bet, z, x, r, s, d', d by n)
 __device__ double g_eigmx_dump[64 * 64 + 12 * 64];
-template <class T, int DBG = 0>
-__global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ descs,
-                                                 T* __restrict__ out) {
+// TRI = 1: the register-resident tridiagonalisation (split_tridiag_keepv, 576 threads; the
+// ninth wave only builds reflectors), TRI = 0: tridiag_lds2 on 512 threads
+template <class T, int DBG = 0, int TRI = 1>
+__global__ __launch_bounds__(TRI ? 576 : 512) void eigmin_mx(const MatDesc<T>* __restrict__ descs,
+                                                             T* __restrict__ out,
+                                                             int* __restrict__ redo) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   constexpr int NT = 512, NW = 8, R = eigmx_refine<T>();
   const MatDesc<T> d = descs[blockIdx.x];
@@ -2168,7 +2384,7 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
   unsigned long long t_prev = DBG ? __builtin_amdgcn_s_memtime() : 0ull;
   auto stamp = [&](int slot) {
     if constexpr (DBG != 0) {
-      if (tid == 0) {
+      if (tid == 0 && slot < 16) {
         const unsigned long long t = __builtin_amdgcn_s_memtime();
         dbg[slot] = (double)(t - t_prev);
         t_prev = t;
@@ -2178,8 +2394,10 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
   bool ok = n >= 3;
   if (ok) {
     const int ld = eig2_ld<double>(n);
-    double* A = reinterpret_cast<double*>(smem_raw);  // n x ld
-    double* vb = A + (size_t)n * ld;                  // 2 x ld
+    double* sd = reinterpret_cast<double*>(smem_raw);  // 64 padded diagonal for the counts
+    double* se = sd + 64;                              // 64 padded squared couplings
+    double* A = se + 64;                               // n x ld
+    double* vb = A + (size_t)n * ld;                   // 2 x ld
     double* p = vb + 2 * ld;                           // ld
     double* dg = p + ld;                               // n
     double* e2 = dg + n;                               // n
@@ -2188,18 +2406,15 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
     double* V = redw + 16;                             // n x n reflectors
     double* bet = V + (size_t)n * n;                   // n
     double* eo = bet + n;                              // n signed off-diagonal
-    double* rfd = eo + n;                              // n  1 / U's diagonal
-    double* fdu = rfd + n;                             // n  U first superdiagonal
-    double* fdu2 = fdu + n;                            // n  U second superdiagonal
-    double* fdl = fdu2 + n;                            // n  L multipliers
-    double* fpv = fdl + n;                             // n  interchange flags
-    double* wv = fpv + n;                              // n  right-hand side / solution
+    double* rd = eo + n;                               // n  1 / D of T - mu I = L D L^T
+    double* ll = rd + n;                               // n  L's subdiagonal
+    double* wv = ll + 4 * n;                           // n  right-hand side / solution
     double* sc = wv + n;                               // 64 scalars
     unsigned long long* masks = reinterpret_cast<unsigned long long*>(sc + 64);  // 8
     T* xv = reinterpret_cast<T*>(masks + 8);           // n   the eigenvector estimate
     T* part = xv + n;                                  // 8 x n  row partials of A_s x
     // (1) leading words of the symmetrised block, then the fp64 tridiagonalisation
-    for (int j = w; j < n; j += NW)
+    for (int j = w; j < n && w < NW; j += NW)
       for (int i = lane; i < n; i += 64) {
         if (i < j) continue;
         const T s = (d.A[i + (size_t)j * d.lda] + d.A[j + (size_t)i * d.lda]) * T(0.5);
@@ -2208,7 +2423,14 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
       }
     __syncthreads();
     stamp(0);
-    tridiag_lds2<double, true>(A, ld, n, vb, p, dg, e2, scal, redw, V, bet, eo);
+    int ex0 = 0;  // (TRI 1: T comes out scaled by 2^-ex0)
+    if constexpr (TRI == 1) {
+      ex0 = split_tridiag_keepv(A, ld, n, dg, V, bet, eo);
+      for (int i = tid; i + 1 < n; i += NT) e2[i] = eo[i] * eo[i];
+      __syncthreads();
+    } else {
+      tridiag_lds2<double, true>(A, ld, n, vb, p, dg, e2, scal, redw, V, bet, eo);
+    }
     stamp(1);
     // Gershgorin bracket of T and the power of two that scales it below 1
     if (tid == 0) {
@@ -2224,6 +2446,7 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
       const int ex = fin ? __builtin_amdgcn_frexp_exp(mag) : 0;
       sc[0] = fin ? 1.0 : 0.0;
       sc[1] = (double)ex;
+      sc[6] = (double)(ex + ex0);  // A's units -> the scaled T's
       const double span = ldexp(ghi - glo, -ex);
       sc[2] = ldexp(glo, -ex) - span * 1e-3 - 1e-300;
       sc[3] = ldexp(ghi, -ex) + span * 1e-3 + 1e-300;
@@ -2239,8 +2462,8 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
       }
       __syncthreads();
       auto first_hit = [&](bool hit) -> int {
-        const unsigned long long mk = __ballot(hit);
-        if (lane == 0) masks[w] = mk;
+        const unsigned long long mk = __ballot(hit && tid < NT);
+        if (lane == 0 && w < NW) masks[w] = mk;
         __syncthreads();
         int f = -1;
         for (int q = 0; q < NW && f < 0; ++q)
@@ -2248,11 +2471,18 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
         __syncthreads();
         return f;
       };
-      // (2) lambda of T: 6 rounds of 512 division-free counts (54 bits of the span)
+      // (2) lambda of T: eigmin_split's multisection (the padded fp64 arrays, 512-way on all 8
+      // waves, 6 rounds of 9 bits = 2^-54 of the span)
+      const int nr = (n + 7) & ~7;
+      if (tid < nr) {
+        sd[tid] = tid < n ? dg[tid] : 4.0;
+        se[tid] = (tid >= 1 && tid < n) ? fmax(e2[tid - 1], 0x1p-900) : 0.0;
+      }
+      __syncthreads();
       double lo = sc[2], hi = sc[3];
       for (int it = 0; it < 6; ++it) {
         const double width = hi - lo;
-        const bool hit = sturm_any_below_mw<double>(dg, e2, n, lo + width * ((double)(tid + 1) / 513.0));
+        const bool hit = sturm_any_below(sd, se, nr, lo + width * ((double)(tid + 1) / 513.0));
         const int f = first_hit(hit);
         if (f < 0) {
           lo = lo + width * (512.0 / 513.0);
@@ -2262,34 +2492,36 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
         }
       }
       const double lam = 0.5 * (lo + hi), span = sc[3] - sc[2];
-      // lower bound of lambda_2: the largest lam + span 2^(-t/8) with at most one eigenvalue below
-      const double gt = span * exp2(-(double)tid * 0.125);
-      const int f2 = first_hit(sturm_count_piv(dg, e2, n, lam + gt) <= 1);
+      // lower bound of lambda_2: the largest lam + span 2^(-t/4) (t < 256) with at most one
+      // eigenvalue below it
+      bool le1 = false;
+      if (tid < 256) le1 = sturm_count_piv(dg, e2, n, lam + span * exp2(-(double)tid * 0.25)) <= 1;
+      const int f2 = first_hit(le1);
       // the fp64 tridiagonal is within ~n eps64 |T| of A_s (backward stable, plus the rounding
       // of A_s to its leading words): a margin of 2^-40 of the scaled magnitude
-      const double lam2 = f2 < 0 ? -INFINITY : lam + span * exp2(-(double)f2 * 0.125) - 0x1p-40;
+      const double lam2 = f2 < 0 ? -INFINITY : lam + span * exp2(-(double)f2 * 0.25) - 0x1p-40;
       stamp(2);
-      // (3) LU of T - lam I and two inverse-iteration solves from the all-ones vector (thread 0)
+      // (3) L D L^T of T - mu I, mu = lambda - 2^-48 span (below lambda_1: the bracket is 2^-54
+      // span wide), and two inverse-iteration solves from the all-ones vector (thread 0; each
+      // solve grows the vector by at most ~2^48, so no rescaling in between)
+      const double mu = lam - span * 0x1p-48;
       if (tid == 0) {
-        tri_lu(dg, eo, n, lam, rfd, fdu, fdu2, fdl, fpv);
+        tri_ldl(dg, eo, n, mu, rd, ll);
         for (int i = 0; i < n; ++i) wv[i] = 1.0;
-        for (int rep = 0; rep < 2; ++rep) {
-          tri_solve(rfd, fdu, fdu2, fdl, fpv, n, wv);
-          double mx = 0.0;
-          for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(wv[i]));
-          const double s = mx > 0.0 && mx < INFINITY ? 1.0 / mx : 0.0;
-          for (int i = 0; i < n; ++i) wv[i] *= s;
-        }
+        tri_ldl_solve(rd, ll, n, wv);
+        tri_ldl_solve(rd, ll, n, wv);
       }
       __syncthreads();
       stamp(3);
       // (3') wave 0: z = wv / ||wv||, x = Q z (reflectors n-3 .. 0), x / ||x||
       double zl = 0.0;  // (wave 0, lane l < n: z_l; kept in the register for the projections)
-      // x <- Q x (H_{n-3} first) or Q^T x (H_0 first), lane l holding x_l: the next reflector's
-      // entry is loaded ahead of the current one's wave sum
+      // x <- Q x (H_{n-2} first) or Q^T x (H_0 first), lane l holding x_l: the next reflector's
+      // entry is loaded ahead of the current one's wave sum.  (The last "reflector" H_{n-2} acts
+      // on one entry: it is the identity unless the contracted tail s - x0^2 came out positive,
+      // in which case it flips the sign of row n-1 and T's last coupling is -x0.)
       auto apply_q = [&](double xl, bool transpose) -> double {
-        const int m = n - 2, dk = transpose ? 1 : -1;
-        int k = transpose ? 0 : n - 3;
+        const int m = n - 1, dk = transpose ? 1 : -1;
+        int k = transpose ? 0 : n - 2;
         double vk = lane > k && lane < n ? V[lane + (size_t)k * n] : 0.0, bk = bet[k];
         for (int s = 0; s < m; ++s) {
           const int kn = k + dk;
@@ -2308,6 +2540,10 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
       };
       if (w == 0) {
         double zz = lane < n ? wv[lane] : 0.0;
+        double mz = fabs(zz);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mz = fmax(mz, __shfl_xor(mz, o));
+        zz = mz > 0.0 && mz < INFINITY ? zz / mz : 0.0;
         const double nz = sqrt(wave_sum_mw<double>(zz * zz));
         zl = nz > 0.0 ? zz / nz : 0.0;
         double xl = apply_q(zl, false);
@@ -2323,7 +2559,7 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
             dm[3 * n + lane] = zl;
             dm[4 * n + lane] = xl;
             for (int k = 0; k < n; ++k) g_eigmx_dump[lane + (size_t)k * n] = V[lane + (size_t)k * n];
-            if (lane == 0) { dm[10 * n] = lam; dm[10 * n + 1] = sc[1]; }
+            if (lane == 0) { dm[10 * n] = mu; dm[10 * n + 1] = sc[6]; }
           }
         }
         if (lane == 0) sc[4] = nz > 0.0 && nx > 0.0 ? 1.0 : 0.0;
@@ -2331,10 +2567,11 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
       __syncthreads();
       stamp(4);
       ok = sc[4] != 0.0;
-      // (4) R refinement steps, then (5) the accepted Rayleigh quotient
+      // (4)-(5) Rayleigh quotient and residual of x; accepted as soon as Temple's width is below
+      // 2^-(BITS+2) of |T| < 1, else a refinement step (at most R: 3 at dd, 4 at qd)
       for (int it = 0; ok && it <= R; ++it) {
         // row partials of y = A_s x: row lane, columns j = w (mod 8)
-        if (lane < n) {
+        if (lane < n && w < NW) {
           T acc = T(0.0);
           for (int j = w; j < n; j += NW) {
             const T s = (d.A[lane + (size_t)j * d.lda] + d.A[j + (size_t)lane * d.lda]) * T(0.5);
@@ -2354,26 +2591,25 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
           const T num = wave_sum_mw<T>(xl * y), den = wave_sum_mw<T>(xl * xl);
           const T rho = num / den;
           const T rr = y - rho * xl;
-          const double rh = ldexp(Num<T>::hi(rr), -(int)sc[1]);  // scaled residual
+          const double rh = ldexp(Num<T>::hi(rr), -(int)sc[6]);  // scaled residual
           const double eta = wave_sum_mw<double>(rh * rh) / Num<T>::hi(den);
           if constexpr (DBG != 0) {
-            if (lane == 0) dbg[16 + it] = eta;
+            if (lane == 0 && it < 4) dbg[16 + it] = eta;
           }
-          if (it == R) {
-            const double rhs = ldexp(Num<T>::hi(rho), -(int)sc[1]);
-            const double tw = lam2 > rhs ? eta / (lam2 - rhs) : INFINITY;
-            const bool acc = tw <= 0x1p-3 * Num<T>::eps();  // 2^-(BITS+2) of |T| < 1
-            if (lane == 0) {
-              sc[5] = acc ? 1.0 : 0.0;
-              if (acc) out[blockIdx.x] = rho;
-              if constexpr (DBG != 0) {
-                dbg[20] = lam;
-                dbg[21] = lam2;
-                dbg[22] = rhs;
-                dbg[23] = tw;
-              }
+          const double rhs = ldexp(Num<T>::hi(rho), -(int)sc[6]);
+          const double tw = lam2 > rhs ? eta / (lam2 - rhs) : INFINITY;
+          const bool acc = tw <= 0x1p-3 * Num<T>::eps();  // 2^-(BITS+2) of |T| < 1
+          if (lane == 0) {
+            sc[5] = acc ? 1.0 : (it == R ? -1.0 : 0.0);  // accepted / rejected / refine
+            if (acc) out[blockIdx.x] = rho;
+            if constexpr (DBG != 0) {
+              dbg[20] = lam;
+              dbg[21] = lam2;
+              dbg[22] = rhs;
+              dbg[23] = tw;
             }
-          } else {
+          }
+          if (!acc && it < R) {
             // s = P Q^T (-r) in fp64 (scaled) -> wv for the solve
             double s = apply_q(-rh, true);
             s -= wave_sum_mw<double>(zl * s) * zl;
@@ -2388,11 +2624,11 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
           }
         }
         __syncthreads();
-        if (it == R) {
-          ok = sc[5] != 0.0;
+        if (sc[5] != 0.0) {
+          ok = sc[5] > 0.0;
           break;
         }
-        if (tid == 0) tri_solve(rfd, fdu, fdu2, fdl, fpv, n, wv);  // (T - lam I) d' = s
+        if (tid == 0) tri_ldl_solve(rd, ll, n, wv);  // (T - mu I) d' = s
         __syncthreads();
         stamp(6 + 3 * it);
         if (w == 0) {  // x += Q P d' (unscaled: the residual was scaled by 2^-ex)
@@ -2413,11 +2649,12 @@ __global__ __launch_bounds__(512) void eigmin_mx(const MatDesc<T>* __restrict__ 
       }
     }
   }
-  if (ok) return;
-  // the multi-word path on this block (a clustered lambda_min, or n < 3)
-  if (tid == 0 && n >= 3) atomicAdd(&g_eigmx_fallbacks, 1u);
-  __syncthreads();
-  eigmin_lds2_dev<T, true, 0>(d, out, smem_raw);
+  // redo[block] = 1: the multi-word path (eigmin_lds2, the next launch) takes this block (a
+  // clustered lambda_min, or n < 3)
+  if (tid == 0) {
+    redo[blockIdx.x] = ok ? 0 : 1;
+    if (!ok && n >= 3) atomicAdd(&g_eigmx_fallbacks, 1u);
+  }
 }
 
 }  // namespace clrsdp

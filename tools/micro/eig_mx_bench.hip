@@ -93,6 +93,8 @@ void run(const char* name, int n, int nb, int family, int gexp) {
     }
   }
   T *dA, *dE;
+  int* redo;
+  CK(hipMalloc(&redo, nb * sizeof(int)));
   CK(hipMalloc(&dA, ht.size() * sizeof(T)));
   CK(hipMalloc(&dE, 2 * nb * sizeof(T)));
   CK(hipMemcpy(dA, ht.data(), ht.size() * sizeof(T), hipMemcpyHostToDevice));
@@ -107,16 +109,26 @@ void run(const char* name, int n, int nb, int family, int gexp) {
   const float t2 = timeit([&] { eigmin_lds2<T, true, 0><<<nb, 512, l2>>>(dd_, dE); });
   unsigned zero = 0, fb = 0;
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_eigmx_fallbacks), &zero, sizeof(zero)));
-  eigmin_mx<T><<<nb, 512, lm>>>(dd_, dE + nb);
+  eigmin_mx<T><<<nb, 576, lm>>>(dd_, dE + nb, redo);
+  eigmin_lds2<T, true, 0><<<nb, 512, l2>>>(dd_, dE + nb, redo);
   CK(hipDeviceSynchronize());
   CK(hipMemcpyFromSymbol(&fb, HIP_SYMBOL(g_eigmx_fallbacks), sizeof(fb)));
-  const float tm = timeit([&] { eigmin_mx<T><<<nb, 512, lm>>>(dd_, dE + nb); });
+  const float tm = timeit([&] {
+    eigmin_mx<T><<<nb, 576, lm>>>(dd_, dE + nb, redo);
+    eigmin_lds2<T, true, 0><<<nb, 512, l2>>>(dd_, dE + nb, redo);
+  });
+  CK(hipFuncSetAttribute((const void*)eigmin_mx<T, 0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  const float tl = timeit([&] {
+    eigmin_mx<T, 0, 0><<<nb, 512, lm>>>(dd_, dE + nb, redo);
+    eigmin_lds2<T, true, 0><<<nb, 512, l2>>>(dd_, dE + nb, redo);
+  });
   // diagnostics of the DBG instance: phase stamps (s_memtime ticks) averaged over the
   // blocks, and eta / lambda / lambda_2 / rho / Temple width of the first rejected blocks
   CK(hipFuncSetAttribute((const void*)eigmin_mx<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   std::vector<double> dz(256 * 24, 0.0);
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_eigmx_dbg), dz.data(), dz.size() * sizeof(double)));
-  eigmin_mx<T, 1><<<nb, 512, lm>>>(dd_, dE + nb);
+  eigmin_mx<T, 1><<<nb, 576, lm>>>(dd_, dE + nb, redo);
+  eigmin_lds2<T, true, 0><<<nb, 512, l2>>>(dd_, dE + nb, redo);
   CK(hipDeviceSynchronize());
   CK(hipMemcpyFromSymbol(dz.data(), HIP_SYMBOL(g_eigmx_dbg), dz.size() * sizeof(double)));
   {
@@ -143,12 +155,13 @@ void run(const char* name, int n, int nb, int family, int gexp) {
     const T df = ev[b] - ev[nb + b];
     md = fmax(md, fabs(Num<T>::hi(df)));
   }
-  printf("%s n=%d batch=%d family=%d gap=2^-%d: eigmin_lds2 %.1f us, eigmin_mx %.1f us, "
+  printf("%s n=%d batch=%d family=%d gap=2^-%d: eigmin_lds2 %.1f us, eigmin_mx %.1f us (LDS tridiagonalisation %.1f us), "
          "max |diff| %.2e, fallbacks %u/%d, lambda_min[0] %.17g\n",
-         name, n, nb, family, gexp, t2, tm, md, fb, nb, Num<T>::hi(ev[nb]));
+         name, n, nb, family, gexp, t2, tm, tl, md, fb, nb, Num<T>::hi(ev[nb]));
   CK(hipFree(dA));
   CK(hipFree(dE));
   CK(hipFree(dd_));
+  CK(hipFree(redo));
 }
 
 int main(int argc, char** argv) {
@@ -158,8 +171,8 @@ int main(int argc, char** argv) {
   run<dd>("dd", n, nb, 1, 30);
   run<dd>("dd", n, nb, 1, 45);
   run<dd>("dd", n, nb, 2, 0);
-  run<qd>("qd", n, nb, 0, 0);
-  run<qd>("qd", n, nb, 1, 20);
+  run<qd>("qd", 48, nb, 0, 0);
+  run<qd>("qd", 48, nb, 1, 20);
   run<qd>("qd", 18, 22, 0, 0);
   return 0;
 }

@@ -26,6 +26,8 @@ static void run(int n) {
       Ah[i + (size_t)j * n] = Ah[j + (size_t)i * n] = v;
     }
   dd *dA, *dE;
+  int* redo;
+  CK(hipMalloc(&redo, sizeof(int)));
   CK(hipMalloc(&dA, A.size() * sizeof(dd)));
   CK(hipMalloc(&dE, sizeof(dd)));
   CK(hipMemcpy(dA, A.data(), A.size() * sizeof(dd), hipMemcpyHostToDevice));
@@ -33,7 +35,7 @@ static void run(int n) {
   CK(hipMalloc(&dd_, sizeof(h)));
   CK(hipMemcpy(dd_, &h, sizeof(h), hipMemcpyHostToDevice));
   CK(hipFuncSetAttribute((const void*)eigmin_mx<dd, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  eigmin_mx<dd, 2><<<1, 512, eigmx_lds_bytes<dd>(n)>>>(dd_, dE);
+  eigmin_mx<dd, 2><<<1, 576, eigmx_lds_bytes<dd>(n)>>>(dd_, dE, redo);
   CK(hipDeviceSynchronize());
   std::vector<double> dm(64 * 64 + 12 * 64);
   CK(hipMemcpyFromSymbol(dm.data(), HIP_SYMBOL(g_eigmx_dump), dm.size() * sizeof(double)));
@@ -41,12 +43,12 @@ static void run(int n) {
   const double* X = dm.data() + (size_t)n * n;
   const double *dg = X, *eo = X + n, *bet = X + 2 * n, *z = X + 3 * n, *x = X + 4 * n, *rh = X + 5 * n,
                *s = X + 6 * n, *dp = X + 7 * n, *d = X + 8 * n;
-  const double lam = X[10 * n];
+  const double lam = X[10 * n];  // (the LDL shift mu)
   const int ex = (int)X[10 * n + 1];
-  // Q explicitly: Q = H_0 ... H_{n-3}, applied to the identity from the right end
+  // Q explicitly: Q = H_0 ... H_{n-2}, applied to the identity from the right end
   std::vector<LD> Q((size_t)n * n, 0.0L);
   for (int i = 0; i < n; ++i) Q[i + (size_t)i * n] = 1.0L;
-  for (int k = n - 3; k >= 0; --k)  // Q <- H_k Q
+  for (int k = n - 2; k >= 0; --k)  // Q <- H_k Q
     for (int c = 0; c < n; ++c) {
       LD t = 0;
       for (int i = k + 1; i < n; ++i) t += (LD)V[i + (size_t)k * n] * Q[i + (size_t)c * n];
@@ -76,6 +78,10 @@ static void run(int n) {
       for (int i = k + 2; i < n; ++i) ez0 = fmax(ez0, fabs((double)M[i + (size_t)k * n]));
       const double dd0 = fabs((double)M[k + (size_t)k * n] - ldexp(dg[k], ex));
       const double de0 = fabs((double)fabsl(M[k + 1 + (size_t)k * n]) - fabs(ldexp(eo[k], ex)));
+      if (fabs((double)M[k + 1 + (size_t)k * n] - ldexp(eo[k], ex)) > 1e-12 && shown < 3) {
+        ++shown;
+        printf("  step %d: signed subdiag %.17g against eo %.17g\n", k, (double)M[k + 1 + (size_t)k * n], ldexp(eo[k], ex));
+      }
       if (ez0 > 1e-12 || dd0 > 1e-12 || de0 > 1e-12) {
         ++shown;
         printf("  step %d: below-subdiag %.2e, diag err %.2e, |subdiag| err %.2e (sub %.6g eo %.6g) bet %.6g v[k+1] %.6g\n",
@@ -85,6 +91,8 @@ static void run(int n) {
   }
   // T' = Q^T A_h Q against the tridiagonal (unscaled)
   double et = 0.0, at = 0.0;
+  int ei = -1, ej = -1;
+  double etv = 0.0, erf = 0.0;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) {
       LD t = 0;
@@ -94,9 +102,11 @@ static void run(int n) {
       if (i == j) ref = ldexp(dg[i], ex);
       else if (i == j + 1) ref = ldexp(eo[j], ex);
       else if (j == i + 1) ref = ldexp(eo[i], ex);
+      if (fabs((double)t - ref) > et) { ei = i; ej = j; etv = (double)t; erf = ref; }
       et = fmax(et, fabs((double)t - ref));
       at = fmax(at, fabs((double)t));
     }
+  printf("  max |Q^T A Q - T| at (%d, %d): %.17g against %.17g\n", ei, ej, etv, erf);
   // (T_s - lam) z
   double ez = 0.0;
   for (int i = 0; i < n; ++i) {
