@@ -659,15 +659,25 @@ struct MatPlan : PlanBase {  // potrf / eigmin
       const char* e = std::getenv("CLRSDP_EIG_NEWTON");
       return !(e && e[0] == '0');
     }();
-    // multi-word, n <= 64, with CLRSDP_EIG_MX=1: an fp64 eigenpair refined at the word's width
-    // (eigmin_mx, which falls back to eigmin_lds2's path per block; experimental, off by default)
-    static const bool mx = env_on("CLRSDP_EIG_MX");
+    // multi-word, n <= 64: an fp64 eigenpair refined at the word's width (eigmin_mx; the blocks
+    // it cannot certify go to eigmin_lds2 in a second, flagged launch) unless CLRSDP_EIG_MX=0
+    static const bool mx = [] {
+      const char* e = std::getenv("CLRSDP_EIG_MX");
+      return !(e && e[0] == '0');
+    }();
     if constexpr (!std::is_same<T, double>::value) {
       if (mx && newton && redo && nmax <= 64 && eigmx_lds_bytes<T>(nmax) + EIGMX_STATIC_LDS <= LDS_MAX &&
           eig2_lds_bytes<T>(nmax) <= LDS_MAX && (sizeof(T) <= 16 || nmax <= 64)) {
         static std::atomic<unsigned long long> attrm{0}, attr2r{0};
-        lds_attr_once(attrm, (const void*)eigmin_mx<T>, (int)LDS_MAX);
-        eigmin_mx<T><<<(unsigned)h.size(), 576, eigmx_lds_bytes<T>(nmax), s>>>(d, out, redo);
+        static const bool dbg = env_on("CLRSDP_EIGMX_STATS");
+        if (dbg) {  // (the diagnostics instance: per-block eta / lambda / Temple width)
+          static std::atomic<unsigned long long> attrd{0};
+          lds_attr_once(attrd, (const void*)eigmin_mx<T, 1>, (int)(LDS_MAX - EIGMX_STATIC_LDS));
+          eigmin_mx<T, 1><<<(unsigned)h.size(), 576, eigmx_lds_bytes<T>(nmax), s>>>(d, out, redo);
+        } else {
+          lds_attr_once(attrm, (const void*)eigmin_mx<T>, (int)(LDS_MAX - EIGMX_STATIC_LDS));
+          eigmin_mx<T><<<(unsigned)h.size(), 576, eigmx_lds_bytes<T>(nmax), s>>>(d, out, redo);
+        }
         HIPCHK(hipGetLastError());
         // the flagged blocks (clustered lambda_min) at the full width; the others exit at once
         lds_attr_once(attr2r, (const void*)eigmin_lds2<T, true>, (int)LDS_MAX);
@@ -3185,6 +3195,21 @@ int32_t clrsdp_get_factorization(const clrsdp_handle* h, int32_t* flags) {
 
 int32_t clrsdp_destroy(clrsdp_handle* h) {
   if (!h) return CLRSDP_OK;
+  // CLRSDP_EIGMX_STATS=1: how many blocks eigmin_mx handed to the multi-word path so far (all
+  // handles of the process; diagnostics only)
+  if (env_on("CLRSDP_EIGMX_STATS")) {
+    unsigned int fb = 0;
+    if (hipMemcpyFromSymbol(&fb, HIP_SYMBOL(g_eigmx_fallbacks), sizeof(fb)) == hipSuccess)
+      std::fprintf(stderr, "clrsdp: eigmin_mx multi-word fallbacks so far: %u\n", fb);
+    std::vector<double> z(256 * 24);
+    if (hipMemcpyFromSymbol(z.data(), HIP_SYMBOL(g_eigmx_dbg), z.size() * sizeof(double)) == hipSuccess)
+      for (int b = 0; b < 64; ++b) {
+        const double* q = &z[b * 24];
+        if (q[20] == 0.0 && q[23] == 0.0) continue;
+        std::fprintf(stderr, "  block %d (last launch): eta %.2e %.2e %.2e %.2e lam %.17g lam2 %.17g rho %.17g temple %.2e\n",
+                     b, q[16], q[17], q[18], q[19], q[20], q[21], q[22], q[23]);
+      }
+  }
   GUARD(h, { delete h; return CLRSDP_OK; })
 }
 

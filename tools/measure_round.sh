@@ -19,6 +19,13 @@ timeout -k 10 200 python3 bench.py > $OUT/bench_c3_fp64.log 2>&1
 timeout -k 10 200 python3 bench.py --config c2 > $OUT/bench_c2_fp64.log 2>&1
 timeout -k 10 200 python3 bench.py --config c2 --precision 2 > $OUT/bench_c4_dd.log 2>&1
 timeout -k 10 200 python3 bench.py --config c5 --precision 4 > $OUT/bench_c5_qd.log 2>&1
+# kernel summaries of the multi-word lines (C4 double-double, C5 quad-double)
+for cfg in "c4_dd:--config c2 --precision 2" "c5_qd:--config c5 --precision 4"; do
+  name=${cfg%%:*}; args=${cfg#*:}
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$name -o run -- \
+    python3 bench.py --steps 20 --warmup 3 --no-cpu $args > $OUT/kt_$name.log 2>&1
+  python3 tools/prof_summary.py $OUT/kt_$name/run_kernel_stats.csv > $OUT/${name}_kernel_summary.txt
+done
 for c in 8 16 32; do
   timeout -k 10 120 python3 bench.py --clusters $c --no-cpu --steps 300 > $OUT/clusters_$c.log 2>&1
 done

@@ -105,7 +105,7 @@ void run(const char* name, int n, int nb, int family, int gexp) {
   CK(hipMemcpy(dd_, din.data(), nb * sizeof(MatDesc<T>), hipMemcpyHostToDevice));
   const size_t l2 = eig2_lds_bytes<T>(n), lm = eigmx_lds_bytes<T>(n);
   CK(hipFuncSetAttribute((const void*)eigmin_lds2<T, true, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  CK(hipFuncSetAttribute((const void*)eigmin_mx<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)eigmin_mx<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EIGMX_STATIC_LDS));
   const float t2 = timeit([&] { eigmin_lds2<T, true, 0><<<nb, 512, l2>>>(dd_, dE); });
   unsigned zero = 0, fb = 0;
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_eigmx_fallbacks), &zero, sizeof(zero)));
@@ -124,7 +124,7 @@ void run(const char* name, int n, int nb, int family, int gexp) {
   });
   // diagnostics of the DBG instance: phase stamps (s_memtime ticks) averaged over the
   // blocks, and eta / lambda / lambda_2 / rho / Temple width of the first rejected blocks
-  CK(hipFuncSetAttribute((const void*)eigmin_mx<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)eigmin_mx<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EIGMX_STATIC_LDS));
   std::vector<double> dz(256 * 24, 0.0);
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_eigmx_dbg), dz.data(), dz.size() * sizeof(double)));
   eigmin_mx<T, 1><<<nb, 576, lm>>>(dd_, dE + nb, redo);

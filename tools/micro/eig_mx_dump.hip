@@ -34,7 +34,7 @@ static void run(int n) {
   MatDesc<dd> h{dA, n, n}, *dd_;
   CK(hipMalloc(&dd_, sizeof(h)));
   CK(hipMemcpy(dd_, &h, sizeof(h), hipMemcpyHostToDevice));
-  CK(hipFuncSetAttribute((const void*)eigmin_mx<dd, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)eigmin_mx<dd, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EIGMX_STATIC_LDS));
   eigmin_mx<dd, 2><<<1, 576, eigmx_lds_bytes<dd>(n)>>>(dd_, dE, redo);
   CK(hipDeviceSynchronize());
   std::vector<double> dm(64 * 64 + 12 * 64);
