@@ -385,22 +385,18 @@ __global__ __launch_bounds__(256) void gemm_valu(const GemmDesc<T>* __restrict__
     {  // A tile 16 x 16: i contiguous in memory unless TA
       const int i = TA ? (tid >> 4) : (tid & 15), k = TA ? (tid & 15) : (tid >> 4);
       const int gi = m0 + i, gk = k0 + k;
-      T v = T(0.0);
-      if (gi < d.M && gk < d.K) {
-        if (TA) v = d.A[gk + (size_t)gi * d.lda];
-        else v = d.A[gi + (size_t)gk * d.lda];
-      }
-      As[k][i] = v;
+      // (an unconditional load from a clamped index and a component-wise select: a multi-word
+      // value assigned under a branch stayed in scratch memory)
+      const bool in = gi < d.M && gk < d.K;
+      const size_t ia = in ? (TA ? gk + (size_t)gi * d.lda : gi + (size_t)gk * d.lda) : 0;
+      As[k][i] = sel(in, d.A[ia], T(0.0));
     }
     {  // B tile 16 x 16: j contiguous in memory iff TB
       const int j = TB ? (tid & 15) : (tid >> 4), k = TB ? (tid >> 4) : (tid & 15);
       const int gj = n0 + j, gk = k0 + k;
-      T v = T(0.0);
-      if (gj < d.N && gk < d.K) {
-        if (TB) v = d.B[gj + (size_t)gk * d.ldb];
-        else v = d.B[gk + (size_t)gj * d.ldb];
-      }
-      Bs[k][j] = v;
+      const bool in = gj < d.N && gk < d.K;
+      const size_t ib = in ? (TB ? gj + (size_t)gk * d.ldb : gk + (size_t)gj * d.ldb) : 0;
+      Bs[k][j] = sel(in, d.B[ib], T(0.0));
     }
     __syncthreads();
 #pragma unroll
@@ -443,22 +439,18 @@ __global__ __launch_bounds__(256) void gemm_valu_ks(const GemmDesc<T>* __restric
     {  // A tile 8 x 32 (the contiguous index fastest)
       const int i = TA ? (tid >> 5) : (tid & 7), k = TA ? (tid & 31) : (tid >> 3);
       const int gi = m0 + i, gk = k0 + k;
-      T v = T(0.0);
-      if (gi < d.M && gk < d.K) {
-        if (TA) v = d.A[gk + (size_t)gi * d.lda];
-        else v = d.A[gi + (size_t)gk * d.lda];
-      }
-      As[k][i] = v;
+      // (an unconditional load from a clamped index and a component-wise select: a multi-word
+      // value assigned under a branch stayed in scratch memory)
+      const bool in = gi < d.M && gk < d.K;
+      const size_t ia = in ? (TA ? gk + (size_t)gi * d.lda : gi + (size_t)gk * d.lda) : 0;
+      As[k][i] = sel(in, d.A[ia], T(0.0));
     }
     {  // B tile 32 x 8
       const int j = TB ? (tid & 7) : (tid >> 5), k = TB ? (tid >> 3) : (tid & 31);
       const int gj = n0 + j, gk = k0 + k;
-      T v = T(0.0);
-      if (gj < d.N && gk < d.K) {
-        if (TB) v = d.B[gj + (size_t)gk * d.ldb];
-        else v = d.B[gk + (size_t)gj * d.ldb];
-      }
-      Bs[k][j] = v;
+      const bool in = gj < d.N && gk < d.K;
+      const size_t ib = in ? (TB ? gj + (size_t)gk * d.ldb : gk + (size_t)gj * d.ldb) : 0;
+      Bs[k][j] = sel(in, d.B[ib], T(0.0));
     }
     __syncthreads();
 #pragma unroll

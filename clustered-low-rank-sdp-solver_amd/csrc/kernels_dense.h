@@ -2791,8 +2791,10 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
 #pragma unroll
   for (int q = 0; q < SLOTS; ++q) {
     const int t = wk + NWK * q;
-    TI[q] = NT; TJ[q] = 0;  // empty slot: row NT is never active
-    if (wk >= 0 && t < CT::NOFF) CT::tile(t, TI[q], TJ[q]);
+    int ti = NT, tj = 0;  // empty slot: row NT is never active
+    if (wk >= 0 && t < CT::NOFF) CT::tile(t, ti, tj);
+    TI[q] = ti;
+    TJ[q] = tj;
   }
   // ---- off-diagonal tiles straight into the accumulators (A_ij^T layout, coalesced along
   // rows), diagonal tiles into LDS with identity padding
