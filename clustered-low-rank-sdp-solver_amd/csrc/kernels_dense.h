@@ -2084,7 +2084,7 @@ __global__ __launch_bounds__(512) void eigmin_lds2(const MatDesc<T>* __restrict_
 //      (g_eigmx_fallbacks counts those).
 // ------------------------------------------------------------------------------------------
 __device__ unsigned int g_eigmx_fallbacks = 0;
-template <class T> __host__ __device__ constexpr int eigmx_refine() { return sizeof(T) > 16 ? 4 : 3; }
+template <class T> __host__ __device__ constexpr int eigmx_refine() { return 6; }
 template <class T> size_t eigmx_own_bytes(int n) {
   const size_t ld = eig2_ld<double>(n), W = sizeof(T) / 8;
   return 8 * (128 + (size_t)n * ld + 3 * ld + 2 * (size_t)n + 4 + 16 + (size_t)n * n +
@@ -2568,7 +2568,9 @@ __global__ __launch_bounds__(TRI ? 576 : 512) void eigmin_mx(const MatDesc<T>* _
       stamp(4);
       ok = sc[4] != 0.0;
       // (4)-(5) Rayleigh quotient and residual of x; accepted as soon as Temple's width is below
-      // 2^-(BITS+2) of |T| < 1, else a refinement step (at most R: 3 at dd, 4 at qd)
+      // 2^-(BITS+2) of |T| < 1, else a refinement step (at most R = 6: a close lambda_2 slows
+      // the refinement to ~2^-50 |T| / gap per step, and a few more steps of ~25 us are far
+      // cheaper than the multi-word fallback)
       for (int it = 0; ok && it <= R; ++it) {
         // row partials of y = A_s x: row lane, columns j = w (mod 8)
         if (lane < n && w < NW) {
@@ -2600,7 +2602,9 @@ __global__ __launch_bounds__(TRI ? 576 : 512) void eigmin_mx(const MatDesc<T>* _
           const double tw = lam2 > rhs ? eta / (lam2 - rhs) : INFINITY;
           const bool acc = tw <= 0x1p-3 * Num<T>::eps();  // 2^-(BITS+2) of |T| < 1
           if (lane == 0) {
-            sc[5] = acc ? 1.0 : (it == R ? -1.0 : 0.0);  // accepted / rejected / refine
+            // accepted / rejected (the last step, or no lambda_2 bound above rho: Temple's bound
+            // cannot hold however far x is refined) / refine
+            sc[5] = acc ? 1.0 : ((it == R || !(lam2 > rhs)) ? -1.0 : 0.0);
             if (acc) out[blockIdx.x] = rho;
             if constexpr (DBG != 0) {
               dbg[20] = lam;
@@ -2609,7 +2613,7 @@ __global__ __launch_bounds__(TRI ? 576 : 512) void eigmin_mx(const MatDesc<T>* _
               dbg[23] = tw;
             }
           }
-          if (!acc && it < R) {
+          if (!acc && it < R && lam2 > rhs) {
             // s = P Q^T (-r) in fp64 (scaled) -> wv for the solve
             double s = apply_q(-rh, true);
             s -= wave_sum_mw<double>(zl * s) * zl;
