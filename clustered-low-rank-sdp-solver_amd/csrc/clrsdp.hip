@@ -2590,8 +2590,8 @@ struct Solver final : HandleBase {
       }
   }
   void launch_graph(const clrsdp_params* prm, int pd_feas) {
-    static const bool one_graph = env_on("CLRSDP_PIPE_ONE_GRAPH");  // (A/B: one executable)
-    const int g = pd_feas < 0 ? 2 + (one_graph ? 0 : (graph_launches++ & 1)) : (pd_feas ? 1 : 0);
+    // (one executable for every pipelined body measured the same as two alternating, round 4)
+    const int g = pd_feas < 0 ? 2 + (graph_launches++ & 1) : (pd_feas ? 1 : 0);
     if (!gexec[g] || std::memcmp(&gprm[g], prm, sizeof(*prm)) != 0) {
       if (gexec[g]) HIPCHK(hipGraphExecDestroy(gexec[g]));
       gexec[g] = nullptr;
