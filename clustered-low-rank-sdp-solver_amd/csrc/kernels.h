@@ -1237,21 +1237,29 @@ __global__ __launch_bounds__(NT) void getrf_batched(const LuDesc<T>* __restrict_
       int brow = pm;
       for (int i = j + tid; i < pm; i += NT) {
         const T a = Num<T>::abs_(P[j * pm + i]);
-        if (a > best) { best = a; brow = i; }
+        const bool gt = a > best;  // (component-wise selects: a multi-word value assigned under
+        best = sel(gt, a, best);   // a branch stayed in scratch memory)
+        brow = gt ? i : brow;
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
         const T ob = shfl_xor_t(best, o);
         const int orow = __shfl_xor(brow, o);
-        if (ob > best || (!(ob < best) && orow < brow)) { best = ob; brow = orow; }
+        const bool tk = ob > best || (!(ob < best) && orow < brow);
+        best = sel(tk, ob, best);
+        brow = tk ? orow : brow;
       }
       if (lane == 0) { wbest[wv] = best; wrow[wv] = brow; }
       __syncthreads();
       if (tid == 0) {
         T b = wbest[0];
         int r = wrow[0];
-        for (int w = 1; w < NWV; ++w)
-          if (wbest[w] > b || (!(wbest[w] < b) && wrow[w] < r)) { b = wbest[w]; r = wrow[w]; }
+        for (int w = 1; w < NWV; ++w) {
+          const T bw = wbest[w];
+          const bool tk = bw > b || (!(bw < b) && wrow[w] < r);
+          b = sel(tk, bw, b);
+          r = tk ? wrow[w] : r;
+        }
         if (!(b > T(0.0))) {
           fail = k0 + j + 1;
         } else {
