@@ -314,6 +314,13 @@ def main():
     traffic, traffic_src = schur_pmc_traffic(args.config, args.precision, world, args.clusters)
     achieved = fl / sch_s / 1e12   # in flops of the word type (multi-word flops when w > 1)
     peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]
+    # the library's default (clrsdp.hip use_graph / graph_ok): replay at world 1 unless
+    # CLRSDP_NO_GRAPH, and at quad-double only with CLRSDP_GRAPH_QD; sharded only with
+    # CLRSDP_GRAPH_RCCL on the native exchange
+    graph_on = (not os.environ.get("CLRSDP_NO_GRAPH")
+                and (args.precision != 4 or bool(os.environ.get("CLRSDP_GRAPH_QD")))
+                and (world == 1 or (getattr(dist, "backend", "") == "rccl"
+                                    and os.environ.get("CLRSDP_GRAPH_RCCL") is not None)))
     res = {
         "metric": "interior-point iterations/sec (solverank1sdp loop body, MPMP.jl:755-887)",
         "value": value,
@@ -353,8 +360,7 @@ def main():
         "phase_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.STAGE_NAMES, phase)},
         # the reference's inner buckets (MPMP.jl:997-1012), same instrumented pass
         "inner_ms_per_iteration": {n: float(v / n_inst) for n, v in zip(_lib.INNER_NAMES, inner)},
-        "graph_replay": world == 1 or (getattr(dist, "backend", "") == "rccl"
-                                       and os.environ.get("CLRSDP_GRAPH_RCCL") is not None),
+        "graph_replay": graph_on,
         "exchange": "none (1 GPU)" if dist is None else dist.backend,
         # the communicator the library's loop body really uses: ranks from ncclCommCount on the
         # native RCCL path (clrsdp_comm_info), world_size on the callback path
@@ -365,8 +371,10 @@ def main():
                                 "(clrsdp_set_graph(0): the ~100 launches of one loop body enqueued "
                                 "eagerly, as the sharded path does), 10 bodies from the initial point"),
         "eager_body_ms": eager_body_ms,
-        "host_loop": "pipelined (host one loop body behind, device-side pd_feas/terminate)"
-                     if pipelined else "synchronous (one hipGraph replay per loop body)",
+        "host_loop": ("pipelined (host one loop body behind, device-side pd_feas/terminate)"
+                      if pipelined else
+                      "synchronous (one hipGraph replay per loop body)" if graph_on else
+                      "synchronous (loop body enqueued eagerly: quad-double default)"),
     }
     if world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(pk, cons, b, bi, args.precision)

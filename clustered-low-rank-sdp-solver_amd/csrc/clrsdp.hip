@@ -1758,6 +1758,20 @@ struct Solver final : HandleBase {
     if (n > 0)
       vec_copy_guard<T><<<std::min<unsigned>(cdiv(n, 256), 2048), 256, 0, stream>>>(dst, src, n, info + info_H);
   }
+  // two guarded copies in one launch (16-byte moves)
+  void copy_guarded2(T* d0, const T* s0, int64_t n0, T* d1, const T* s1, int64_t n1) {
+    if (n0 <= 0 && n1 <= 0) return;
+    auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    if (n0 <= 0 || !a16(d0) || !a16(s0) || (n1 > 0 && (!a16(d1) || !a16(s1)))) {
+      copy_guarded(d0, s0, n0);
+      copy_guarded(d1, s1, n1);
+      return;
+    }
+    const long long b0 = (long long)n0 * (long long)sizeof(T), b1 = n1 > 0 ? (long long)n1 * (long long)sizeof(T) : 0;
+    const long long chunks = std::max(b0, b1) / 16 + 1;
+    const unsigned g = (unsigned)std::min<long long>((chunks + 255) / 256, 1024);
+    copy_guard2<<<g, 256, 0, stream>>>(d0, s0, b0, n1 > 0 ? d1 : nullptr, s1, b1, info + info_H);
+  }
   void fill(T* out, double v, int64_t n) {
     if (n > 0) vec_fill<T><<<cdiv(n, 256), 256, 0, stream>>>(out, v, n);
   }
@@ -2514,8 +2528,7 @@ struct Solver final : HandleBase {
     side(ev_s, [&] {
       residuals_rest(true);
       if (keep_res) {
-        copy_guarded(Pres, P, nblk_el);
-        copy_guarded(dres, dvec, nx);
+        copy_guarded2(Pres, P, nblk_el, dres, dvec, nx);
       }
       direction_Z();
       direction_rhs();
@@ -2561,7 +2574,10 @@ struct Solver final : HandleBase {
   hipGraphExec_t gexec[4] = {nullptr, nullptr, nullptr, nullptr};
   clrsdp_params gprm[4];
   unsigned graph_launches = 0;
-  bool use_graph = !env_on("CLRSDP_NO_GRAPH");
+  // quad-double bodies are enqueued eagerly by default: C5 719-730 against 672-706 it/s with
+  // the replayed graph (A/B, round 4; fp64 and double-double measured equal or better with the
+  // graph); CLRSDP_GRAPH_QD=1 replays them too
+  bool use_graph = !env_on("CLRSDP_NO_GRAPH") && (sizeof(T) <= 16 || env_on("CLRSDP_GRAPH_QD"));
   // multi-rank loop bodies with the native communicator are enqueued eagerly by default (the
   // pipelined host loop hides the enqueue); CLRSDP_GRAPH_RCCL=1 captures the all-gathers into
   // the replayed graph as well

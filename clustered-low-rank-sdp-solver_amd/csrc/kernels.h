@@ -2365,6 +2365,28 @@ __global__ void vec_copy_guard(T* __restrict__ dst, const T* __restrict__ src, l
     dst[e] = src[e];
 }
 
+// dst_q = src_q for the (up to two) segments q unless *halt: 16-byte moves over the segments'
+// bytes (the buffers are 256-byte aligned device allocations; an 8-byte tail when a segment's
+// byte count is odd in 8-byte words), one launch for the keep-residuals copies of a pipelined
+// loop body (P and d; the 8 MB P of C3 took 16.7 us as 8-byte element copies)
+__global__ void copy_guard2(void* __restrict__ d0, const void* __restrict__ s0, long long b0,
+                            void* __restrict__ d1, const void* __restrict__ s1, long long b1,
+                            const int* __restrict__ halt) {
+  if (*halt) return;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  auto seg = [&](void* dv, const void* sv, long long bytes) {
+    const long long n16 = bytes >> 4;
+    uint4* dq = reinterpret_cast<uint4*>(dv);
+    const uint4* sq = reinterpret_cast<const uint4*>(sv);
+    for (long long e = tid; e < n16; e += stride) dq[e] = sq[e];
+    if ((bytes & 15) && tid == 0)
+      reinterpret_cast<double*>(dv)[(bytes >> 3) - 1] = reinterpret_cast<const double*>(sv)[(bytes >> 3) - 1];
+  };
+  seg(d0, s0, b0);
+  if (d1) seg(d1, s1, b1);
+}
+
 template <class T>
 __global__ void vec_fill(T* out, double v, long long n) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
