@@ -315,10 +315,10 @@ def main():
     achieved = fl / sch_s / 1e12   # in flops of the word type (multi-word flops when w > 1)
     peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]
     # the library's default (clrsdp.hip use_graph / graph_ok): replay at world 1 unless
-    # CLRSDP_NO_GRAPH, and at quad-double only with CLRSDP_GRAPH_QD; sharded only with
-    # CLRSDP_GRAPH_RCCL on the native exchange
+    # CLRSDP_NO_GRAPH, and at double-double / quad-double only with CLRSDP_GRAPH_MW; sharded only
+    # with CLRSDP_GRAPH_RCCL on the native exchange
     graph_on = (not os.environ.get("CLRSDP_NO_GRAPH")
-                and (args.precision != 4 or bool(os.environ.get("CLRSDP_GRAPH_QD")))
+                and (args.precision == 1 or bool(os.environ.get("CLRSDP_GRAPH_MW")))
                 and (world == 1 or (getattr(dist, "backend", "") == "rccl"
                                     and os.environ.get("CLRSDP_GRAPH_RCCL") is not None)))
     res = {
@@ -374,7 +374,7 @@ def main():
         "host_loop": ("pipelined (host one loop body behind, device-side pd_feas/terminate)"
                       if pipelined else
                       "synchronous (one hipGraph replay per loop body)" if graph_on else
-                      "synchronous (loop body enqueued eagerly: quad-double default)"),
+                      "synchronous (loop body enqueued eagerly: the multi-word default)"),
     }
     if world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(pk, cons, b, bi, args.precision)

@@ -2574,10 +2574,11 @@ struct Solver final : HandleBase {
   hipGraphExec_t gexec[4] = {nullptr, nullptr, nullptr, nullptr};
   clrsdp_params gprm[4];
   unsigned graph_launches = 0;
-  // quad-double bodies are enqueued eagerly by default: C5 719-730 against 672-706 it/s with
-  // the replayed graph (A/B, round 4; fp64 and double-double measured equal or better with the
-  // graph); CLRSDP_GRAPH_QD=1 replays them too
-  bool use_graph = !env_on("CLRSDP_NO_GRAPH") && (sizeof(T) <= 16 || env_on("CLRSDP_GRAPH_QD"));
+  // multi-word bodies are enqueued eagerly by default: C5 (qd) 719-730 against 672-706 it/s,
+  // C4 (dd) 620-625 against 600-617 with the replayed graph (A/B, round 4); fp64 keeps the
+  // replay (C3 equal, C2 2288-2315 against 2122-2288 eager); CLRSDP_GRAPH_MW=1 replays
+  // multi-word bodies too
+  bool use_graph = !env_on("CLRSDP_NO_GRAPH") && (sizeof(T) == 8 || env_on("CLRSDP_GRAPH_MW"));
   // multi-rank loop bodies with the native communicator are enqueued eagerly by default (the
   // pipelined host loop hides the enqueue); CLRSDP_GRAPH_RCCL=1 captures the all-gathers into
   // the replayed graph as well
