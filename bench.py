@@ -47,6 +47,12 @@ HBM_PEAK_GBS = 8000.0
 MW_VALU_PEAK_TFLOPS = {2: 3.736, 4: 0.698}
 
 
+def env_on(name):
+    """The library's switch rule (clrsdp.hip env_on): set, and not starting with '0'."""
+    v = os.environ.get(name)
+    return v is not None and v[:1] != "0"
+
+
 def schur_flops_bytes(bi, word=8):
     """Algorithmic Schur-assembly work of one iteration: per (j,l) block
     4 m^2 delta K (delta + K) + 8 rank^2 D(D+1)/2 flops and
@@ -282,7 +288,9 @@ def main():
         dev.iterate_wait()
         body.append(time.perf_counter() - t1)
         enq.append(t2 - t1)
-    dev.set_graph(True)
+    # back to the library's own default for this handle (the graph at fp64 unless
+    # CLRSDP_NO_GRAPH; eager at double-double / quad-double unless CLRSDP_GRAPH_MW)
+    dev.set_graph(not env_on("CLRSDP_NO_GRAPH") and (args.precision == 1 or env_on("CLRSDP_GRAPH_MW")))
     host_enqueue_ms = float(np.median(enq[2:])) * 1e3
     eager_body_ms = float(np.median(body[2:])) * 1e3
     barrier_sync()
@@ -317,10 +325,10 @@ def main():
     # the library's default (clrsdp.hip use_graph / graph_ok): replay at world 1 unless
     # CLRSDP_NO_GRAPH, and at double-double / quad-double only with CLRSDP_GRAPH_MW; sharded only
     # with CLRSDP_GRAPH_RCCL on the native exchange
-    graph_on = (not os.environ.get("CLRSDP_NO_GRAPH")
-                and (args.precision == 1 or bool(os.environ.get("CLRSDP_GRAPH_MW")))
+    graph_on = (not env_on("CLRSDP_NO_GRAPH")
+                and (args.precision == 1 or env_on("CLRSDP_GRAPH_MW"))
                 and (world == 1 or (getattr(dist, "backend", "") == "rccl"
-                                    and os.environ.get("CLRSDP_GRAPH_RCCL") is not None)))
+                                    and env_on("CLRSDP_GRAPH_RCCL"))))
     res = {
         "metric": "interior-point iterations/sec (solverank1sdp loop body, MPMP.jl:755-887)",
         "value": value,

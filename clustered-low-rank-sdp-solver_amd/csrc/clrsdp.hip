@@ -20,8 +20,6 @@
 #include <string>
 #include <array>
 #include <vector>
-#include <vector>
-#include <array>
 
 #include "../../include/clrsdp.h"
 #include "kernels.h"
@@ -202,6 +200,17 @@ static inline bool env_on(const char* name) {
   const char* e = std::getenv(name);
   return e && e[0] != '0';
 }
+
+// work enqueued on another stream for one scope: `stream` is restored when the scope ends,
+// also when a launch inside throws (a capture-abort path relies on `stream` being the main one)
+struct StreamSwitch {
+  hipStream_t& cur;
+  hipStream_t saved;
+  StreamSwitch(hipStream_t& c, hipStream_t to) : cur(c), saved(c) { cur = to; }
+  ~StreamSwitch() { cur = saved; }
+  StreamSwitch(const StreamSwitch&) = delete;
+  StreamSwitch& operator=(const StreamSwitch&) = delete;
+};
 
 // the plans own their device descriptor arrays (freed with the plan; plans are never copied)
 struct PlanBase {
@@ -730,11 +739,9 @@ struct LuPlan : PlanBase {
   }
   size_t lds = 0;
   // (outside any graph capture: the LDS attribute is set here, not at launch)
-  int* redo = nullptr;  // eigmin_mx's per-block fallback flags
   void finalize() {
     if (h.empty()) return;
     d = own(h);
-    if (!std::is_same<T, double>::value) redo = own(std::vector<int>(h.size(), 1));
     lds = getrf_lds_bytes<T, NB>(nmax);
     // the static LDS of the kernel (pivot search, pivots) comes on top of the dynamic panel
     if (lds > LDS_MAX - 4096) throw ClrsdpError{CLRSDP_E_ARG, "LU fallback: matrix too large for the on-chip panel"};
@@ -864,6 +871,7 @@ struct Solver final : HandleBase {
   int64_t nx = 0, nblk_el = 0, nV = 0, nK = 0, nT = 0, nBX = 0, nAY = 0, nS = 0, nB = 0, nRS = 0;
   bool anyMgt1 = false, hasC = false;
   int nc2 = 0;  // clusters factorised as 2x2 blocks (128 < dim_S <= 256, fp64)
+  bool s_lower = false;  // the last SCHUR enqueued assembled the lower triangle of S only
 
   // ---------------- device memory
   hipStream_t own_stream = nullptr, stream = nullptr;
@@ -1383,7 +1391,8 @@ struct Solver final : HandleBase {
         s2off += 2 * (int64_t)D2 * D1;
         b2off += (int64_t)D2 * n_y;
         s11.push_back(MatDesc<T>{S11, D1, D});                                          // S11 <- L11^-1
-        f_a.add_op(false, false, 1.0, 0.0, S11, D, S12, D, nullptr, 0, T12, D1, D1, D2, D1);
+        // (S21^T, not S12: the fused Schur kernel may assemble only the lower triangle)
+        f_a.add_op(false, true, 1.0, 0.0, S11, D, S21, D, nullptr, 0, T12, D1, D1, D2, D1);
         f_a.add_op(false, false, 1.0, 0.0, S11, D, Bc, D, nullptr, 0, Wc, D, D1, ny, D1);  // W1
         f_b.add_op(true, false, -1.0, 1.0, T12, D1, T12, D1, S22, D, S22, D, D2, D2, D1);  // S22 - L21 L21^T
         f_b.add_op(true, false, 1.0, 0.0, Wc, D, Wc, D, nullptr, 0, slab, ny, ny, ny, D1); // W1^T W1
@@ -1393,7 +1402,7 @@ struct Solver final : HandleBase {
         f_d.add(Wc + D1, D, Wc + D1, D, slab, ny, slab, ny, ny, ny, D2);               // slab += W2^T W2
         f_x1.add(S22, D, T12, D1, nullptr, 0, Mb, D2, D2, D1, D2);                      // M = L22^-1 L21
         f_x2.add(Mb, D2, S11, D, nullptr, 0, S21, D, D2, D1, D1);                       // S21 <- -M L11^-1
-        // S12 keeps the assembled S: the products with L^-1 below are split so that none reads it
+        // S12 is not part of L^-1: the products with L^-1 below are split so that none reads it
         q_t.add(S11, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D1, 1, D1);
         q_t.add(Sc + D1, D, rhs + xo, D, nullptr, 0, tvec + xo + D1, D, D2, 1, D);
         // dx = (L^-1)^T u: columns 0..D1-1 of L^-1 are [L11^-1; X21], the rest L22^-1
@@ -1971,10 +1980,16 @@ struct Solver final : HandleBase {
         } else if (!(schur_fused && fused_y)) {
           p_ty.launch(stream, 1.0, 0.0);
         }
+        // the fused kernel writes the lower triangle of S only when every reader takes that
+        // triangle (the fp64 Cholesky FACTOR: chol_inv_tiles, and L21^T = L11^-1 S21^T); the
+        // pivoted LU and the rank-group sums read all of it.  CLRSDP_SCHUR_FULL=1 for A/B
+        static const bool force_full = env_on("CLRSDP_SCHUR_FULL");
+        const bool full = force_full || !fac2 || n_gsum > 0 || lu_sq();
+        s_lower = schur_fused && !full;
         if (schur_fused && fused_y)
-          schur_fused_f64<0, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4);
+          schur_fused_f64<0, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
         else if (schur_fused)
-          schur_fused_f64<0><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4);
+          schur_fused_f64<0><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
         else if (n_ptiles)
           schur_pairs_f64<16><<<n_ptiles, 256, 0, stream>>>(d_ptd, d_pt2d, stamps + 4);
         if (n_gsum) {
@@ -2000,6 +2015,7 @@ struct Solver final : HandleBase {
   }
   // side_x21: X21 on the side stream (the loop body), joined before the first solve
   void factor_local(bool side_x21 = false) {
+    s_lower = false;  // S now turns into L^-1 (or the LU factors)
     // (inner timing buckets: a mixed batch counts where most of its work is; the reference's
     // chol_S / CinvB / Q split, MPMP.jl:1429-1495)
     if (lu_sq()) {                            // approx_lu! (MPMP.jl:1433-1494)
@@ -2026,12 +2042,13 @@ struct Solver final : HandleBase {
           const hipStream_t main_s = stream;
           HIPCHK(hipEventRecord(ev_x2, main_s));
           HIPCHK(hipStreamWaitEvent(aux, ev_x2, 0));
-          stream = aux;
-          seg(CLRSDP_INNER_CHOL_S, [&] {
-            f_x1.launch(aux, 1.0, 0.0);
-            f_x2.launch(aux, -1.0, 0.0);
-          });
-          stream = main_s;
+          {
+            StreamSwitch on_aux(stream, aux);  // restored on scope exit, also when a launch throws
+            seg(CLRSDP_INNER_CHOL_S, [&] {
+              f_x1.launch(aux, 1.0, 0.0);
+              f_x2.launch(aux, -1.0, 0.0);
+            });
+          }
           HIPCHK(hipEventRecord(ev_x21, aux));
           pending_x21 = true;
         } else {
@@ -2211,7 +2228,11 @@ struct Solver final : HandleBase {
         return !(e && e[0] == '0');
       }();
       const size_t lds = ((size_t)n_y + 256) * sizeof(double);
-      if (reg_Q && fused_q && lds <= 64 * 1024) {
+      // every workgroup re-forms all of r: cdiv(n_y, 64) x cnt x n_y slab reads in all.  Fused
+      // only while those stay small (C3: 2 x 64 x 128); otherwise slab_sum forms r once
+      const long long cnt_x = (world == 1 && nc()) ? nc() : world;
+      const bool small_sum = (long long)cdiv(n_y, 64) * cnt_x * n_y <= (1LL << 20);
+      if (reg_Q && fused_q && small_sum && lds <= 64 * 1024) {
         const double* src = pslab;
         int cnt = nc();
         if (!(world == 1 && nc())) {
@@ -2503,9 +2524,8 @@ struct Solver final : HandleBase {
     auto side = [&](hipEvent_t ev, auto&& work) {
       HIPCHK(hipEventRecord(ev, main_s));
       HIPCHK(hipStreamWaitEvent(aux, ev, 0));
-      stream = aux;
+      StreamSwitch on_aux(stream, aux);
       work();
-      stream = main_s;
     };
     mark(CLRSDP_STAGE_MU_R);
     stage(CLRSDP_STAGE_MU_R, prm, pd_feas);
@@ -2539,10 +2559,11 @@ struct Solver final : HandleBase {
     // side stream: chol(Q) -> L_Q^-1, waited for just before the first Q solve
     HIPCHK(hipEventRecord(ev_qa, main_s));
     HIPCHK(hipStreamWaitEvent(aux, ev_qa, 0));
-    stream = aux;
-    factor_q();
+    {
+      StreamSwitch on_aux(stream, aux);
+      factor_q();
+    }
     HIPCHK(hipEventRecord(ev_q, aux));
-    stream = main_s;
     pending_q = true;
     mark(CLRSDP_STAGE_RESIDUALS);
     HIPCHK(hipStreamWaitEvent(main_s, ev_r, 0));
@@ -2804,6 +2825,14 @@ struct Solver final : HandleBase {
     }
     if (count) *count = n;
     if (host) get(src, host, n, 0, n);
+    if (host && buf == CLRSDP_BUF_S && s_lower) {  // (fp64 only) the full symmetric S_j
+      for (int c = 0; c < nc(); ++c) {
+        const int64_t D = Ds[oc[c]];
+        double* Sc = host + c_Soff[c];
+        for (int64_t j = 0; j < D; ++j)
+          for (int64_t i = 0; i < j; ++i) Sc[i + j * D] = Sc[j + i * D];
+      }
+    }
   }
 
   int64_t exchange_bytes() const override { return xcap * (int64_t)sizeof(T); }

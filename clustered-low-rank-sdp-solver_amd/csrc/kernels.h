@@ -1745,7 +1745,9 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
 //            current one.  G[p, q] = lambda_p lambda_q P_X P_Y is staged in LDS (XOR-swizzled
 //            64 x 64) and written to (p, q) and to its mirror (q, p) as whole 64-row column
 //            segments; a diagonal tile takes its p <= q half for both, and writes AY[p] =
-//            P_Y[p, p].
+//            P_Y[p, p].  With full = false (G is S itself and every reader of it takes the lower
+//            triangle: the fp64 Cholesky path) only the tile below the diagonal and the lower
+//            half of a diagonal tile are written, K(K+1)/2-ish instead of K^2 stores.
 // MPMP.jl:1291-1330 + 1373-1398 at m = 1, as schur_pairs_f64.
 // ------------------------------------------------------------------------------------------
 struct FusedPairDesc {
@@ -1778,7 +1780,8 @@ __device__ __forceinline__ int st_idx(int row, int col) { return row * 64 + (col
 template <int DBG = 0, bool YV = false>
 __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __restrict__ descs,
                                                        const TileRef* __restrict__ t2d,
-                                                       unsigned long long* stamp = nullptr) {
+                                                       unsigned long long* stamp = nullptr,
+                                                       bool full = true) {
   using namespace schur_fused;
   if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   extern __shared__ __attribute__((aligned(16))) double sm_fused[];
@@ -1983,16 +1986,19 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
       for (int r = 0; r < 4; ++r) St[st_idx(16 * nt + 4 * r + lk, 16 * (2 * h + u) + lr)] = g[u][r];
     if (s + 1 < nb) storev();
     __syncthreads();
-    // (p, q) and its mirror (q, p) from the staging tile as 64-row column segments
+    // (p, q) and its mirror (q, p) from the staging tile as 64-row column segments (lower
+    // triangle only unless full: the tile whose row block is the larger one, and p >= q of a
+    // diagonal tile)
     {
       const int il = tid & 63;
+      const bool w_pq = full || a > b, w_qp = full || b > a;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         const int jl = (tid >> 6) + 8 * c;
-        if (a0 + il < K && b0 + jl < K && (!diag || il <= jl))  // G[a0 + il][b0 + jl]
+        if (a0 + il < K && b0 + jl < K && (diag ? full && il <= jl : w_pq))  // G[a0 + il][b0 + jl]
           d.G[(a0 + il) + (size_t)(b0 + jl) * d.ldG] = St[st_idx(il, jl)];
-        if (b0 + il < K && a0 + jl < K && (!diag || jl < il))   // G[b0 + il][a0 + jl]
-          d.G[(b0 + il) + (size_t)(a0 + jl) * d.ldG] = St[st_idx(jl, il)];
+        if (b0 + il < K && a0 + jl < K && (diag ? jl < il || (!full && jl == il) : w_qp))
+          d.G[(b0 + il) + (size_t)(a0 + jl) * d.ldG] = St[st_idx(jl, il)];  // G[b0 + il][a0 + jl]
       }
     }
   }

@@ -386,6 +386,16 @@ def _terminate(gap, perr, derr, gthr, pthr, dthr, need_p, need_d, out):
     return False
 
 
+def log_row(it, t, st, p_obj, d_obj, dual_gap):
+    """One row of the iteration table (MPMP.jl:923-937) as plain floats at every precision: the
+    loop control keeps the gap at full width (an mpmath number at dd/qd), the log and RunInfo.log
+    hold its leading double, like the other columns (the values at full width are in
+    RunInfo.exact with record_exact)."""
+    return (int(it), float(t), float(st.mu), float(p_obj), float(d_obj), float(dual_gap),
+            float(st.P_err), float(st.p_err), float(st.d_err), float(st.alpha_p),
+            float(st.alpha_d), float(st.beta_c))
+
+
 HEADER = "%5s %8s %11s %11s %11s %10s %10s %10s %10s %10s %10s %10s" % (
     "iter", "time(s)", "μ", "P-obj", "D-obj", "gap", "P-error", "p-error", "d-error", "α_p",
     "α_d", "beta")
@@ -469,7 +479,8 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     ``factorization``: clrsdp_set_factorization flags (default FACT_FALLBACK: Cholesky, and the
     reference's pivoted LU once a Cholesky fails, announced like MPMP.jl:776-778).  At
     double-double and quad-double the returned gap and objectives are mpmath numbers at the
-    state's full precision (MPMP.jl:1021-1023), not leading limbs.
+    state's full precision (MPMP.jl:1021-1023), not leading limbs; at fp64 they are floats.  The
+    log rows (RunInfo.log) are floats at every precision (:func:`log_row`).
     """
     kw = dict(beta_infeasible=beta_infeasible, beta_feasible=beta_feasible, gamma=gamma,
               omega_p=omega_p, omega_d=omega_d, duality_gap_threshold=duality_gap_threshold,
@@ -559,8 +570,7 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
             inner[:] += np.array(st.inner_ms[:])
         elif testing and timed:  # MPMP.jl:899-920: the times of the first iterations
             out(_first_iteration_times(np.array(st.phase_ms[:]) / 1e3))
-        row = (it, time.time() - t_start, st.mu, p_obj, d_obj, dual_gap, st.P_err, st.p_err,
-               st.d_err, st.alpha_p, st.alpha_d, st.beta_c)
+        row = log_row(it, time.time() - t_start, st, p_obj, d_obj, dual_gap)
         log.append(row)
         out("%5d %8.1f %11.3e %11.3e %11.3e %10.2e %10.2e %10.2e %10.2e %10.2e %10.2e %10.2e" % row)
         p_obj, d_obj = st.p_obj, st.d_obj

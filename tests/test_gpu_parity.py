@@ -345,26 +345,11 @@ def test_not_positive_definite_reports_error(pk, fallback):
     dev.close()
 
 
-def test_c3_full_size_newton_identities(pk, oracle):
-    """At the bench size (64 clusters x 128x128 blocks) check size-independent properties of one
-    GPU iteration: B^T dx = p, Tr(A_* dY) + B dy = d, dX = P + sum dx_i A_i, S symmetric."""
+def _newton_identities(pk, oracle, dev, cons, b, bi, words, what):
+    """The Newton-system identities of the direction in the device buffers: B^T dx = p,
+    Tr(A_* dY) + B dy = d, dX = P + sum dx_i A_i (MPMP.jl:1741-1786)."""
     from clrsdp_amd import _lib as L
     from clrsdp_amd import instance as inst
-    cons, b = pk.synth(seed=0, J=64, delta=128, rank=1, n_y=128)
-    bi = pk.get_block_info(cons)
-    dev = pk.DeviceSolver(cons, b, bi)
-    P = pk.make_params("0.3", "0.1", "0.7", 0)
-    dev.set_state(*pk.initial_point(bi, 100.0, 100.0))
-    for _ in range(2):
-        dev.iterate(P, False)
-    for s in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR):
-        dev.run_stage(s, P, False)
-    S = dev.buffer(L.BUF_S)
-    D = bi.dim_S[0]
-    S0 = S[:D * D].reshape(D, D, order="F")
-    assert np.array_equal(S0, S0.T)
-    for s in (L.STAGE_FACTOR, L.STAGE_RESIDUALS, L.STAGE_PREDICTOR):
-        dev.run_stage(s, P, False)
     ar = oracle.Fp64()
     dx, dy = dev.buffer(L.BUF_DX), dev.buffer(L.BUF_DY)
     dY = inst.flat_to_blocks(dev.buffer(L.BUF_DYMAT), bi)
@@ -372,13 +357,89 @@ def test_c3_full_size_newton_identities(pk, oracle):
     Pm = inst.flat_to_blocks(dev.buffer(L.BUF_P), bi)
     p, d = dev.buffer(L.BUF_PVEC), dev.buffer(L.BUF_DVEC)
     Bst = oracle.stack_B(cons)
-    assert rel_err(Bst.T @ dx, p, np.abs(b).max()) < 1e-9
+    assert rel_err(Bst.T @ dx, p, np.abs(b).max()) < 1e-9, what
+    if words > 1:
+        import mpmath
+        # (decimal strings: np.longdouble(mpf) would round through a double)
+        dxl = np.array([np.longdouble(mpmath.nstr(v, 30)) for v in dev.buffer(L.BUF_DX, exact=True)])
+        pl = np.array([np.longdouble(mpmath.nstr(v, 30)) for v in dev.buffer(L.BUF_PVEC, exact=True)])
+        r = Bst.astype(np.longdouble).T @ dxl - pl
+        assert float(np.max(np.abs(r))) / float(np.abs(b).max()) < 1e-16, what
     lhs = oracle.trace_A(ar, cons, dY, bi) + Bst @ dy
-    assert rel_err(lhs, d, np.abs(oracle.stack_c(cons)).max()) < 1e-8
+    assert rel_err(lhs, d, np.abs(oracle.stack_c(cons)).max()) < 1e-8, what
     WA = oracle.compute_weighted_A(ar, cons, dx, bi)
-    for j in range(0, bi.J, 7):
-        assert rel_err(dX[j][0], WA[j][0] + Pm[j][0]) < 1e-12
-    dev.close()
+    for j in range(0, bi.J, 5):
+        assert rel_err(dX[j][0], WA[j][0] + Pm[j][0]) < 1e-12, what
+    return dX, dY
+
+
+def _full_size_iteration_checks(pk, oracle, cons, b, words=1, gamma=0.7, bitwise_sym=False):
+    """One GPU iteration of a full-size instance, stage by stage, through size-independent
+    properties (MPMP.jl:755-887):
+      * S symmetric after SCHUR (bitwise on the fused rank-1 path, round-off otherwise);
+      * the predictor's and the corrector's Newton identities (_newton_identities);
+      * STEP: alpha_p, alpha_d in (0, 1]; lambda_min of L^-1 dM L^-T of every block recomputed on
+        the host (scipy eigh of the pencil (dM, M), the same spectrum) and the device's minimum
+        over blocks equal to it to 1e-10 relative; alpha = min(1, -gamma/lambda_min)
+        (MPMP.jl:1893-1897) to 1e-10;
+      * UPDATE: X + alpha_p dX and Y + alpha_d dY, and both Cholesky-factorisable."""
+    import scipy.linalg as sla
+    from clrsdp_amd import _lib as L
+    bi = pk.get_block_info(cons)
+    dev = pk.DeviceSolver(cons, b, bi, precision_words=words)
+    try:
+        P = pk.make_params("0.3", "0.1", str(gamma), 0)
+        dev.set_state(*pk.initial_point(bi, 100.0, 100.0))
+        for _ in range(2):
+            dev.iterate(P, False)
+        for s in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR):
+            dev.run_stage(s, P, False)
+        S = dev.buffer(L.BUF_S)
+        D = bi.dim_S[0]
+        S0 = np.asarray(S[:D * D], dtype=float).reshape(D, D, order="F")
+        if bitwise_sym:
+            assert np.array_equal(S0, S0.T)
+        assert np.max(np.abs(S0 - S0.T)) <= 1e-14 * np.max(np.abs(S0))
+        for s in (L.STAGE_FACTOR, L.STAGE_RESIDUALS, L.STAGE_PREDICTOR):
+            dev.run_stage(s, P, False)
+        _newton_identities(pk, oracle, dev, cons, b, bi, words, "predictor")
+        for s in (L.STAGE_CORRECTOR_R, L.STAGE_CORRECTOR):
+            dev.run_stage(s, P, False)
+        dX, dY = _newton_identities(pk, oracle, dev, cons, b, bi, words, "corrector")
+        _, X, _, Y = dev.get_state()
+        dev.run_stage(L.STAGE_STEP, P, False)
+        sc = dev.buffer(L.BUF_SCALARS)
+        a_p, a_d = float(sc[L.SC["alpha_p"]]), float(sc[L.SC["alpha_d"]])
+        assert 0.0 < a_p <= 1.0 and 0.0 < a_d <= 1.0, (a_p, a_d)
+        for M, dM, key, a in ((X, dX, "mineig_X", a_p), (Y, dY, "mineig_Y", a_d)):
+            lam = [sla.eigh(dM[j][l], M[j][l], eigvals_only=True)[0]
+                   for j in range(bi.J) for l in range(len(M[j]))]
+            ref = min(lam)
+            scale = max(abs(v) for v in lam)
+            got = float(sc[L.SC[key]])
+            assert abs(got - ref) <= 1e-10 * scale, (key, got, ref)
+            a_ref = 1.0 if ref > -gamma else -gamma / ref
+            assert abs(a - a_ref) <= 1e-10 * a_ref, (key, a, a_ref)
+        dev.run_stage(L.STAGE_UPDATE, P, False)
+        _, X1, _, Y1 = dev.get_state()
+        for M, dM, M1, a in ((X, dX, X1, a_p), (Y, dY, Y1, a_d)):
+            for j in range(bi.J):
+                for l in range(len(M[j])):
+                    assert rel_err(M1[j][l], M[j][l] + a * dM[j][l]) < 1e-13
+                    np.linalg.cholesky(np.asarray(M1[j][l], dtype=float))
+        return a_p, a_d
+    finally:
+        dev.close()
+
+
+def test_c3_full_size_newton_identities(pk, oracle):
+    """At the bench size (64 clusters x 128x128 blocks, rank 1, n_y = 128) one GPU iteration
+    through every stage: S symmetric (bitwise), the predictor's and the corrector's Newton
+    identities, the step lengths against the host's lambda_min of every block's L^-1 dM L^-T,
+    and the updated X, Y positive definite (_full_size_iteration_checks)."""
+    cons, b = pk.synth(seed=0, J=64, delta=128, rank=1, n_y=128)
+    a_p, a_d = _full_size_iteration_checks(pk, oracle, cons, b, bitwise_sym=True)
+    print("C3 alpha_p", a_p, "alpha_d", a_d)
 
 
 def _sp_real_deviation(pk, words):
@@ -522,48 +583,11 @@ def test_save_restore_state_replays_bitwise(pk):
 @pytest.mark.parametrize("words", [1, 2])
 def test_c2_c4_full_size_newton_identities(pk, oracle, words):
     """Config 2 (fp64) and config 4 (the C2 instance at double-double) at their full size (16
-    clusters x 64x64 blocks, rank 2, n_y = 64): the size-independent identities of one GPU
-    iteration, as for C3 -- B^T dx = p, Tr(A_* dY) + B dy = d, dX = P + sum dx_i A_i, S
-    symmetric.  At double-double B^T dx = p is checked in extended precision (longdouble, all
-    limbs of dx) to 1e-16, below what an fp64 solve reaches; the trace and weighted-A identities
-    use the fp64 oracle."""
-    from clrsdp_amd import _lib as L
-    from clrsdp_amd import instance as inst
+    clusters x 64x64 blocks, rank 2, n_y = 64): the checks of the C3 test through every stage.
+    At double-double B^T dx = p is checked in extended precision (longdouble, all limbs of dx)
+    to 1e-16, below what an fp64 solve reaches; the trace, weighted-A and step-length checks use
+    fp64 (the leading limbs).  (Rank 2: the rank-group sums of the general pairing leave S
+    symmetric to round-off, not bitwise as the fused rank-1 path of C3.)"""
     cons, b = pk.synth(seed=0, J=16, delta=64, rank=2, n_y=64)
-    bi = pk.get_block_info(cons)
-    dev = pk.DeviceSolver(cons, b, bi, precision_words=words)
-    P = pk.make_params("0.3", "0.1", "0.7", 0)
-    dev.set_state(*pk.initial_point(bi, 100.0, 100.0))
-    for _ in range(2):
-        dev.iterate(P, False)
-    for s in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR):
-        dev.run_stage(s, P, False)
-    S = dev.buffer(L.BUF_S)
-    D = bi.dim_S[0]
-    S0 = np.asarray(S[:D * D], dtype=float).reshape(D, D, order="F")
-    # (rank 2: the rank-group sums of the general pairing leave S symmetric to round-off, not
-    # bitwise as the fused rank-1 path of C3)
-    assert np.max(np.abs(S0 - S0.T)) <= 1e-14 * np.max(np.abs(S0))
-    for s in (L.STAGE_FACTOR, L.STAGE_RESIDUALS, L.STAGE_PREDICTOR):
-        dev.run_stage(s, P, False)
-    ar = oracle.Fp64()
-    dx, dy = dev.buffer(L.BUF_DX), dev.buffer(L.BUF_DY)
-    dY = inst.flat_to_blocks(dev.buffer(L.BUF_DYMAT), bi)
-    dX = inst.flat_to_blocks(dev.buffer(L.BUF_DXMAT), bi)
-    Pm = inst.flat_to_blocks(dev.buffer(L.BUF_P), bi)
-    p, d = dev.buffer(L.BUF_PVEC), dev.buffer(L.BUF_DVEC)
-    Bst = oracle.stack_B(cons)
-    assert rel_err(Bst.T @ dx, p, np.abs(b).max()) < 1e-9
-    if words > 1:
-        import mpmath
-        # (decimal strings: np.longdouble(mpf) would round through a double)
-        dxl = np.array([np.longdouble(mpmath.nstr(v, 30)) for v in dev.buffer(L.BUF_DX, exact=True)])
-        pl = np.array([np.longdouble(mpmath.nstr(v, 30)) for v in dev.buffer(L.BUF_PVEC, exact=True)])
-        r = Bst.astype(np.longdouble).T @ dxl - pl
-        assert float(np.max(np.abs(r))) / float(np.abs(b).max()) < 1e-16
-    lhs = oracle.trace_A(ar, cons, dY, bi) + Bst @ dy
-    assert rel_err(lhs, d, np.abs(oracle.stack_c(cons)).max()) < 1e-8
-    WA = oracle.compute_weighted_A(ar, cons, dx, bi)
-    for j in range(0, bi.J, 5):
-        assert rel_err(dX[j][0], WA[j][0] + Pm[j][0]) < 1e-12
-    dev.close()
+    a_p, a_d = _full_size_iteration_checks(pk, oracle, cons, b, words)
+    print("C2/C4 words", words, "alpha_p", a_p, "alpha_d", a_d)
