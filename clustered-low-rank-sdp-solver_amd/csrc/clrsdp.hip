@@ -200,6 +200,11 @@ static inline bool env_on(const char* name) {
   const char* e = std::getenv(name);
   return e && e[0] != '0';
 }
+// a default-on switch is off only when set to a value starting with '0'
+static inline bool env_off(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] == '0';
+}
 
 // work enqueued on another stream for one scope: `stream` is restored when the scope ends,
 // also when a launch inside throws (a capture-abort path relies on `stream` being the main one)
@@ -429,6 +434,40 @@ struct GemmPlan : PlanBase {
       else if (!ta && tb) gemm_valu<T, false, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else gemm_valu<T, true, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
     }
+    HIPCHK(hipGetLastError());
+  }
+};
+
+// Two dependent products of every block as one launch by column strips (chain_f64, fp64,
+// uniform n x n blocks with n <= 128): T = a1 A1 op(B1)[:, S] + b1 C1[:, S], O[:, S] = A2 T
+struct ChainPlan {
+  bool on = false, tb1 = false, sym = false, trace = false;
+  ChainGemm u{};
+  // one pointer set per arena; the blocks sit at stride n^2 (checked by the caller)
+  void set(int half, const double* A1, const double* B1, const double* C1, const double* A2,
+           double* O) {
+    u.A1[half] = A1; u.B1[half] = B1; u.C1[half] = C1; u.A2[half] = A2; u.O[half] = O;
+  }
+  void init(int n, int nb, int halves, bool tb, bool sy) {
+    on = true;
+    tb1 = tb;
+    sym = sy;
+    u.n = n;
+    u.lda1 = u.ldb1 = u.ldc1 = u.lda2 = u.ldo = n;
+    u.sA1 = u.sB1 = u.sC1 = u.sA2 = u.sO = (long long)n * n;
+    u.P1 = nb;
+    u.P = nb * halves;
+    if (halves == 1) set(1, nullptr, nullptr, nullptr, nullptr, nullptr);
+    for (const void* k : {(const void*)chain_f64<false, false>, (const void*)chain_f64<true, true>,
+                          (const void*)chain_f64<false, false, true>})
+      HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chain::LDS));
+  }
+  void launch(hipStream_t s, double a1, double b1) const {
+    const unsigned grid = (unsigned)(u.P * (int)cdiv(trace ? u.NC : u.n, chain::NS));
+    if (trace) chain_f64<false, false, true><<<grid, 512, chain::LDS, s>>>(u, a1, b1);
+    else if (tb1 && sym) chain_f64<true, true><<<grid, 512, chain::LDS, s>>>(u, a1, b1);
+    else if (!tb1 && !sym) chain_f64<false, false><<<grid, 512, chain::LDS, s>>>(u, a1, b1);
+    else throw ClrsdpError{CLRSDP_E_ARG, "chain_f64: unsupported variant"};
     HIPCHK(hipGetLastError());
   }
 };
@@ -920,6 +959,8 @@ struct Solver final : HandleBase {
   bool reg_blk = false, reg_S = false, reg_Q = false;
   CholInvPlan<T> ci_XY, ci_S, ci_S22, ci_Q;
   GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2, q_qinv, q_qdy;
+  // fp64, uniform blocks: Z, dY and the step-length products as one strip-chain launch each
+  ChainPlan c_Z, c_dY, c_step, c_trZ;
   // fp64 FACTOR with every dim_S <= 256 (fac2): f_a = {W = L^-1 B | L21^T = L11^-1 S12, W1} and
   // f_b = {W^T W | S22 - L21 L21^T, W1^T W1, B2 - L21 W1} as mixed batches, then (dim_S > 128)
   // chol_inv(S22), f_c: W2 = L22^-1 B2', f_d: slab += W2^T W2 (measured 1% faster than one
@@ -1314,7 +1355,35 @@ struct Solver final : HandleBase {
     }
     for (const LBlk& b : lb) ci_XY.add(Y + b.off, b.n, b.n, LY + b.off, b.n);
     for (const LBlk& b : lb) e_XY.add(tC + b.off, b.n, b.n);
+    if constexpr (std::is_same<T, double>::value) {
+      // the strip chains need one block size n <= 128 at stride n^2 (one cluster shape: C3 and
+      // its shards); by default taken for 64 < n (C2's n = 64 keeps the tiled GEMMs); Z only for
+      // m = 1 (no symmetrisation of Z); CLRSDP_CHAIN=0 / 1 forces either
+      const char* ec = std::getenv("CLRSDP_CHAIN");
+      bool uni_blk = !lb.empty() && !anyMgt1;
+      for (size_t q = 0; q < lb.size() && uni_blk; ++q)
+        uni_blk = lb[q].n == lb[0].n && lb[q].off == lb[0].off + (int64_t)q * lb[0].n * lb[0].n;
+      const int n0 = lb.empty() ? 0 : lb[0].n;
+      const bool chains = uni_blk && n0 <= 128 && reg_blk && !(ec && ec[0] == '0') &&
+                          ((ec && ec[0] == '1') || n0 > 64);
+      if (chains) {
+        const int nbk = (int)lb.size();
+        c_Z.init(n0, nbk, 1, false, false);
+        c_Z.set(0, P, Y, R, Xinv, Z);            // Z = X^-1 (P Y - R)
+        c_dY.init(n0, nbk, 1, false, false);
+        c_dY.set(0, dX, Y, R, Xinv, dY);         // dY = X^-1 (R - dX Y)
+        c_step.init(n0, nbk, 2, true, true);
+        c_step.set(0, dX, LX, nullptr, LX, tB);  // L_X^-1 dX L_X^-T
+        c_step.set(1, dY, LY, nullptr, LY, tC);  // L_Y^-1 dY L_Y^-T
+      }
+    }
     n_blk_m = (int)bdm.size();
+    if (std::is_same<T, double>::value && !env_off("CLRSDP_SYM_TILES")) {
+      int nmx = 0;
+      for (const LBlk& b : lb) nmx = std::max(nmx, b.n);
+      const int nt = (nmx + 31) / 32;
+      sym_pairs = nt * (nt + 1) / 2;
+    }
     d_blk = descs.own(bd);
     if (n_blk_m) d_blk_m = descs.own(bdm);
     d_ayd = descs.own(ayd);
@@ -1335,6 +1404,30 @@ struct Solver final : HandleBase {
     }
     d_pair = descs.own(pd);
     d_scale = descs.own(sd);
+    // U = Z V and the column sums of the right-hand side in one launch (chain_f64 TRACE): with
+    // the Z chain, trivial tuples and every block's K, lambda and tuple slices at fixed strides
+    if constexpr (std::is_same<T, double>::value) {
+      bool tr = c_Z.on && trivial_tuples && (int)pd.size() == (int)lb.size();
+      for (size_t q = 0; q < pd.size() && tr; ++q)
+        tr = pd[q].K == pd[0].K && pd[q].delta == lb[0].n && pd[q].v_off == pd[0].v_off + (long long)q * pd[0].delta * pd[0].K &&
+             (long long)pd[q].lam_off == pd[0].lam_off + (long long)q * pd[0].K &&
+             (long long)pd[q].x_off == pd[0].x_off + (long long)q * pd[0].K;
+      if (tr) {
+        c_trZ.init(lb[0].n, (int)lb.size(), 1, false, false);
+        c_trZ.trace = true;
+        c_trZ.set(0, Z, V + pd[0].v_off, nullptr, nullptr, nullptr);
+        c_trZ.u.ldb1 = pd[0].delta;
+        c_trZ.u.sB1 = (long long)pd[0].delta * pd[0].K;
+        c_trZ.u.NC = pd[0].K;
+        c_trZ.u.lam = lam + pd[0].lam_off;
+        c_trZ.u.sLam = pd[0].K;
+        c_trZ.u.din = dvec + pd[0].x_off;
+        c_trZ.u.rout = rhs + pd[0].x_off;
+        c_trZ.u.sX = pd[0].K;
+        c_trZ.u.c_in = -1.0;  // rhs_x = -d - Tr(A_* Z)  (MPMP.jl:1733-1739)
+        c_trZ.u.c_agg = -1.0;
+      }
+    }
     // trivial tuples + fp64 + the fused Schur layout: x_i / dx_i of column p is entry p of the
     // cluster's slice, lambda_p entry p of the block's
     wa_fused = std::is_same<T, double>::value && trivial_tuples && fast_schur;
@@ -1784,9 +1877,14 @@ struct Solver final : HandleBase {
   void fill(T* out, double v, int64_t n) {
     if (n > 0) vec_fill<T><<<cdiv(n, 256), 256, 0, stream>>>(out, v, n);
   }
+  int sym_pairs = 0;  // lower 32x32 tiles of the largest local block (blk_sym_tiles grid)
   void sym(T* out, const T* Zm, int mode, bool only_m = false) {
     if (only_m) {
       if (n_blk_m) blk_sym2<T><<<dim3(n_blk_m, 32), 128, 0, stream>>>(d_blk_m, out, Zm, mode);
+    } else if (std::is_same<T, double>::value && mode == 0 && nb() && sym_pairs) {
+      // (fp64: coalesced tile pairs; CLRSDP_SYM_TILES=0 keeps blk_sym2)
+      blk_sym_tiles<<<dim3(nb(), sym_pairs), 256, 0, stream>>>(
+          d_blk, reinterpret_cast<double*>(out), reinterpret_cast<const double*>(Zm));
     } else if (nb()) {
       blk_sym2<T><<<dim3(nb(), 32), 128, 0, stream>>>(d_blk, out, Zm, mode);
     }
@@ -2169,19 +2267,25 @@ struct Solver final : HandleBase {
     seg(CLRSDP_INNER_Z, [&] { direction_Z_(); });
   }
   void direction_Z_() {
-    p_PY.launch(stream, 1.0, -1.0);
-    p_Z.launch(stream, 1.0, 0.0);
+    if (c_Z.on) {
+      c_Z.launch(stream, 1.0, -1.0);
+    } else {
+      p_PY.launch(stream, 1.0, -1.0);
+      p_Z.launch(stream, 1.0, 0.0);
+    }
     // Z is only consumed by trace_A: v^T Z v = v^T sym(Z) v, so the symmetrisation
     // (MPMP.jl:1704-1716) matters only for the off-diagonal (r != s) blocks of m > 1
     if (anyMgt1) sym(Z, Z, 0);
-    p_trU_Z.launch(stream, 1.0, 0.0);
+    if (!c_trZ.on) p_trU_Z.launch(stream, 1.0, 0.0);  // (else U stays on chip, direction_rhs_)
   }
   // rhs_x = -d - Tr(A_* Z)   (MPMP.jl:1733-1739)
   void direction_rhs() {
     seg(CLRSDP_INNER_RHS_X, [&] { direction_rhs_(); });
   }
   void direction_rhs_() {
-    if (trivial_tuples) {
+    if (c_trZ.on) {
+      c_trZ.launch(stream, 1.0, 0.0);   // rhs = -d - lambda (V^T Z V)_tt, U = Z V on chip
+    } else if (trivial_tuples) {
       dim3 g(cdiv(max_K, 4), n_pair);
       colsum_rhs<T><<<g, 256, 0, stream>>>(d_pair, TU, V, lam, dvec, -1.0, nullptr, 0.0, -1.0, rhs);
     } else {
@@ -2196,8 +2300,12 @@ struct Solver final : HandleBase {
     seg(CLRSDP_INNER_DX, [&] { weighted_A(dx, p_wA_dX, dX, 1.0); });
     // dY = sym(X^-1 (R - dX Y))
     seg(CLRSDP_INNER_DY, [&] {
-      p_dXY.launch(stream, -1.0, 1.0);
-      p_dY.launch(stream, 1.0, 0.0);
+      if (c_dY.on) {
+        c_dY.launch(stream, -1.0, 1.0);
+      } else {
+        p_dXY.launch(stream, -1.0, 1.0);
+        p_dY.launch(stream, 1.0, 0.0);
+      }
       sym(dY, dY, 0);
     });
   }
@@ -2322,8 +2430,12 @@ struct Solver final : HandleBase {
   void st_step(const clrsdp_params* prm, int pd_feas) {
     if (reg_blk) {
       // L_X^-1, L_Y^-1 from the X^-1 stage;  M = L^-1 dM L^-T on MFMA; one eigen launch
-      q_sx1.launch(stream, 1.0, 0.0);             // X and Y blocks together
-      q_sx2.launch(stream, 1.0, 0.0);
+      if (c_step.on) {
+        c_step.launch(stream, 1.0, 0.0);          // X and Y blocks together, one launch
+      } else {
+        q_sx1.launch(stream, 1.0, 0.0);           // X and Y blocks together
+        q_sx2.launch(stream, 1.0, 0.0);
+      }
       e_XY.eigmin(stream, eigX);
     } else {
       // X: L_X from the X^-1 stage

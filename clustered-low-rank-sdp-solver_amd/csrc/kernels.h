@@ -342,6 +342,241 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double 
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// chain_f64: two dependent products of one block as ONE launch, by column strips,
+//     T = a1 A1 op(B1)[:, S] + b1 C1[:, S]        (stage 1, n x NS, kept on chip)
+//     O[:, S] = A2 T                              (stage 2)
+// for every problem p of a uniform batch (n x n blocks, n <= 128, all at constant strides; a
+// second pointer set for problems p >= P1, so the X and the Y blocks of the step length share
+// one launch).  Each strip S of NS = 32 columns depends on its own strip of T only, so the
+// intermediate never goes to HBM and the second product does not wait for a whole launch:
+//   Z  = X^-1 (P Y - R)          (compute_search_direction, MPMP.jl:1698-1716)
+//   dY = X^-1 (R - dX Y)         (MPMP.jl:1789-1805; symmetrised afterwards)
+//   L^-1 dM L^-T = L^-1 (dM (L^-1[S, :])^T)   (compute_step_length, MPMP.jl:1853-1856), SYM:
+//        the strip's lower part and its mirror image are written, so the result is exactly
+//        symmetric; stage 1 stops at k = s0 + NS (L^-1 is lower triangular) and stage 2 skips
+//        the row tiles above the strip.
+// 512 threads: wave w owns rows 16w..16w+15 of the strip (two 16x16 MFMA tiles).  The k-slabs
+// of A1 / A2 (128 x 32) and of op(B1) (32 x NS) are double-buffered in LDS (one barrier per
+// slab); T goes from the accumulators to LDS in B-fragment order; the output tile is staged in
+// LDS so every store writes whole 128-row column segments.  Workgroup b takes strip b / P of
+// problem b % P, so all strips of a problem share one XCD's L2 (P a multiple of 8).
+// ------------------------------------------------------------------------------------------
+// TRACE (one stage, the trace_A of the search direction for m = L = rank = 1, MPMP.jl:1537-1578
+// with 1733-1739): U = Z V[:, S] (A1 = Z, B1 = V, n x NC) and, in the epilogue, for every
+// column t of the strip  rout[t] = c_agg lam[t] (U[:, t] . V[:, t]) + c_in din[t]  -- no U in HBM
+// and no separate column-sum launch.
+struct ChainGemm {
+  const double* A1[2];
+  const double* B1[2];
+  const double* C1[2];
+  const double* A2[2];
+  double* O[2];
+  long long sA1, sB1, sC1, sA2, sO;  // per-problem strides (elements) within a pointer set
+  int n, lda1, ldb1, ldc1, lda2, ldo;
+  int P, P1;  // problems; p >= P1 uses pointer set 1 at index p - P1
+  // TRACE only: B1 has NC columns; lam at stride sLam, din / rout at stride sX per problem
+  int NC;
+  const double* lam;
+  const double* din;
+  double* rout;
+  long long sLam, sX;
+  double c_in, c_agg;
+};
+namespace chain {
+constexpr int NS = 32, BK = 32, LA = 128 + 16, LB = NS + 16, SP = NS + 1;
+constexpr int AIMG = BK * LA;        // one A slab image (k-major)
+constexpr int BIMG = BK * LB;        // one op(B1) slab image (k-major)
+constexpr int TOFF = 2 * AIMG;       // T (n x NS, k-major, pitch LB); the B1 images live there
+constexpr int END = TOFF + 128 * LB;
+static_assert(2 * BIMG <= 128 * LB && NS * (BK + 2) <= BIMG && 128 * SP <= 2 * AIMG,
+              "chain LDS regions");
+constexpr size_t LDS = sizeof(double) * END;  // 120 KB
+}  // namespace chain
+
+template <bool TB1, bool SYM, bool TRACE = false>
+__global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, double b1) {
+  using namespace chain;
+  extern __shared__ __attribute__((aligned(16))) double sm_chain[];
+  const int P = u.P, p = blockIdx.x % P, s = blockIdx.x / P;
+  const int hs = p >= u.P1 ? 1 : 0, pl = p - hs * u.P1;
+  const double* A1 = u.A1[hs] + pl * u.sA1;
+  const double* B1 = u.B1[hs] + pl * u.sB1;
+  const double* C1 = u.C1[hs] ? u.C1[hs] + pl * u.sC1 : nullptr;
+  const double* A2 = u.A2[hs] + pl * u.sA2;
+  double* O = u.O[hs] + pl * u.sO;
+  const int n = u.n, s0 = NS * s, NC = TRACE ? u.NC : n;  // NC: columns of op(B1)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lk = lane >> 4;
+  double* Tm = sm_chain + TOFF;
+  // stage 1 stops where L^-1[s0 + j, k] vanishes (SYM); stage 2 skips rows above the strip
+  const int K1 = SYM ? min(n, s0 + NS) : n;
+  const bool live1 = 16 * w < n, live2 = live1 && (!SYM || 16 * w + 15 >= s0);
+  double ra[8], rb[2];
+  auto loadA = [&](const double* A, int ld, int k0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 512 * q, i = e & 127, k = e >> 7;
+      ra[q] = gload(A + min(i, n - 1) + (size_t)min(k0 + k, n - 1) * ld);
+    }
+  };
+  auto storeA = [&](double* S, int k0, int K) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 512 * q, i = e & 127, k = e >> 7;
+      S[k * LA + i] = k0 + k < K ? ra[q] : 0.0;
+    }
+  };
+  auto loadB = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 512 * q;
+      const int k = TB1 ? e >> 5 : e & 31, j = TB1 ? e & 31 : e >> 5;
+      const int gk = min(k0 + k, n - 1), gj = min(s0 + j, NC - 1);
+      rb[q] = gload(B1 + (TB1 ? gj + (size_t)gk * u.ldb1 : gk + (size_t)gj * u.ldb1));
+    }
+  };
+  // op(B1) slab in LDS as it is contiguous in HBM: k-major (pitch LB) for TB1, else j-major
+  // (pitch BK + 2), so the stores are conflict-free and so are the fragment reads
+  auto storeB = [&](double* S, int k0, int K) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 512 * q;
+      const int k = TB1 ? e >> 5 : e & 31, j = TB1 ? e & 31 : e >> 5;
+      S[TB1 ? k * LB + j : j * (BK + 2) + k] = k0 + k < K ? rb[q] : 0.0;
+    }
+  };
+  auto fragB = [&](const double* S, int k, int j) {
+    return TB1 ? S[k * LB + j] : S[j * (BK + 2) + k];
+  };
+  // C1 (TRACE: B1 itself, for the column dot products) in the accumulator layout (rows
+  // 16w + lk + 4r, columns s0 + 16u + lr), loaded up front
+  double cr[2][4];
+  const double* CL = TRACE ? B1 : C1;
+  const int ldcl = TRACE ? u.ldb1 : u.ldc1;
+#pragma unroll
+  for (int u2 = 0; u2 < 2; ++u2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = min(16 * w + lk + 4 * r, n - 1), gj = min(s0 + 16 * u2 + lr, NC - 1);
+      cr[u2][r] = CL ? gload(CL + gi + (size_t)gj * ldcl) : 0.0;
+    }
+  // ---------------- stage 1
+  d4 acc[2];
+  acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+  loadA(A1, u.lda1, 0);
+  loadB(0);
+  storeA(sm_chain, 0, K1);
+  storeB(Tm, 0, K1);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < K1; k0 += BK) {
+    const bool more = k0 + BK < K1;
+    if (more) {
+      loadA(A1, u.lda1, k0 + BK);
+      loadB(k0 + BK);
+    } else if constexpr (!TRACE) {
+      loadA(A2, u.lda2, 0);  // stage 2's first slab in flight during the last MFMAs
+    }
+    const double* As = sm_chain + cur * AIMG;
+    const double* Bs = Tm + cur * BIMG;
+    if (live1) {
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4) {
+        const double af = As[(kk + lk) * LA + 16 * w + lr];
+        const double b0 = fragB(Bs, kk + lk, lr), b1v = fragB(Bs, kk + lk, 16 + lr);
+        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, b0, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, b1v, acc[1], 0, 0, 0);
+      }
+    }
+    if (!more) break;
+    cur ^= 1;  // (the other images were last read before the previous barrier)
+    storeA(sm_chain + cur * AIMG, k0 + BK, K1);
+    storeB(Tm + cur * BIMG, k0 + BK, K1);
+    __syncthreads();
+  }
+  __syncthreads();  // every wave is done with the stage-1 images
+  if constexpr (TRACE) {
+    // column dot products U[:, t] . V[:, t]: the wave's 16 rows (4 registers x the 4 lane
+    // groups lk), then the 8 waves in a fixed order
+    double* part = sm_chain;  // 8 x NS
+#pragma unroll
+    for (int u2 = 0; u2 < 2; ++u2) {
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (16 * w + lk + 4 * r < n) v += acc[u2][r] * cr[u2][r];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lk == 0) part[w * NS + 16 * u2 + lr] = v;
+    }
+    __syncthreads();
+    if (tid < NS && s0 + tid < NC) {
+      double v = part[tid];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v += part[q * NS + tid];
+      const long long g = (long long)pl * u.sX + s0 + tid;
+      double o = u.lam[(long long)pl * u.sLam + s0 + tid] * v * u.c_agg;
+      if (u.din) o += u.din[g] * u.c_in;
+      u.rout[g] = o;
+    }
+    return;
+  }
+  // T = a1 acc + b1 C1 -> LDS as the B operand of stage 2 (rows >= n zero)
+#pragma unroll
+  for (int u2 = 0; u2 < 2; ++u2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * w + lk + 4 * r;
+      Tm[row * LB + 16 * u2 + lr] = row < n ? a1 * acc[u2][r] + b1 * cr[u2][r] : 0.0;
+    }
+  storeA(sm_chain, 0, n);
+  __syncthreads();
+  // ---------------- stage 2: O[:, S] = A2 T
+  acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+  cur = 0;
+  for (int k0 = 0; k0 < n; k0 += BK) {
+    const bool more = k0 + BK < n;
+    if (more) loadA(A2, u.lda2, k0 + BK);
+    const double* As = sm_chain + cur * AIMG;
+    if (live2) {
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4) {
+        const double af = As[(kk + lk) * LA + 16 * w + lr];
+        const double* tb = Tm + (k0 + kk + lk) * LB + lr;
+        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, tb[0], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, tb[16], acc[1], 0, 0, 0);
+      }
+    }
+    if (!more) break;
+    cur ^= 1;
+    storeA(sm_chain + cur * AIMG, k0 + BK, n);
+    __syncthreads();
+  }
+  __syncthreads();  // the A images become the output staging tile
+  double* St = sm_chain;
+#pragma unroll
+  for (int u2 = 0; u2 < 2; ++u2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) St[(16 * w + lk + 4 * r) * SP + 16 * u2 + lr] = acc[u2][r];
+  __syncthreads();
+  {  // columns of the strip as 128-row segments (SYM: the rows on and below the diagonal)
+    const int row = tid & 127;
+#pragma unroll
+    for (int c = 0; c < NS / 4; ++c) {
+      const int cl = (tid >> 7) + 4 * c, col = s0 + cl;
+      if (row < n && col < n && (!SYM || row >= col)) O[row + (size_t)col * u.ldo] = St[row * SP + cl];
+    }
+  }
+  if constexpr (SYM) {  // mirror: O[col][row] for row > col, as NS-long row segments
+    const int cl = tid & (NS - 1), col = s0 + cl;
+#pragma unroll
+    for (int c = 0; c < 128 / (512 / NS); ++c) {
+      const int row = (tid / NS) + (512 / NS) * c;
+      if (row < n && col < n && row > col) O[col + (size_t)row * u.ldo] = St[row * SP + cl];
+    }
+  }
+}
+
 // Mixed batch: op(A), op(B) and (flags bit 2) alpha/beta per problem, so independent products of
 // different shapes share one launch (one uniform branch per workgroup picks the instantiation).
 template <int BK = 32, int NW = 8>
@@ -2105,6 +2340,47 @@ __global__ void blk_sym2(const BlkDesc* __restrict__ bd, T* out, const T* Z, int
   }
 }
 
+// fp64 out = (Z + Z^T)/2 per block (blk_sym2 mode 0) by 32x32 tile pairs staged in LDS, so
+// both the reads and the writes of the transposed tile are coalesced column segments (blk_sym2
+// reads and writes one of the two orientations with a stride of n doubles per lane).
+// grid = (blocks, pairs of a 32-tile grid of the largest block); pair q = (I, J), I >= J, in
+// row-major order over the lower tiles.  The diagonal is copied (as blk_sym2).
+__global__ __launch_bounds__(256) void blk_sym_tiles(const BlkDesc* __restrict__ bd, double* out,
+                                                     const double* Z) {
+  __shared__ double ta[32][33], tb[32][33];
+  const BlkDesc B = bd[blockIdx.x];
+  const int n = B.n, nt = (n + 31) / 32;
+  int I = 0;
+  const int q = blockIdx.y;
+  while ((I + 1) * (I + 2) / 2 <= q) ++I;
+  const int J = q - I * (I + 1) / 2;
+  if (I >= nt) return;
+  const double* z = Z + B.off;
+  double* o = out + B.off;
+  const int r = threadIdx.x & 31, c0 = threadIdx.x >> 5;
+  const int i0 = 32 * I, j0 = 32 * J;
+  // ta = tile (I, J), tb = tile (J, I), each as column segments
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = c0 + 8 * u;
+    const bool a_ok = i0 + r < n && j0 + c < n, b_ok = j0 + r < n && i0 + c < n;
+    ta[c][r] = a_ok ? z[(i0 + r) + (size_t)(j0 + c) * n] : 0.0;
+    tb[c][r] = b_ok ? z[(j0 + r) + (size_t)(i0 + c) * n] : 0.0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = c0 + 8 * u;
+    // (i0 + r, j0 + c) = (A(i0+r, j0+c) + A(j0+c, i0+r)) / 2; tile (J, I) gets its transpose
+    if (i0 + r < n && j0 + c < n) {
+      const bool dg = i0 + r == j0 + c;
+      o[(i0 + r) + (size_t)(j0 + c) * n] = dg ? ta[c][r] : (ta[c][r] + tb[r][c]) * 0.5;
+    }
+    if (I != J && j0 + r < n && i0 + c < n)
+      o[(j0 + r) + (size_t)(i0 + c) * n] = (ta[r][c] + tb[c][r]) * 0.5;
+  }
+}
+
 // X += alpha * dX with alpha = *sc  (skipped when *flag != 0: the state survives a failed step)
 template <class T>
 __global__ void blk_axpy_dev(const BlkDesc* __restrict__ bd, T* X, const T* dX, const T* sc,
@@ -2727,17 +3003,79 @@ __device__ __forceinline__ T fold_wave(const FoldRed<T>& r, int lane) {
   return acc;
 }
 
+// fp64: all folds of a launch at once -- every lane issues its loads of every fold before the
+// first combine (one memory latency instead of one per fold and per 64 elements), then the six
+// butterflies interleaved.  Bitwise fold_wave's result: lane l combines elements l, l+64, ... in
+// order, then the same xor butterfly.
+__device__ __forceinline__ double fold_op(int op, double acc, double v) {
+  if (op == 0) return acc + v;
+  if (op == 3) return v < acc ? v : acc;
+  return v > acc ? v : acc;
+}
+__device__ __forceinline__ void fold_all_f64(const ScalarParams<double>& p, double* sc, int lane) {
+  double acc[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) acc[q] = 0.0;
+  const int nred = p.nred;
+  int maxcnt = 0;
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    if (q < nred) maxcnt = max(maxcnt, p.red[q].cnt);
+  for (int i0 = 0; i0 < maxcnt; i0 += 256) {
+    double v[6][4];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + lane + 64 * u;
+        v[q][u] = (q < nred && i < p.red[q].cnt) ? p.red[q].src[(size_t)i * p.red[q].stride] : 0.0;
+      }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      if (q >= nred) continue;
+      const int op = p.red[q].op, cnt = p.red[q].cnt;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + lane + 64 * u;
+        if (i >= cnt) continue;
+        double x = op == 4 ? fabs(v[q][u]) : v[q][u];
+        acc[q] = (i < 64) ? x : fold_op(op, acc[q], x);  // the lane's first element starts it
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {  // lanes without elements: neutral (sum 0, else element 0)
+    if (q >= nred) continue;
+    if (lane >= p.red[q].cnt && p.red[q].op != 0) {
+      const double x0 = p.red[q].src[0];
+      acc[q] = p.red[q].op == 4 ? fabs(x0) : x0;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      if (q < nred) acc[q] = fold_op(p.red[q].op, acc[q], __shfl_xor(acc[q], o));
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    if (q < nred && lane == 0) sc[p.red[q].dst] = acc[q];
+}
+
 template <class T>
 __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
   const int lane = threadIdx.x;
   for (int e = lane; e < p.zero_n; e += 64) p.zero_ptr[e] = 0;
-  // compile-time indices into the by-value parameter block (a runtime index makes the
-  // compiler copy the whole block to scratch: 104 B/lane at quad-double)
+  if constexpr (sizeof(T) == 8) {
+    fold_all_f64(p, sc, lane);
+  } else {
+    // compile-time indices into the by-value parameter block (a runtime index makes the
+    // compiler copy the whole block to scratch: 104 B/lane at quad-double)
 #pragma unroll
-  for (int q = 0; q < 6; ++q) {
-    if (q < p.nred) {
-      const T v = fold_wave(p.red[q], lane);
-      if (lane == 0) sc[p.red[q].dst] = v;
+    for (int q = 0; q < 6; ++q) {
+      if (q < p.nred) {
+        const T v = fold_wave(p.red[q], lane);
+        if (lane == 0) sc[p.red[q].dst] = v;
+      }
     }
   }
   // any status word set (which == 3): the wave reads them strided, one ballot

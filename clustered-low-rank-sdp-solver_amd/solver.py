@@ -387,11 +387,12 @@ def _terminate(gap, perr, derr, gthr, pthr, dthr, need_p, need_d, out):
 
 
 def log_row(it, t, st, p_obj, d_obj, dual_gap):
-    """One row of the iteration table (MPMP.jl:923-937) as plain floats at every precision: the
-    loop control keeps the gap at full width (an mpmath number at dd/qd), the log and RunInfo.log
-    hold its leading double, like the other columns (the values at full width are in
-    RunInfo.exact with record_exact)."""
-    return (int(it), float(t), float(st.mu), float(p_obj), float(d_obj), float(dual_gap),
+    """One row of the iteration table (MPMP.jl:923-937).  Every column is a float (the leading
+    double of the device's value) except the gap, which is the loop control's own value: a float
+    at fp64, the full-width mpmath number at dd/qd (the value terminate() compared, MPMP.jl:
+    942-945, 1147-1173); the other columns at full width are in RunInfo.exact (record_exact)."""
+    gap = dual_gap if not isinstance(dual_gap, (float, int, np.floating)) else float(dual_gap)
+    return (int(it), float(t), float(st.mu), float(p_obj), float(d_obj), gap,
             float(st.P_err), float(st.p_err), float(st.d_err), float(st.alpha_p),
             float(st.alpha_d), float(st.beta_c))
 
@@ -480,7 +481,8 @@ def solverank1sdp(constraints, b, blockinfo: BlockInfo, C=None, b0=0, maxiterati
     reference's pivoted LU once a Cholesky fails, announced like MPMP.jl:776-778).  At
     double-double and quad-double the returned gap and objectives are mpmath numbers at the
     state's full precision (MPMP.jl:1021-1023), not leading limbs; at fp64 they are floats.  The
-    log rows (RunInfo.log) are floats at every precision (:func:`log_row`).
+    log rows (RunInfo.log) are floats except the gap column, which is an mpmath number at dd/qd
+    like the returned gap (:func:`log_row`).
     """
     kw = dict(beta_infeasible=beta_infeasible, beta_feasible=beta_feasible, gamma=gamma,
               omega_p=omega_p, omega_d=omega_d, duality_gap_threshold=duality_gap_threshold,

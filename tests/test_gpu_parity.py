@@ -96,6 +96,20 @@ def test_stage_parity_fp64(pk, oracle, cfg):
     _stage_compare(pk, oracle, cons, b)
 
 
+@pytest.mark.parametrize("cfg", [dict(J=4, delta=20, rank=1, n_y=8), dict(J=2, delta=64, rank=2, n_y=64),
+                                 dict(J=3, delta=100, rank=1, n_y=40), dict(J=2, delta=128, rank=1, n_y=128)],
+                         ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+@pytest.mark.parametrize("chain", ["0", "1"])
+def test_stage_parity_fp64_strip_chains(pk, oracle, cfg, chain, monkeypatch):
+    """The strip-chain launches (chain_f64: Z = X^-1 (P Y - R), dY = X^-1 (R - dX Y), the step
+    length's L^-1 dM L^-T, U = Z V with the right-hand side's column sums) forced on (1) and off
+    (0) for block sizes below one strip (20), not a multiple of the strip (100), rank 2 (no fused
+    trace) and the C3 block: every stage against the oracle at the fp64 tolerance."""
+    monkeypatch.setenv("CLRSDP_CHAIN", chain)
+    cons, b = pk.synth(seed=5, **cfg)
+    _stage_compare(pk, oracle, cons, b)
+
+
 @pytest.mark.parametrize("cfg", CONFIGS_GPU[-3:], ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_stage_parity_fp64_64x64_tiles(pk, oracle, cfg, monkeypatch):
     """The batches of these small instances take the 32x32-tile GEMM (gemm_f64_uni TS = 32);

@@ -232,19 +232,21 @@ def test_device_thresholds_are_exact_limb_sums():
 
 def test_return_and_log_types_per_precision(pk):
     """The public types of solverank1sdp's outputs: the iteration log holds plain
-    floats at every precision, whatever the type of the loop-control gap (an mpmath number at
-    dd/qd, :func:`device_threshold`'s exact comparisons), and the docstring states that the
-    returned gap and objectives are mpmath numbers at dd/qd and floats at fp64."""
+    floats except the gap column, which keeps the loop control's type (a float at fp64, the
+    full-width mpmath number at dd/qd that device_threshold's exact comparisons use), and the
+    docstring states that the returned gap and objectives are mpmath numbers at dd/qd and floats
+    at fp64."""
     import types
 
     import mpmath
     from clrsdp_amd import solver
     st = types.SimpleNamespace(mu=0.5, P_err=1e-3, p_err=2e-3, d_err=3e-3, alpha_p=0.7,
                                alpha_d=0.8, beta_c=0.1)
-    for gap in (1e-5, mpmath.mpf("1e-25"), solver.device_threshold("1e-20", 2)):
+    for gap in (1e-5, np.float64(2e-7), mpmath.mpf("1e-25"), solver.device_threshold("1e-20", 2)):
         row = solver.log_row(3, 0.25, st, mpmath.mpf("1.5"), 1.25, gap)
-        assert type(row[0]) is int and all(type(v) is float for v in row[1:])
-        assert row[5] == float(gap)
+        assert type(row[0]) is int and all(type(v) is float for i, v in enumerate(row) if i not in (0, 5))
+        assert row[5] == gap
+        assert type(row[5]) is (mpmath.mpf if isinstance(gap, mpmath.mpf) else float)
     doc = solver.solverank1sdp.__doc__
     assert "mpmath numbers" in doc and "at fp64 they are floats" in doc
 

@@ -15,6 +15,8 @@ export TMPDIR=/tmp
 bash tools/profile_round.sh $TAG > $OUT/profile.log 2>&1
 cp gpurun_out/prof_$TAG/schur_pmc.json profiles/${TAG}_schur_pmc.json
 cp gpurun_out/prof_$TAG/schur_pmc.json $OUT/schur_pmc.json
+cp gpurun_out/prof_$TAG/kernels_pmc.json profiles/${TAG}_kernels_pmc.json
+cp gpurun_out/prof_$TAG/kernel_summary.txt profiles/${TAG}_c3_kernel_summary.txt
 timeout -k 10 200 python3 bench.py > $OUT/bench_c3_fp64.log 2>&1
 timeout -k 10 200 python3 bench.py --config c2 > $OUT/bench_c2_fp64.log 2>&1
 timeout -k 10 200 python3 bench.py --config c2 --precision 2 > $OUT/bench_c4_dd.log 2>&1
