@@ -464,7 +464,7 @@ struct ChainPlan {
   }
   void launch(hipStream_t s, double a1, double b1) const {
     const unsigned grid = (unsigned)(u.P * (int)cdiv(trace ? u.NC : u.n, chain::NS));
-    if (trace) chain_f64<false, false, true><<<grid, 512, chain::LDS, s>>>(u, a1, b1);
+    if (trace) chain_f64<false, false, true><<<grid, 512, chain::LDS_TRACE, s>>>(u, a1, b1);
     else if (tb1 && sym) chain_f64<true, true><<<grid, 512, chain::LDS, s>>>(u, a1, b1);
     else if (!tb1 && !sym) chain_f64<false, false><<<grid, 512, chain::LDS, s>>>(u, a1, b1);
     else throw ClrsdpError{CLRSDP_E_ARG, "chain_f64: unsupported variant"};
@@ -666,6 +666,19 @@ struct MatPlan : PlanBase {  // potrf / eigmin
   void potrf(hipStream_t s, int* info) const {
     if (h.empty()) return;
     if constexpr (!std::is_same<T, double>::value) {
+      // the look-ahead potrf (chol_lookahead: the pivot chain beside the trailing update, bitwise
+      // chol_packed's factors); CLRSDP_CHOL_LA=0 keeps chol_packed
+      static const bool la = !env_off("CLRSDP_CHOL_LA");
+      if (reg_potrf && la && nmax <= (std::is_same<T, mw::dd>::value ? 128 : 64)) {
+        if (std::is_same<T, mw::dd>::value && nmax > 64)
+          chol_lookahead<T, false, 128><<<(unsigned)h.size(), 1024, 0, s>>>(d, info);
+        else if (std::is_same<T, mw::qd>::value && chol_ldl_on())
+          chol_lookahead<T, true, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, info);
+        else
+          chol_lookahead<T, false, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, info);
+        HIPCHK(hipGetLastError());
+        return;
+      }
       if (reg_potrf) {
         if constexpr (std::is_same<T, mw::dd>::value) {
           if (nmax > 64) {
@@ -966,6 +979,10 @@ struct Solver final : HandleBase {
   // chol_inv(S22), f_c: W2 = L22^-1 B2', f_d: slab += W2^T W2 (measured 1% faster than one
   // W^T W product after W2); f_x1/f_x2: X21 (side stream)
   GemmPlan<T> f_a, f_b, f_c, f_d, f_x1, f_x2;
+  // the 2x2-blocked clusters' {W1 = L11^-1 B1} and {W1^T W1, B2 - L21 W1}: off the chain
+  // chol(S11) -> L21^T -> S22 - L21 L21^T -> chol(S22'), so a loop body runs them on a second side
+  // stream beside it (joined before W2 = L22^-1 B2')
+  GemmPlan<T> f_w, f_w2;
   bool fac2 = false;
   T* B2p = nullptr;
   // weighted A with the column scaling inside the GEMM's slab staging (fp64, every local block
@@ -1037,9 +1054,9 @@ struct Solver final : HandleBase {
   }
   // side stream: the local residuals overlap the Schur factorisation, chol(Q) overlaps the
   // first part of the predictor (iterate only; run_stage stays serial)
-  hipStream_t aux = nullptr;
+  hipStream_t aux = nullptr, aux2 = nullptr;
   hipEvent_t ev_m = nullptr, ev_x = nullptr, ev_s = nullptr, ev_r = nullptr, ev_qa = nullptr,
-             ev_q = nullptr, ev_join = nullptr;
+             ev_q = nullptr, ev_join = nullptr, ev_fa = nullptr, ev_w = nullptr, ev_join2 = nullptr;
   bool pending_q = false;
   float phase_ms[CLRSDP_NUM_STAGES];
 
@@ -1141,9 +1158,16 @@ struct Solver final : HandleBase {
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
     // CLRSDP_ONE_STREAM=1: the side-stream work runs in order on the main stream (experiment:
     // graph-boundary and join idle time against the lost overlap)
-    if (env_on("CLRSDP_ONE_STREAM")) aux = own_stream;
-    else HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21, &ev_ty, &ev_join})
+    if (env_on("CLRSDP_ONE_STREAM")) {
+      aux = aux2 = own_stream;
+    } else {
+      HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+      // CLRSDP_FACTOR_SPLIT=0: FACTOR's W1 products stay on the main stream
+      if (env_off("CLRSDP_FACTOR_SPLIT")) aux2 = own_stream;
+      else HIPCHK(hipStreamCreateWithFlags(&aux2, hipStreamNonBlocking));
+    }
+    for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21, &ev_ty, &ev_join,
+                          &ev_fa, &ev_w, &ev_join2})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
     build_plans();
@@ -1172,11 +1196,13 @@ struct Solver final : HandleBase {
       if (r) (void)hipHostFree(r);
     for (auto& e : ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : seg_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ev_ty, ev_join, ring_ev[0], ring_ev[1]})
+    for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ev_ty, ev_join, ev_fa, ev_w,
+                         ev_join2, ring_ev[0], ring_ev[1]})
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
       if (g) (void)hipGraphExecDestroy(g);
     if (aux && aux != own_stream) (void)hipStreamDestroy(aux);
+    if (aux2 && aux2 != own_stream) (void)hipStreamDestroy(aux2);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 
@@ -1486,10 +1512,10 @@ struct Solver final : HandleBase {
         s11.push_back(MatDesc<T>{S11, D1, D});                                          // S11 <- L11^-1
         // (S21^T, not S12: the fused Schur kernel may assemble only the lower triangle)
         f_a.add_op(false, true, 1.0, 0.0, S11, D, S21, D, nullptr, 0, T12, D1, D1, D2, D1);
-        f_a.add_op(false, false, 1.0, 0.0, S11, D, Bc, D, nullptr, 0, Wc, D, D1, ny, D1);  // W1
+        f_w.add_op(false, false, 1.0, 0.0, S11, D, Bc, D, nullptr, 0, Wc, D, D1, ny, D1);  // W1
         f_b.add_op(true, false, -1.0, 1.0, T12, D1, T12, D1, S22, D, S22, D, D2, D2, D1);  // S22 - L21 L21^T
-        f_b.add_op(true, false, 1.0, 0.0, Wc, D, Wc, D, nullptr, 0, slab, ny, ny, ny, D1); // W1^T W1
-        f_b.add_op(true, false, -1.0, 1.0, T12, D1, Wc, D, Bc + D1, D, B2, D2, D2, ny, D1);  // B2'
+        f_w2.add_op(true, false, 1.0, 0.0, Wc, D, Wc, D, nullptr, 0, slab, ny, ny, ny, D1); // W1^T W1
+        f_w2.add_op(true, false, -1.0, 1.0, T12, D1, Wc, D, Bc + D1, D, B2, D2, D2, ny, D1);  // B2'
         ci_S22.add(S22, D2, D, S22, D);                                                 // S22 <- L22^-1
         f_c.add(S22, D, B2, D2, nullptr, 0, Wc + D1, D, D2, ny, D2);                   // W2 = L22^-1 B2'
         f_d.add(Wc + D1, D, Wc + D1, D, slab, ny, slab, ny, ny, ny, D2);               // slab += W2^T W2
@@ -1555,7 +1581,7 @@ struct Solver final : HandleBase {
     for (GemmPlan<T>* g : {&p_txy, &p_ty, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
-                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &f_a, &f_b, &f_c, &f_d, &f_x1, &f_x2,
+                           &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &f_a, &f_b, &f_c, &f_d, &f_x1, &f_x2, &f_w, &f_w2,
                            &p_wA_Ps, &p_wA_dXs})
       g->finalize();
     for (CholInvPlan<T>* c : {&ci_XY, &ci_S, &ci_S22, &ci_Q}) c->finalize();
@@ -1907,6 +1933,8 @@ struct Solver final : HandleBase {
     p.need_d = need_d;
     p.dim = dimtot;
     p.pd_feas = pd_feas;
+    static const int fold_all = env_off("CLRSDP_FOLD_ALL") ? 0 : 1;
+    p.fold_all = fold_all;
     return p;
   }
   void set_control(const clrsdp_control* c) override {
@@ -2132,8 +2160,25 @@ struct Solver final : HandleBase {
     }
     if (fac2) {                               // fp64: S_j <- L_j^-1 in place, W_j and Q's slabs
       seg(CLRSDP_INNER_CHOL_S, [&] { ci_S.launch(stream, info + info_S0); });  // S / S11 blocks
-      seg(CLRSDP_INNER_CINVB, [&] { f_a.launch(stream, 1.0, 0.0); });          // {L21^T, W1}
-      seg(CLRSDP_INNER_CHOL_S, [&] { f_b.launch(stream, 1.0, 0.0); });         // S22 - L21 L21^T, ...
+      seg(CLRSDP_INNER_CINVB, [&] { f_a.launch(stream, 1.0, 0.0); });          // {L21^T | W}
+      // W1 = L11^-1 B1, then W1^T W1 and B2' = B2 - L21 W1: beside the S22 chain in a loop body
+      const bool split = side_x21 && nc2 && aux2 != stream;
+      auto w_work = [&] {
+        seg(CLRSDP_INNER_CINVB, [&] { f_w.launch(stream, 1.0, 0.0); });
+        seg(CLRSDP_INNER_Q, [&] { f_w2.launch(stream, 1.0, 0.0); });
+      };
+      if (split) {
+        HIPCHK(hipEventRecord(ev_fa, stream));
+        HIPCHK(hipStreamWaitEvent(aux2, ev_fa, 0));
+        {
+          StreamSwitch on_aux2(stream, aux2);
+          w_work();
+        }
+        HIPCHK(hipEventRecord(ev_w, aux2));
+      } else {
+        w_work();
+      }
+      seg(CLRSDP_INNER_CHOL_S, [&] { f_b.launch(stream, 1.0, 0.0); });         // S22 - L21 L21^T | W^T W
       if (nc2) {
         seg(CLRSDP_INNER_CHOL_S, [&] { ci_S22.launch(stream, info + info_S0 + nc()); });
         if (side_x21) {
@@ -2155,6 +2200,7 @@ struct Solver final : HandleBase {
             f_x2.launch(stream, -1.0, 0.0);
           });
         }
+        if (split) HIPCHK(hipStreamWaitEvent(stream, ev_w, 0));
         seg(CLRSDP_INNER_CINVB, [&] { f_c.launch(stream, 1.0, 0.0); });
         seg(CLRSDP_INNER_Q, [&] { f_d.launch(stream, 1.0, 1.0); });
       }
@@ -2180,12 +2226,12 @@ struct Solver final : HandleBase {
   void sum_q_slabs() {
     const int64_t q2 = n_y * n_y;
     if (world == 1 && nc()) {
-      slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(Qslab, nc(), q2, q2, Q);
+      slab_sum4<T><<<cdiv(q2, 64), 256, 0, stream>>>(Qslab, nc(), q2, q2, Q);
     } else {
-      if (nc()) slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(Qslab, nc(), q2, q2, xsend);
+      if (nc()) slab_sum4<T><<<cdiv(q2, 64), 256, 0, stream>>>(Qslab, nc(), q2, q2, xsend);
       else fill(xsend, 0.0, q2);
       exchange(2, q2);
-      slab_sum<T><<<cdiv(q2, 256), 256, 0, stream>>>(xrecv, world, q2, q2, Q);
+      slab_sum4<T><<<cdiv(q2, 64), 256, 0, stream>>>(xrecv, world, q2, q2, Q);
     }
   }
   void factor_q() {
@@ -2238,18 +2284,18 @@ struct Solver final : HandleBase {
   void residuals_finish() {
     const int64_t k = n_y + 2;
     if (world == 1 && nc()) {  // p = b - sum_j B_j^T x_j in one launch; maxima folded
-      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, pvec, bvec, 1.0, -1.0);
+      slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, pvec, bvec, 1.0, -1.0);
       fold(tmpsc, 1, 2, SC_ERR_PMAT);
       fold(tmpsc + 1, 1, 2, SC_ERR_DVEC);
       fold(pvec, (int)n_y, 4, SC_ERR_PVEC);
       flush_scalars();
       return;
     }
-    if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+    if (nc()) slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
     else fill(xsend, 0.0, n_y);
     vlin(xsend + n_y, tmpsc, 1.0, nullptr, 0, nullptr, 0, 2);
     exchange(3, k);
-    slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, k, n_y, uvec);
+    slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(xrecv, world, k, n_y, uvec);
     vlin(pvec, bvec, 1.0, uvec, -1.0, nullptr, 0, n_y);      // p = b - sum B^T x
     reduce_ranks(k, n_y, 2, SC_ERR_PMAT);
     reduce_ranks(k, n_y + 1, 2, SC_ERR_DVEC);
@@ -2344,7 +2390,7 @@ struct Solver final : HandleBase {
         const double* src = pslab;
         int cnt = nc();
         if (!(world == 1 && nc())) {
-          if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+          if (nc()) slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
           else fill(xsend, 0.0, n_y);
           exchange(tag, n_y);
           src = xrecv;
@@ -2364,12 +2410,12 @@ struct Solver final : HandleBase {
       // r = p - sum_j W_j^T t_j  (-> uvec with the explicit Q^-1, -> dyv for the two solves)
       T* rv = reg_Q ? uvec : dyv;
       if (world == 1 && nc()) {  // one launch
-        slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, rv, pvec, 1.0, -1.0);
+        slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, rv, pvec, 1.0, -1.0);
       } else {
-        if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+        if (nc()) slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
         else fill(xsend, 0.0, n_y);
         exchange(tag, n_y);
-        slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, rv, pvec, 1.0, -1.0);
+        slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(xrecv, world, n_y, n_y, rv, pvec, 1.0, -1.0);
       }
       if (pending_q) {  // L_Q^-1 and Q^-1 are being computed on the side stream (iterate)
         HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
@@ -2398,12 +2444,12 @@ struct Solver final : HandleBase {
     tl_t.launch(stream, false);               // t_j = L_j^-1 t_j
     lq_Wt.launch(stream, 1.0, 0.0);           // slab_j = W2_j^T t_j  (B_j^T U_j^-1 t_j)
     if (world == 1 && nc()) {
-      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, uvec, pvec, 1.0, -1.0);
+      slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, uvec, pvec, 1.0, -1.0);
     } else {
-      if (nc()) slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
+      if (nc()) slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
       else fill(xsend, 0.0, n_y);
       exchange(tag, n_y);
-      slab_sum<T><<<cdiv(n_y, 256), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec, pvec, 1.0, -1.0);
+      slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(xrecv, world, n_y, n_y, uvec, pvec, 1.0, -1.0);
     }
     if (pending_q) {
       HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
@@ -2754,6 +2800,8 @@ struct Solver final : HandleBase {
         // ends cleanly and the streams stay usable
         if (aux != stream && hipEventRecord(ev_join, aux) == hipSuccess)
           (void)hipStreamWaitEvent(stream, ev_join, 0);
+        if (aux2 != stream && hipEventRecord(ev_join2, aux2) == hipSuccess)
+          (void)hipStreamWaitEvent(stream, ev_join2, 0);
         (void)hipStreamEndCapture(stream, &graph);
         if (graph) (void)hipGraphDestroy(graph);
         (void)hipGetLastError();

@@ -356,11 +356,14 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double 
 //        the strip's lower part and its mirror image are written, so the result is exactly
 //        symmetric; stage 1 stops at k = s0 + NS (L^-1 is lower triangular) and stage 2 skips
 //        the row tiles above the strip.
-// 512 threads: wave w owns rows 16w..16w+15 of the strip (two 16x16 MFMA tiles).  The k-slabs
-// of A1 / A2 (128 x 32) and of op(B1) (32 x NS) are double-buffered in LDS (one barrier per
-// slab); T goes from the accumulators to LDS in B-fragment order; the output tile is staged in
-// LDS so every store writes whole 128-row column segments.  Workgroup b takes strip b / P of
-// problem b % P, so all strips of a problem share one XCD's L2 (P a multiple of 8).
+// 512 threads: wave w owns rows 16w..16w+15 of the strip (two 16x16 MFMA tiles).  The wave's
+// rows of A1 and A2 are loaded straight into registers in A-fragment order (32 k-steps x one
+// double per lane each: no LDS and no barrier for the A operands), and every load of the launch
+// -- A1, A2, the op(B1) strip and C1 -- is issued at the start, so the kernel sees one memory
+// latency instead of one per k-slab.  op(B1)[:, S] (n x NS) is staged in LDS once, T goes from
+// the accumulators to LDS in B-fragment order, and the output tile is staged in LDS so every
+// store writes whole 128-row column segments.  Workgroup b takes strip b / P of problem b % P,
+// so all strips of a problem share one XCD's L2 (P a multiple of 8).
 // ------------------------------------------------------------------------------------------
 // TRACE (one stage, the trace_A of the search direction for m = L = rank = 1, MPMP.jl:1537-1578
 // with 1733-1739): U = Z V[:, S] (A1 = Z, B1 = V, n x NC) and, in the epilogue, for every
@@ -384,14 +387,15 @@ struct ChainGemm {
   double c_in, c_agg;
 };
 namespace chain {
-constexpr int NS = 32, BK = 32, LA = 128 + 16, LB = NS + 16, SP = NS + 1;
-constexpr int AIMG = BK * LA;        // one A slab image (k-major)
-constexpr int BIMG = BK * LB;        // one op(B1) slab image (k-major)
-constexpr int TOFF = 2 * AIMG;       // T (n x NS, k-major, pitch LB); the B1 images live there
-constexpr int END = TOFF + 128 * LB;
-static_assert(2 * BIMG <= 128 * LB && NS * (BK + 2) <= BIMG && 128 * SP <= 2 * AIMG,
-              "chain LDS regions");
-constexpr size_t LDS = sizeof(double) * END;  // 120 KB
+constexpr int NS = 32, KT = 32;            // strip width; k-steps of 4 for n <= 128
+constexpr int LBK = NS + 16;               // k-major B image pitch (TB1, and T)
+constexpr int LBJ = 128 + 2;               // j-major B image pitch (!TB1)
+constexpr int SP = NS + 1;                 // output staging pitch
+constexpr int BREG = 128 * LBK;            // the op(B1) image (either layout fits)
+static_assert(NS * LBJ <= BREG && 128 * SP <= BREG, "chain LDS regions");
+constexpr int TOFF = BREG, END = 2 * BREG;  // op(B1) image | T image (the staging reuses the first)
+constexpr size_t LDS = sizeof(double) * END;  // 96 KB
+constexpr size_t LDS_TRACE = sizeof(double) * BREG;
 }  // namespace chain
 
 template <bool TB1, bool SYM, bool TRACE = false>
@@ -403,108 +407,79 @@ __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, d
   const double* A1 = u.A1[hs] + pl * u.sA1;
   const double* B1 = u.B1[hs] + pl * u.sB1;
   const double* C1 = u.C1[hs] ? u.C1[hs] + pl * u.sC1 : nullptr;
-  const double* A2 = u.A2[hs] + pl * u.sA2;
-  double* O = u.O[hs] + pl * u.sO;
+  const double* A2 = TRACE ? nullptr : u.A2[hs] + pl * u.sA2;
+  double* O = TRACE ? nullptr : u.O[hs] + pl * u.sO;
   const int n = u.n, s0 = NS * s, NC = TRACE ? u.NC : n;  // NC: columns of op(B1)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lk = lane >> 4;
+  double* Bs = sm_chain;
   double* Tm = sm_chain + TOFF;
   // stage 1 stops where L^-1[s0 + j, k] vanishes (SYM); stage 2 skips rows above the strip
   const int K1 = SYM ? min(n, s0 + NS) : n;
   const bool live1 = 16 * w < n, live2 = live1 && (!SYM || 16 * w + 15 >= s0);
-  double ra[8], rb[2];
-  auto loadA = [&](const double* A, int ld, int k0) {
+  const int arow = min(16 * w + lr, n - 1);
+  // ---------------- every load up front, in the order they are consumed (vmcnt retires in
+  // order, so stage 1 starts when the op(B1) strip and its first A fragments are in): the
+  // op(B1) strip, A1's rows (A fragments), C1, A2's rows
+  double rb[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + 512 * q, i = e & 127, k = e >> 7;
-      ra[q] = gload(A + min(i, n - 1) + (size_t)min(k0 + k, n - 1) * ld);
-    }
-  };
-  auto storeA = [&](double* S, int k0, int K) {
+  for (int q = 0; q < 8; ++q) {
+    const int e = tid + 512 * q;
+    const int k = TB1 ? e >> 5 : e & 127, j = TB1 ? e & 31 : e >> 7;
+    const int gk = min(k, n - 1), gj = min(s0 + j, NC - 1);
+    rb[q] = gload(B1 + (TB1 ? gj + (size_t)gk * u.ldb1 : gk + (size_t)gj * u.ldb1));
+  }
+  double fa1[KT], fa2[TRACE ? 1 : KT];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + 512 * q, i = e & 127, k = e >> 7;
-      S[k * LA + i] = k0 + k < K ? ra[q] : 0.0;
-    }
-  };
-  auto loadB = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int e = tid + 512 * q;
-      const int k = TB1 ? e >> 5 : e & 31, j = TB1 ? e & 31 : e >> 5;
-      const int gk = min(k0 + k, n - 1), gj = min(s0 + j, NC - 1);
-      rb[q] = gload(B1 + (TB1 ? gj + (size_t)gk * u.ldb1 : gk + (size_t)gj * u.ldb1));
-    }
-  };
-  // op(B1) slab in LDS as it is contiguous in HBM: k-major (pitch LB) for TB1, else j-major
-  // (pitch BK + 2), so the stores are conflict-free and so are the fragment reads
-  auto storeB = [&](double* S, int k0, int K) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int e = tid + 512 * q;
-      const int k = TB1 ? e >> 5 : e & 31, j = TB1 ? e & 31 : e >> 5;
-      S[TB1 ? k * LB + j : j * (BK + 2) + k] = k0 + k < K ? rb[q] : 0.0;
-    }
-  };
-  auto fragB = [&](const double* S, int k, int j) {
-    return TB1 ? S[k * LB + j] : S[j * (BK + 2) + k];
-  };
-  // C1 (TRACE: B1 itself, for the column dot products) in the accumulator layout (rows
-  // 16w + lk + 4r, columns s0 + 16u + lr), loaded up front
+  for (int t = 0; t < KT; ++t) {
+    const int k = min(4 * t + lk, n - 1);
+    fa1[t] = gload(A1 + arow + (size_t)k * u.lda1);
+  }
   double cr[2][4];
-  const double* CL = TRACE ? B1 : C1;
-  const int ldcl = TRACE ? u.ldb1 : u.ldc1;
 #pragma unroll
   for (int u2 = 0; u2 < 2; ++u2)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int gi = min(16 * w + lk + 4 * r, n - 1), gj = min(s0 + 16 * u2 + lr, NC - 1);
-      cr[u2][r] = CL ? gload(CL + gi + (size_t)gj * ldcl) : 0.0;
+      cr[u2][r] = (!TRACE && C1) ? gload(C1 + gi + (size_t)gj * u.ldc1) : 0.0;
     }
-  // ---------------- stage 1
+  if constexpr (!TRACE) {
+#pragma unroll
+    for (int t = 0; t < KT; ++t) fa2[t] = gload(A2 + arow + (size_t)min(4 * t + lk, n - 1) * u.lda2);
+  }
+  // op(B1) strip into LDS (k-major for TB1, j-major otherwise: conflict-free stores and reads);
+  // k >= n zeroed (the A fragments beyond n are clamped copies, their products must vanish)
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = tid + 512 * q;
+    const int k = TB1 ? e >> 5 : e & 127, j = TB1 ? e & 31 : e >> 7;
+    Bs[TB1 ? k * LBK + j : j * LBJ + k] = k < K1 ? rb[q] : 0.0;
+  }
+  auto fragB = [&](int k, int j) { return TB1 ? Bs[k * LBK + j] : Bs[j * LBJ + k]; };
+  __syncthreads();
+  // ---------------- stage 1: acc = A1 op(B1)[:, S] (k < K1)
   d4 acc[2];
   acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
-  loadA(A1, u.lda1, 0);
-  loadB(0);
-  storeA(sm_chain, 0, K1);
-  storeB(Tm, 0, K1);
-  __syncthreads();
-  int cur = 0;
-  for (int k0 = 0; k0 < K1; k0 += BK) {
-    const bool more = k0 + BK < K1;
-    if (more) {
-      loadA(A1, u.lda1, k0 + BK);
-      loadB(k0 + BK);
-    } else if constexpr (!TRACE) {
-      loadA(A2, u.lda2, 0);  // stage 2's first slab in flight during the last MFMAs
-    }
-    const double* As = sm_chain + cur * AIMG;
-    const double* Bs = Tm + cur * BIMG;
-    if (live1) {
+  if (live1) {
 #pragma unroll
-      for (int kk = 0; kk < BK; kk += 4) {
-        const double af = As[(kk + lk) * LA + 16 * w + lr];
-        const double b0 = fragB(Bs, kk + lk, lr), b1v = fragB(Bs, kk + lk, 16 + lr);
-        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, b0, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, b1v, acc[1], 0, 0, 0);
-      }
+    for (int t = 0; t < KT; ++t) {
+      if (4 * t >= K1) break;  // (uniform)
+      const double b0 = fragB(4 * t + lk, lr), b1v = fragB(4 * t + lk, 16 + lr);
+      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa1[t], b0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa1[t], b1v, acc[1], 0, 0, 0);
     }
-    if (!more) break;
-    cur ^= 1;  // (the other images were last read before the previous barrier)
-    storeA(sm_chain + cur * AIMG, k0 + BK, K1);
-    storeB(Tm + cur * BIMG, k0 + BK, K1);
-    __syncthreads();
   }
-  __syncthreads();  // every wave is done with the stage-1 images
   if constexpr (TRACE) {
-    // column dot products U[:, t] . V[:, t]: the wave's 16 rows (4 registers x the 4 lane
-    // groups lk), then the 8 waves in a fixed order
-    double* part = sm_chain;  // 8 x NS
+    // column dot products U[:, t] . V[:, t] (V = op(B1), in LDS): the wave's 16 rows (4
+    // registers x the 4 lane groups lk), then the 8 waves in a fixed order
+    __shared__ double part[8 * NS];
 #pragma unroll
     for (int u2 = 0; u2 < 2; ++u2) {
       double v = 0.0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (16 * w + lk + 4 * r < n) v += acc[u2][r] * cr[u2][r];
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * w + lk + 4 * r;
+        if (row < n) v += acc[u2][r] * fragB(row, 16 * u2 + lr);
+      }
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
       if (lk == 0) part[w * NS + 16 * u2 + lr] = v;
@@ -520,59 +495,50 @@ __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, d
       u.rout[g] = o;
     }
     return;
-  }
-  // T = a1 acc + b1 C1 -> LDS as the B operand of stage 2 (rows >= n zero)
+  } else {
+    // T = a1 acc + b1 C1 -> LDS as the B operand of stage 2 (rows >= n zero)
 #pragma unroll
-  for (int u2 = 0; u2 < 2; ++u2)
+    for (int u2 = 0; u2 < 2; ++u2)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 16 * w + lk + 4 * r;
-      Tm[row * LB + 16 * u2 + lr] = row < n ? a1 * acc[u2][r] + b1 * cr[u2][r] : 0.0;
-    }
-  storeA(sm_chain, 0, n);
-  __syncthreads();
-  // ---------------- stage 2: O[:, S] = A2 T
-  acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
-  cur = 0;
-  for (int k0 = 0; k0 < n; k0 += BK) {
-    const bool more = k0 + BK < n;
-    if (more) loadA(A2, u.lda2, k0 + BK);
-    const double* As = sm_chain + cur * AIMG;
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * w + lk + 4 * r;
+        Tm[row * LBK + 16 * u2 + lr] = row < n ? a1 * acc[u2][r] + b1 * cr[u2][r] : 0.0;
+      }
+    __syncthreads();
+    // ---------------- stage 2: O[:, S] = A2 T
+    acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
     if (live2) {
 #pragma unroll
-      for (int kk = 0; kk < BK; kk += 4) {
-        const double af = As[(kk + lk) * LA + 16 * w + lr];
-        const double* tb = Tm + (k0 + kk + lk) * LB + lr;
-        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, tb[0], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, tb[16], acc[1], 0, 0, 0);
+      for (int t = 0; t < KT; ++t) {
+        if (4 * t >= n) break;  // (uniform)
+        const double* tb = Tm + (4 * t + lk) * LBK + lr;
+        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa2[t], tb[0], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa2[t], tb[16], acc[1], 0, 0, 0);
       }
     }
-    if (!more) break;
-    cur ^= 1;
-    storeA(sm_chain + cur * AIMG, k0 + BK, n);
+    // the output tile through LDS (over the op(B1) image: every wave is past its last read of
+    // it, the barrier above), so the stores are 128-row column segments
+    double* St = Bs;
+#pragma unroll
+    for (int u2 = 0; u2 < 2; ++u2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) St[(16 * w + lk + 4 * r) * SP + 16 * u2 + lr] = acc[u2][r];
     __syncthreads();
-  }
-  __syncthreads();  // the A images become the output staging tile
-  double* St = sm_chain;
+    {  // columns of the strip as 128-row segments (SYM: the rows on and below the diagonal)
+      const int row = tid & 127;
 #pragma unroll
-  for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) St[(16 * w + lk + 4 * r) * SP + 16 * u2 + lr] = acc[u2][r];
-  __syncthreads();
-  {  // columns of the strip as 128-row segments (SYM: the rows on and below the diagonal)
-    const int row = tid & 127;
-#pragma unroll
-    for (int c = 0; c < NS / 4; ++c) {
-      const int cl = (tid >> 7) + 4 * c, col = s0 + cl;
-      if (row < n && col < n && (!SYM || row >= col)) O[row + (size_t)col * u.ldo] = St[row * SP + cl];
+      for (int c = 0; c < NS / 4; ++c) {
+        const int cl = (tid >> 7) + 4 * c, col = s0 + cl;
+        if (row < n && col < n && (!SYM || row >= col)) O[row + (size_t)col * u.ldo] = St[row * SP + cl];
+      }
     }
-  }
-  if constexpr (SYM) {  // mirror: O[col][row] for row > col, as NS-long row segments
-    const int cl = tid & (NS - 1), col = s0 + cl;
+    if constexpr (SYM) {  // mirror: O[col][row] for row > col, as NS-long row segments
+      const int cl = tid & (NS - 1), col = s0 + cl;
 #pragma unroll
-    for (int c = 0; c < 128 / (512 / NS); ++c) {
-      const int row = (tid / NS) + (512 / NS) * c;
-      if (row < n && col < n && row > col) O[col + (size_t)row * u.ldo] = St[row * SP + cl];
+      for (int c = 0; c < 128 / (512 / NS); ++c) {
+        const int row = (tid / NS) + (512 / NS) * c;
+        if (row < n && col < n && row > col) O[col + (size_t)row * u.ldo] = St[row * SP + cl];
+      }
     }
   }
 }
@@ -2565,6 +2531,39 @@ __global__ void slab_sum(const T* in, int cnt, long long stride, long long n, T*
   out[e] = acc;
 }
 
+// slab_sum with the slabs split into 4 contiguous chunks (fixed order inside each, then
+// ((c0 + c1) + (c2 + c3))): 256 threads = 64 elements x 4 chunks, each chunk's loads 8 in flight,
+// so a sum over 64 slabs takes two memory latencies instead of eight.  grid = cdiv(n, 64).
+template <class T>
+__device__ __forceinline__ T slab_chunk_sum(const T* in, int i0, int i1, long long stride, long long e) {
+  T acc = T(0.0);
+  int i = i0;
+  for (; i + 7 < i1; i += 8) {
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = in[(size_t)(i + u) * stride + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; i < i1; ++i) acc += in[(size_t)i * stride + e];
+  return acc;
+}
+template <class T>
+__global__ __launch_bounds__(256) void slab_sum4(const T* in, int cnt, long long stride, long long n,
+                                                 T* out, const T* base = nullptr, double cbase = 0.0,
+                                                 double csum = 1.0) {
+  __shared__ T part[4][64];
+  const int el = threadIdx.x & 63, ch = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + el;
+  const int i0 = (int)((long long)cnt * ch / 4), i1 = (int)((long long)cnt * (ch + 1) / 4);
+  part[ch][el] = e < n ? slab_chunk_sum(in, i0, i1, stride, e) : T(0.0);
+  __syncthreads();
+  if (ch != 0 || e >= n) return;
+  T acc = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
+  if (base) acc = base[e] * T(cbase) + acc * T(csum);
+  out[e] = acc;
+}
+
 // dy = Q^-1 r with r = cbase*base + csum*sum_{i<cnt} in[i*stride + .] (slab_sum's order): the
 // slab sum and the Q^-1 GEMV of the block solve (MPMP.jl:1758-1764) in one launch.  Every
 // workgroup forms all of r in LDS (n values, a few KB), then 64 rows of the product: 4 column
@@ -2577,19 +2576,20 @@ __global__ __launch_bounds__(256) void slab_qsolve(const double* __restrict__ in
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_sq[];
   double* r = reinterpret_cast<double*>(smem_sq);  // n
   double* part = r + n;                            // 4 x 64
-  for (int e = threadIdx.x; e < n; e += 256) {
-    double acc = in[e];
-    int i = 1;
-    for (; i + 7 < cnt; i += 8) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = in[(size_t)(i + u) * stride + e];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+  {  // r in slab_sum4's order: 64 elements x 4 slab chunks at a time
+    const int el = threadIdx.x & 63, sc = threadIdx.x >> 6;
+    const int i0 = (int)((long long)cnt * sc / 4), i1 = (int)((long long)cnt * (sc + 1) / 4);
+    for (int e0 = 0; e0 < n; e0 += 64) {
+      const int e = e0 + el;
+      part[sc * 64 + el] = e < n ? slab_chunk_sum(in, i0, i1, stride, e) : 0.0;
+      __syncthreads();
+      if (sc == 0 && e < n) {
+        double acc = (part[el] + part[64 + el]) + (part[128 + el] + part[192 + el]);
+        if (base) acc = base[e] * cbase + acc * csum;
+        r[e] = acc;
+      }
+      __syncthreads();
     }
-    for (; i < cnt; ++i) acc += in[(size_t)i * stride + e];
-    if (base) acc = base[e] * cbase + acc * csum;
-    r[e] = acc;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, ch = threadIdx.x >> 6;
@@ -2900,6 +2900,7 @@ template <class T> struct ScalarParams {
   int need_p, need_d;
   int nred;
   int zero_cy;  // which == 3 without C: <C,Y> = 0
+  int fold_all;  // fp64: fold_all_f64 (all loads of all folds in flight; CLRSDP_FOLD_ALL=0: off)
   int zero_n;   // zero the status words zero_ptr[0..zero_n) (start of an iteration)
   int* zero_ptr;
   int* halt_ptr;  // which == 0: status word "skip this loop body" (device-decided termination)
@@ -3065,8 +3066,8 @@ template <class T>
 __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
   const int lane = threadIdx.x;
   for (int e = lane; e < p.zero_n; e += 64) p.zero_ptr[e] = 0;
-  if constexpr (sizeof(T) == 8) {
-    fold_all_f64(p, sc, lane);
+  if (sizeof(T) == 8 && p.fold_all) {
+    if constexpr (sizeof(T) == 8) fold_all_f64(p, sc, lane);
   } else {
     // compile-time indices into the by-value parameter block (a runtime index makes the
     // compiler copy the whole block to scratch: 104 B/lane at quad-double)

@@ -374,6 +374,195 @@ __global__ __launch_bounds__(NT) void chol_packed(const MatDesc<T>* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------
+// chol_lookahead: the multi-word potrf (A = L L^T in place, INV = false) of chol_packed with a
+// one-column look-ahead, so the serial pivot chain no longer waits for the trailing update.
+// 1024 threads: wave 0 is the CHAIN, waves 1..15 the BULK.  Phase j (one barrier each):
+//   chain: column j+1 as the bulk published it (updated by columns 0..j-1) minus column j's
+//          contribution, its pivot (LDL: d and 1/d by recip_fast; LL^T: sqrt and 1/sqrt by
+//          pivot_sqrt), the scaled column j+1 -> LDS (buffer (j+1) & 1) and to the output;
+//   bulk:  every element of columns >= j+2 minus column j's contribution (chol_packed's
+//          liveness-packed slots, 15 waves), then the owners of column j+2 publish it.
+// The chain's step (one multi-word FMA per lane, the pivot, one product per lane) and the bulk's
+// update run side by side: a phase costs max(chain, bulk) + one barrier, where chol_packed's
+// step costs chain + bulk + two barriers.  Every element sees the same operations in the same
+// order as in chol_packed (column j's term at step j), so the factors are bitwise chol_packed's.
+// LDL (quad-double): A = U D U^T, then L = U D^1/2 with all n square roots side by side.
+// MPMP.jl:1433-1442 / 1499-1505 (the factorisations of S_j and Q; the reference's approx_lu!).
+// ------------------------------------------------------------------------------------------
+template <class T>
+__device__ __forceinline__ T readlane0(const T& v) {
+  T o;
+  const double* s = reinterpret_cast<const double*>(&v);
+  double* d = reinterpret_cast<double*>(&o);
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(T) / 8); ++q) d[q] = readlane_d(s[q], 0);
+  return o;
+}
+template <class T, bool LDL, int NMAX>
+__global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restrict__ mats,
+                                                       int* __restrict__ info) {
+  constexpr int NW = 15;                                 // bulk waves
+  constexpr int SA = (NMAX * (NMAX + 1) / 2 + 63) / 64;  // 64-element slots of the triangle
+  constexpr int KA = (SA + NW - 1) / NW;
+  constexpr int RC = (NMAX + 63) / 64;                   // chain rows per lane
+  __shared__ T colb[2][NMAX];    // scaled column j (LDL: of U), by parity
+  __shared__ T colub[LDL ? 2 : 1][LDL ? NMAX : 1];  // LDL: the unscaled column j
+  __shared__ T nextc[2][NMAX];   // column j+1 as the bulk leaves it, by parity
+  __shared__ T dgl[LDL ? NMAX : 1];
+  __shared__ int fail;
+  const MatDesc<T> d = mats[blockIdx.x];
+  const int n = d.n, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const bool chain = w == 0;
+  const int wb = w - 1;
+  auto wave_max = [](int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return __builtin_amdgcn_readfirstlane(v);
+  };
+  // ---- bulk slots: slot wb + NW k, element e = 64 slot + lane of the column-major triangle
+  T a[KA];
+  int ar[KA], ac[KA], alo[KA], ahi[KA];
+  const int ne = n * (n + 1) / 2;
+#pragma unroll
+  for (int k = 0; k < KA; ++k) {
+    const int e = 64 * (wb + NW * k) + lane;
+    int r = -1, c = -1;
+    if (!chain && e < ne) {
+      int rem = e;
+      c = 0;
+      while (rem >= n - c) {
+        rem -= n - c;
+        ++c;
+      }
+      r = c + rem;
+    }
+    ar[k] = r;
+    ac[k] = c;
+    a[k] = T(0.0);
+    if (c >= 0) a[k] = d.A[r + (size_t)c * d.lda];
+    ahi[k] = chain ? -1 : wave_max(c);
+    alo[k] = chain ? NMAX : -wave_max(c >= 0 ? -c : -NMAX);
+  }
+  // ---- phase -1: the chain factors column 0, the bulk publishes column 1
+  T cv[RC];  // chain: its rows of the current column
+  if (chain) {
+    if (lane == 0) fail = 0;
+#pragma unroll
+    for (int q = 0; q < RC; ++q) {
+      const int r = lane + 64 * q;
+      cv[q] = r < n ? d.A[r] : T(0.0);
+    }
+    const T dn = readlane0(cv[0]);
+    T s, rs;
+    if constexpr (LDL) {
+      rs = recip_fast(dn);
+    } else {
+      pivot_sqrt(dn, s, rs);
+    }
+#pragma unroll
+    for (int q = 0; q < RC; ++q) {
+      const int r = lane + 64 * q;
+      if (r < n) {
+        T o;
+        if constexpr (LDL) {
+          o = r == 0 ? dn : cv[q] * rs;
+          colub[0][r] = cv[q];
+        } else {
+          o = r == 0 ? s : cv[q] * rs;
+        }
+        colb[0][r] = o;
+        d.A[r] = o;
+      }
+    }
+    if (lane == 0) {
+      if constexpr (LDL) dgl[0] = dn;
+      if (!(dn > T(0.0))) fail = 1;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < KA; ++k)
+      if (alo[k] <= 1 && 1 <= ahi[k] && ac[k] == 1) nextc[1][ar[k]] = a[k];
+  }
+  __syncthreads();
+  for (int j = 0; j + 1 < n; ++j) {
+    if (fail) break;
+    const int p = j & 1, p1 = (j + 1) & 1;
+    if (chain) {
+      // column j+1: the published values minus column j's term, the pivot, the scaled column
+      const int c = j + 1;
+      const T cuj = LDL ? colub[p][c] : colb[p][c];
+#pragma unroll
+      for (int q = 0; q < RC; ++q) {
+        const int r = c + lane + 64 * q;
+        cv[q] = r < n ? nextc[p1][r] - colb[p][r] * cuj : T(0.0);
+      }
+      const T dn = readlane0(cv[0]);
+      T s, rs;
+      if constexpr (LDL) {
+        rs = recip_fast(dn);
+      } else {
+        pivot_sqrt(dn, s, rs);
+      }
+#pragma unroll
+      for (int q = 0; q < RC; ++q) {
+        const int r = c + lane + 64 * q;
+        if (r < n) {
+          T o;
+          if constexpr (LDL) {
+            o = r == c ? dn : cv[q] * rs;
+            colub[p1][r] = cv[q];
+          } else {
+            o = r == c ? s : cv[q] * rs;
+          }
+          colb[p1][r] = o;
+          d.A[r + (size_t)c * d.lda] = o;
+        }
+      }
+      if (lane == 0) {
+        if constexpr (LDL) dgl[c] = dn;
+        if (!(dn > T(0.0))) fail = c + 1;
+      }
+    } else {
+      // columns >= j+2 minus column j's term; then the owners of column j+2 publish it
+#pragma unroll
+      for (int k = 0; k < KA; ++k)
+        if (ahi[k] >= j + 2 && ac[k] >= j + 2)
+          a[k] = a[k] - colb[p][ar[k]] * (LDL ? colub[p] : colb[p])[ac[k]];
+      const int c2 = j + 2;
+      if (c2 < n) {
+#pragma unroll
+        for (int k = 0; k < KA; ++k)
+          if (alo[k] <= c2 && c2 <= ahi[k] && ac[k] == c2) nextc[p][ar[k]] = a[k];
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && info) info[blockIdx.x] = fail;
+  __syncthreads();
+  if constexpr (LDL) {
+    // L = U D^1/2: column c times sqrt d_c, the diagonal sqrt d_c (the square roots side by side)
+    if (!fail) {
+      for (int c = tid; c < n; c += 1024) {
+        T s, r;
+        pivot_sqrt(dgl[c], s, r);
+        colb[0][c] = s;
+      }
+    }
+    __syncthreads();
+    if (!fail)
+      for (int e = tid; e < n * n; e += 1024) {
+        const int r = e % n, c = e / n;
+        if (r > c) d.A[r + (size_t)c * d.lda] = d.A[r + (size_t)c * d.lda] * colb[0][c];
+        else if (r == c) d.A[r + (size_t)c * d.lda] = colb[0][c];
+      }
+  }
+  for (int e = tid; e < n * n; e += 1024) {  // zeros above the diagonal
+    const int r = e % n, c = e / n;
+    if (c > r) d.A[r + (size_t)c * d.lda] = T(0.0);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // eigmin_lds: smallest eigenvalue of a symmetric matrix (n <= NMAX), 512 threads.  The matrix
 // is symmetrised into LDS (ld = n), tridiagonalised by Householder reflections (full storage),
 // then one wave runs a 64-point Sturm multisection.
