@@ -388,8 +388,12 @@ struct GemmPlan : PlanBase {
       throw ClrsdpError{CLRSDP_E_ARG, "fused diagonal epilogue is fp64 only"};
     const unsigned grid = (unsigned)t2d.size();
     if (gemv) {  // (tb only with K = 1: B[0] is the vector either way)
-      if (ta) gemv_batched<T, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
-      else gemv_batched<T, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      // fp64: deep load pipelines (CLRSDP_GEMV_DEEP=0: the 8-deep round-4 loops)
+      static const bool deep = !env_off("CLRSDP_GEMV_DEEP");
+      if (ta && deep) gemv_batched<T, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (ta) gemv_batched<T, true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else if (deep) gemv_batched<T, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      else gemv_batched<T, false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       HIPCHK(hipGetLastError());
       return;
     }
@@ -671,11 +675,11 @@ struct MatPlan : PlanBase {  // potrf / eigmin
       static const bool la = !env_off("CLRSDP_CHOL_LA");
       if (reg_potrf && la && nmax <= (std::is_same<T, mw::dd>::value ? 128 : 64)) {
         if (std::is_same<T, mw::dd>::value && nmax > 64)
-          chol_lookahead<T, false, 128><<<(unsigned)h.size(), 1024, 0, s>>>(d, info);
+          chol_lookahead<T, false, false, 128><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info);
         else if (std::is_same<T, mw::qd>::value && chol_ldl_on())
-          chol_lookahead<T, true, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, info);
+          chol_lookahead<T, false, true, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info);
         else
-          chol_lookahead<T, false, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, info);
+          chol_lookahead<T, false, false, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info);
         HIPCHK(hipGetLastError());
         return;
       }
@@ -855,7 +859,13 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
       else go<128>(s, nb, info);
     } else {
       using C = RegCfg<T>;
-      if (chol_packed_on() && nmax <= 64)
+      static const bool la = !env_off("CLRSDP_CHOL_LA");
+      if (la && nmax <= 64) {  // the look-ahead factorisation with L^-1 (bitwise chol_packed's)
+        if (std::is_same<T, mw::qd>::value && chol_ldl_on())
+          chol_lookahead<T, true, true, 64><<<nb, 1024, 0, s>>>(din, dout, dl, info);
+        else
+          chol_lookahead<T, true, false, 64><<<nb, 1024, 0, s>>>(din, dout, dl, info);
+      } else if (chol_packed_on() && nmax <= 64)
         launch_chol_packed<T, true>(nb, s, din, dout, dl, info);
       else
         chol_inv_reg<T, C::TR, C::TC, C::GR, C::GC><<<nb, C::GR * C::GC, 0, s>>>(din, dout, dl, info);
@@ -2140,8 +2150,12 @@ struct Solver final : HandleBase {
     factor_q();
   }
   // side_x21: X21 on the side stream (the loop body), joined before the first solve
+  bool w_split = false;  // the last factor_local ran W1's products on aux2 (ev_w recorded)
+  bool fuse_alpha = false;   // enqueue_iteration: STEP leaves alpha to UPDATE's launch
+  bool alpha_fused = false;  // STEP left it (the next st_update forms it)
   void factor_local(bool side_x21 = false) {
     s_lower = false;  // S now turns into L^-1 (or the LU factors)
+    w_split = false;
     // (inner timing buckets: a mixed batch counts where most of its work is; the reference's
     // chol_S / CinvB / Q split, MPMP.jl:1429-1495)
     if (lu_sq()) {                            // approx_lu! (MPMP.jl:1433-1494)
@@ -2163,6 +2177,7 @@ struct Solver final : HandleBase {
       seg(CLRSDP_INNER_CINVB, [&] { f_a.launch(stream, 1.0, 0.0); });          // {L21^T | W}
       // W1 = L11^-1 B1, then W1^T W1 and B2' = B2 - L21 W1: beside the S22 chain in a loop body
       const bool split = side_x21 && nc2 && aux2 != stream;
+      w_split = split;
       auto w_work = [&] {
         seg(CLRSDP_INNER_CINVB, [&] { f_w.launch(stream, 1.0, 0.0); });
         seg(CLRSDP_INNER_Q, [&] { f_w2.launch(stream, 1.0, 0.0); });
@@ -2499,6 +2514,12 @@ struct Solver final : HandleBase {
       t_sY2.launch(stream, false);
       e_Y.eigmin(stream, eigY);
     }
+    if (world == 1 && nb() && fuse_alpha) {
+      // (a loop body: the minima and alpha are formed by UPDATE's update_state, one launch less)
+      flush_scalars();
+      alpha_fused = true;
+      return;
+    }
     if (world == 1 && nb()) {  // min over the blocks straight into the scalar slots
       fold(eigX, nb(), 3, SC_MINEIG_X);
       fold(eigY, nb(), 3, SC_MINEIG_Y);
@@ -2541,9 +2562,24 @@ struct Solver final : HandleBase {
   void st_update(const clrsdp_params* prm, int pd_feas) {
     // one launch updates x, y, X, Y (guarded by the status words: no update after a failed
     // factorisation) and leaves the partial sums <X,Y> (next MU_R), <c,x> and <b,y>
+    StepAlpha<T> sa{};
+    if (alpha_fused) {
+      sa.eigX = eigX;
+      sa.eigY = eigY;
+      sa.nb = nb();
+      sa.pd_feas = pd_feas;
+      sa.gamma = limbs(prm->gamma);
+      sa.sc = sc;
+      sa.sx = SC_MINEIG_X;
+      sa.sy = SC_MINEIG_Y;
+      sa.sap = SC_ALPHA_P;
+      sa.sad = SC_ALPHA_D;
+      sa.pdslot = SC_PDFEAS;
+      alpha_fused = false;
+    }
     update_state<T><<<RED_G, 256, 0, stream>>>(X, dX, Y, dY, nblk_el, x, dx, nx, cvec, y, dyv, n_y,
                                                bvec, sc + SC_ALPHA_P, sc + SC_ALPHA_D, info,
-                                               info_count, upart);
+                                               info_count, upart, sa);
     if (world == 1 && !hasC) {  // the objectives from the partials, folded into one scalar launch
       zero_cy = true;
       fold(upart + RED_G, RED_G, 0, SC_DOT_CX);
@@ -2703,17 +2739,24 @@ struct Solver final : HandleBase {
     stage(CLRSDP_STAGE_SCHUR, prm, pd_feas);
     // (Z waits for SCHUR although it could start after XINV: beside the MFMA-bound Schur
     // products it only slowed them down, beside FACTOR's latency-bound factorisations it is free)
+    // The predictor's Z first (its MFMA chain fills the CUs that chol(S11) leaves idle), then the
+    // residuals; the right-hand side (U = Z V and its column sums) after FACTOR's side products
+    // W1^T W1 and B2' (ev_w), which are on the critical path to W2 = L22^-1 B2'
     side(ev_s, [&] {
+      direction_Z();
       residuals_rest(true);
       if (keep_res) {
         copy_guarded2(Pres, P, nblk_el, dres, dvec, nx);
       }
-      direction_Z();
-      direction_rhs();
-      HIPCHK(hipEventRecord(ev_r, aux));
     });
     mark(CLRSDP_STAGE_FACTOR);
     factor_local(true);
+    {
+      if (w_split) HIPCHK(hipStreamWaitEvent(aux, ev_w, 0));
+      StreamSwitch on_aux(stream, aux);
+      direction_rhs();
+      HIPCHK(hipEventRecord(ev_r, aux));
+    }
     // side stream: chol(Q) -> L_Q^-1, waited for just before the first Q solve
     HIPCHK(hipEventRecord(ev_qa, main_s));
     HIPCHK(hipStreamWaitEvent(aux, ev_qa, 0));
@@ -2730,10 +2773,15 @@ struct Solver final : HandleBase {
     HIPCHK(hipGetLastError());
     mark(CLRSDP_STAGE_PREDICTOR);
     direction_rest(4);   // Z, U and rhs came from the side stream
+    // (STEP's alpha is formed inside UPDATE's launch; CLRSDP_FUSE_ALPHA=0 keeps the scalar
+    // launch; the per-stage timing mode keeps it so STEP's time includes alpha)
+    static const bool fa = !env_off("CLRSDP_FUSE_ALPHA");
+    fuse_alpha = fa && timing != 1;
     for (int s = CLRSDP_STAGE_CORRECTOR_R; s < CLRSDP_NUM_STAGES; ++s) {
       mark(s);
       stage(s, prm, pd_feas);
     }
+    fuse_alpha = false;
     if (pending_q) {
       HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
       pending_q = false;
@@ -2815,6 +2863,23 @@ struct Solver final : HandleBase {
     HIPCHK(hipGraphLaunch(gexec[g], stream));
   }
 
+  // A sharded body whose capture fails (CLRSDP_GRAPH_RCCL with an RCCL that cannot be captured)
+  // is enqueued eagerly instead, and the handle stays eager from then on; one rank rethrows (its
+  // capture has no collective in it, so a failure there is a real error)
+  void launch_graph_or_eager(const clrsdp_params* prm, int pd_feas) {
+    if (world == 1) {
+      launch_graph(prm, pd_feas);
+      return;
+    }
+    try {
+      launch_graph(prm, pd_feas);
+    } catch (const ClrsdpError& e) {
+      std::fprintf(stderr, "clrsdp: graph capture of the sharded loop body failed (%s); "
+                           "enqueueing it eagerly from now on\n", e.msg.c_str());
+      graph_rccl = false;
+      enqueue_iteration(prm, pd_feas);
+    }
+  }
   int iterate(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) override {
     if (!uploaded) { err = "constraints not uploaded"; return CLRSDP_E_STATE; }
     if (inflight) { err = "iterate with loop bodies in flight (call iterate_wait)"; return CLRSDP_E_STATE; }
@@ -2824,7 +2889,7 @@ struct Solver final : HandleBase {
     }
   }
   int iterate_once(const clrsdp_params* prm, int pd_feas, clrsdp_iter_stats* st) {
-    if (graph_ok()) launch_graph(prm, pd_feas);
+    if (graph_ok()) launch_graph_or_eager(prm, pd_feas);
     else enqueue_iteration(prm, pd_feas);
     res_from_copy = false;
     std::memset(st, 0, sizeof(*st));
@@ -2906,7 +2971,7 @@ struct Solver final : HandleBase {
         HIPCHK(hipEventCreateWithFlags(&ring_ev[i], hipEventDisableTiming));
       }
     }
-    if (graph_ok()) launch_graph(prm, -1);
+    if (graph_ok()) launch_graph_or_eager(prm, -1);
     else enqueue_iteration(prm, -1);
     const int slot = (ring_head + inflight) % 2;
     HIPCHK(hipMemcpyAsync(ring_host[slot], stat_dev, stat_bytes, hipMemcpyDeviceToHost, stream));

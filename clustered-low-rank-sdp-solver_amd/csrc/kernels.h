@@ -760,7 +760,7 @@ __device__ __forceinline__ T row16_sum_t(T v) {
 //   TA: wave w owns 16 outputs (columns); lane (k-offset kk = lane & 15, column c4 = lane >> 4)
 //       streams 4 columns at once (16 consecutive k per column per load instruction), 4 column
 //       groups x 2 k-steps of loads in flight; each column sum is a 16-lane DPP reduction.
-template <class T, bool TA>
+template <class T, bool TA, bool DEEP = true>
 __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restrict__ descs,
                                                     const TileRef* __restrict__ t2d, double alpha,
                                                     double beta) {
@@ -776,21 +776,40 @@ __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restric
     const int r = tid & 63, g = tid >> 6, i = o0 + r;
     const int ic = min(i, d.M - 1);
     T acc0 = T(0.0), acc1 = T(0.0);
-    int k = g;
-    for (; k + 28 < K; k += 32) {
-      T a[8], xv[8];
+    if constexpr (sizeof(T) == 8 && DEEP) {
+      // fp64: 32 elements of the row in flight per thread (a GEMV is a stream: the bytes in
+      // flight per CU, not the FMAs, set its rate), the tail by clamped loads times zero
+      for (int k0 = g; k0 < K; k0 += 128) {
+        T a[32], xv[32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        a[u] = A[ic + (size_t)(k + 4 * u) * d.lda];
-        xv[u] = x[k + 4 * u];
-      }
+        for (int u = 0; u < 32; ++u) {
+          const int k = min(k0 + 4 * u, K - 1);
+          a[u] = A[ic + (size_t)k * d.lda];
+          xv[u] = k0 + 4 * u < K ? x[k] : T(0.0);
+        }
 #pragma unroll
-      for (int u = 0; u < 8; u += 2) {
-        acc0 += a[u] * xv[u];
-        acc1 += a[u + 1] * xv[u + 1];
+        for (int u = 0; u < 32; u += 2) {
+          acc0 += a[u] * xv[u];
+          acc1 += a[u + 1] * xv[u + 1];
+        }
       }
+    } else {
+      int k = g;
+      for (; k + 28 < K; k += 32) {
+        T a[8], xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          a[u] = A[ic + (size_t)(k + 4 * u) * d.lda];
+          xv[u] = x[k + 4 * u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+          acc0 += a[u] * xv[u];
+          acc1 += a[u + 1] * xv[u + 1];
+        }
+      }
+      for (; k < K; k += 4) acc0 += A[ic + (size_t)k * d.lda] * x[k];
     }
-    for (; k < K; k += 4) acc0 += A[ic + (size_t)k * d.lda] * x[k];
     part[g][r] = acc0 + acc1;
     __syncthreads();
     if (g == 0 && i < d.M) {
@@ -806,6 +825,21 @@ __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restric
     for (int q = 0; q < 4; ++q) col[q] = A + (size_t)min(jb + 4 * q + c4, d.M - 1) * d.lda;
     T acc[4] = {T(0.0), T(0.0), T(0.0), T(0.0)};
     int k = kk;
+    if constexpr (sizeof(T) == 8 && DEEP) {  // fp64: 8 k-steps (32 column elements) in flight per lane
+      for (; k + 112 < K; k += 128) {
+        T av[4][8], xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          xv[u] = x[k + 16 * u];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) av[q][u] = col[q][k + 16 * u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] += av[q][u] * xv[u] + av[q][u + 1] * xv[u + 1];
+      }
+    }
     for (; k + 16 < K; k += 32) {
       T a0[4], a1[4];
       const T x0 = x[k], x1 = x[k + 16];
@@ -861,6 +895,36 @@ __device__ __forceinline__ void flat_chunk(long long n, int blk, int nblk, long 
 // workgroup the partial <X,Y> of the new state (the next iteration's mu, with flat_reduce's
 // chunking, per-thread order and tree, so it is bitwise flat_reduce's partial), <c,x> and <b,y>
 // (the objectives, MPMP.jl:940-941).  part = [<X,Y> | <c,x> | <b,y>], gridDim.x partials each.
+// The step lengths folded into the update (one rank, a loop body): every workgroup forms
+// lambda_min of X and Y as the minimum over the blocks (scalar_kernel's fold: lane l takes
+// blocks l, l+64, ..., then the xor butterfly; min is exact, so the order is immaterial) and
+// alpha = min(1, -gamma / lambda_min), the pd-feasible alpha_p = alpha_d = min of the two
+// (MPMP.jl:863-874, 1893-1897; scalar_kernel which == 2); workgroup 0 writes the four slots.
+template <class T> struct StepAlpha {
+  const T* eigX;
+  const T* eigY;
+  int nb;       // blocks (0: alpha from the slots, as computed by the STEP stage)
+  int pd_feas;  // 0/1 from the host, -1: sc[pdslot] (decided on the device)
+  T gamma;
+  T* sc;
+  int sx, sy, sap, sad, pdslot;
+};
+template <class T>
+__device__ __forceinline__ T min_fold64(const T* v, int cnt, int lane) {
+  T acc = v[0];
+  bool have = false;
+  for (int i = lane; i < cnt; i += 64) {
+    const T e = v[i];
+    if (!have) { acc = e; have = true; }
+    else if (e < acc) acc = e;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const T e = shfl_xor_t(acc, o);
+    if (e < acc) acc = e;
+  }
+  return acc;
+}
 template <class T>
 __global__ __launch_bounds__(256) void update_state(T* __restrict__ X, const T* __restrict__ dX,
                                                     T* __restrict__ Y, const T* __restrict__ dY,
@@ -870,31 +934,72 @@ __global__ __launch_bounds__(256) void update_state(T* __restrict__ X, const T* 
                                                     const T* __restrict__ dy, long long ny,
                                                     const T* __restrict__ bv, const T* alpha_p,
                                                     const T* alpha_d, const int* info, int ninfo,
-                                                    T* __restrict__ part) {
+                                                    T* __restrict__ part, StepAlpha<T> sa) {
   __shared__ T red[3][256];
-  __shared__ int any;
+  __shared__ T alph[2];
   const int tid = threadIdx.x, G = gridDim.x, g = blockIdx.x;
-  if (tid == 0) any = 0;
-  __syncthreads();
-  for (int i = tid; i < ninfo; i += 256)
-    if (info[i]) any = 1;
-  __syncthreads();
-  const bool upd = !any;
-  const T ap = *alpha_p, ad = *alpha_d;
   long long lo, hi;
-  T axy = T(0.0), acx = T(0.0), aby = T(0.0);
   flat_chunk(nb, g, G, lo, hi);
-#pragma unroll 4
-  for (long long e = lo + tid; e < hi; e += 256) {
-    T xv = X[e], yv = Y[e];
+  // the first PF elements of X, Y, dX, dY are in flight while the step lengths and the status
+  // words are formed (wave 0: alpha; waves 1-3: the status words, OR-ed by the barrier)
+  constexpr int PF = 4;
+  T px[PF], py[PF], pdx[PF], pdy[PF];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const long long e = lo + tid + 256 * u;
+    px[u] = py[u] = pdx[u] = pdy[u] = T(0.0);
+    if (e < hi) {
+      px[u] = X[e];
+      py[u] = Y[e];
+      pdx[u] = dX[e];
+      pdy[u] = dY[e];
+    }
+  }
+  int flag = 0;
+  if (sa.nb > 0 && tid < 64) {
+    const T mx = min_fold64(sa.eigX, sa.nb, tid), my = min_fold64(sa.eigY, sa.nb, tid);
+    if (tid == 0) {
+      const T gm = sa.gamma;
+      T ap = T(1.0), ad = T(1.0);
+      if (!(mx > -gm)) ap = -gm / mx;
+      if (!(my > -gm)) ad = -gm / my;
+      const bool pdf = sa.pd_feas < 0 ? sa.sc[sa.pdslot] > T(0.5) : sa.pd_feas != 0;
+      if (pdf) {
+        if (ad < ap) ap = ad;
+        else ad = ap;
+      }
+      alph[0] = ap;
+      alph[1] = ad;
+      if (g == 0) {
+        sa.sc[sa.sx] = mx;
+        sa.sc[sa.sy] = my;
+        sa.sc[sa.sap] = ap;
+        sa.sc[sa.sad] = ad;
+      }
+    }
+  } else {
+    const int t0 = sa.nb > 0 ? tid - 64 : tid, ts = sa.nb > 0 ? 192 : 256;
+    for (int i = t0; i < ninfo; i += ts) flag |= info[i] != 0;
+  }
+  const bool upd = !__syncthreads_or(flag);
+  const T ap = sa.nb > 0 ? alph[0] : *alpha_p, ad = sa.nb > 0 ? alph[1] : *alpha_d;
+  T axy = T(0.0), acx = T(0.0), aby = T(0.0);
+  auto step = [&](long long e, T xv, T yv, T dxv, T dyv) {
     if (upd) {
-      xv = xv + ap * dX[e];
-      yv = yv + ad * dY[e];
+      xv = xv + ap * dxv;
+      yv = yv + ad * dyv;
       X[e] = xv;
       Y[e] = yv;
     }
     axy = madd(axy, xv, yv);
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const long long e = lo + tid + 256 * u;
+    if (e < hi) step(e, px[u], py[u], pdx[u], pdy[u]);
   }
+#pragma unroll 4
+  for (long long e = lo + tid + 256 * PF; e < hi; e += 256) step(e, X[e], Y[e], dX[e], dY[e]);
   flat_chunk(nx, g, G, lo, hi);
   for (long long e = lo + tid; e < hi; e += 256) {
     T v = x[e];

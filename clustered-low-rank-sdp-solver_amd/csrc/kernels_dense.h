@@ -398,19 +398,28 @@ __device__ __forceinline__ T readlane0(const T& v) {
   for (int q = 0; q < (int)(sizeof(T) / 8); ++q) d[q] = readlane_d(s[q], 0);
   return o;
 }
-template <class T, bool LDL, int NMAX>
-__global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restrict__ mats,
+template <class T, bool INV, bool LDL, int NMAX>
+__global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restrict__ in,
+                                                       const MatDesc<T>* __restrict__ out_inv,
+                                                       const MatDesc<T>* __restrict__ out_l,
                                                        int* __restrict__ info) {
   constexpr int NW = 15;                                 // bulk waves
   constexpr int SA = (NMAX * (NMAX + 1) / 2 + 63) / 64;  // 64-element slots of the triangle
   constexpr int KA = (SA + NW - 1) / NW;
+  constexpr int SX = (NMAX / 8) * (NMAX / 8 + 1) / 2;    // 8 x 8 tiles of L^-1
+  constexpr int KX = INV ? (SX + NW - 1) / NW : 1;
   constexpr int RC = (NMAX + 63) / 64;                   // chain rows per lane
+  static_assert(!INV || NMAX <= 64, "the chain holds one row of L^-1 per lane");
   __shared__ T colb[2][NMAX];    // scaled column j (LDL: of U), by parity
   __shared__ T colub[LDL ? 2 : 1][LDL ? NMAX : 1];  // LDL: the unscaled column j
   __shared__ T nextc[2][NMAX];   // column j+1 as the bulk leaves it, by parity
+  __shared__ T rowb[INV ? 2 : 1][INV ? NMAX : 1];   // row j of L^-1 (LDL: of U^-1), by parity
+  __shared__ T nextr[INV ? 2 : 1][INV ? NMAX : 1];  // row j+1 of L^-1 as the bulk leaves it
   __shared__ T dgl[LDL ? NMAX : 1];
   __shared__ int fail;
-  const MatDesc<T> d = mats[blockIdx.x];
+  const MatDesc<T> d = in[blockIdx.x];
+  const MatDesc<T> ol = out_l ? out_l[blockIdx.x] : MatDesc<T>{nullptr, 0, 0};
+  const MatDesc<T> oi = INV ? out_inv[blockIdx.x] : MatDesc<T>{nullptr, 0, 0};
   const int n = d.n, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const bool chain = w == 0;
   const int wb = w - 1;
@@ -419,7 +428,7 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
     return __builtin_amdgcn_readfirstlane(v);
   };
-  // ---- bulk slots: slot wb + NW k, element e = 64 slot + lane of the column-major triangle
+  // ---- bulk slots of A: slot wb + NW k, element e = 64 slot + lane of the column-major triangle
   T a[KA];
   int ar[KA], ac[KA], alo[KA], ahi[KA];
   const int ne = n * (n + 1) / 2;
@@ -443,15 +452,36 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
     ahi[k] = chain ? -1 : wave_max(c);
     alo[k] = chain ? NMAX : -wave_max(c >= 0 ? -c : -NMAX);
   }
-  // ---- phase -1: the chain factors column 0, the bulk publishes column 1
-  T cv[RC];  // chain: its rows of the current column
-  if (chain) {
-    if (lane == 0) fail = 0;
+  // ---- bulk tiles of L^-1 (chol_packed's 8 x 8 tiles, R >= C), identity to start
+  T x[KX];
+  int xr[KX], xc[KX], xR[KX], xC[KX];
+  if constexpr (INV) {
+    const int nt8 = (n + 7) / 8;
 #pragma unroll
-    for (int q = 0; q < RC; ++q) {
-      const int r = lane + 64 * q;
-      cv[q] = r < n ? d.A[r] : T(0.0);
+    for (int k = 0; k < KX; ++k) {
+      int t = wb + NW * k, C = 0;
+      bool tv = !chain;
+      if (tv) {
+        while (C < nt8 && t >= nt8 - C) {
+          t -= nt8 - C;
+          ++C;
+        }
+        tv = C < nt8;
+      }
+      const int R = C + t;
+      xR[k] = tv ? R : -1;
+      xC[k] = tv ? C : 0;
+      const int r = 8 * R + (lane & 7), c = 8 * C + (lane >> 3);
+      const bool v = tv && r < n && c < n;
+      xr[k] = v ? r : -1;
+      xc[k] = v ? c : NMAX;
+      x[k] = T((v && r == c) ? 1.0 : 0.0);
     }
+  }
+  // chain: the pivot of column c from the updated column cv (row c in lane 0), the scaled
+  // column to colb / colub (buffer q) and to L
+  T cv[RC];
+  auto chain_column = [&](int c, int q) {
     const T dn = readlane0(cv[0]);
     T s, rs;
     if constexpr (LDL) {
@@ -460,79 +490,100 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
       pivot_sqrt(dn, s, rs);
     }
 #pragma unroll
-    for (int q = 0; q < RC; ++q) {
-      const int r = lane + 64 * q;
+    for (int u = 0; u < RC; ++u) {
+      const int r = c + lane + 64 * u;
       if (r < n) {
         T o;
         if constexpr (LDL) {
-          o = r == 0 ? dn : cv[q] * rs;
-          colub[0][r] = cv[q];
+          o = r == c ? dn : cv[u] * rs;
+          colub[q][r] = cv[u];
         } else {
-          o = r == 0 ? s : cv[q] * rs;
+          o = r == c ? s : cv[u] * rs;
         }
-        colb[0][r] = o;
-        d.A[r] = o;
+        colb[q][r] = o;
+        if (ol.A) ol.A[r + (size_t)c * ol.lda] = o;
       }
     }
     if (lane == 0) {
-      if constexpr (LDL) dgl[0] = dn;
-      if (!(dn > T(0.0))) fail = 1;
+      if constexpr (LDL) dgl[c] = dn;
+      if (!(dn > T(0.0))) fail = c + 1;
     }
+    return rs;
+  };
+  // chain: row c of L^-1 (lane = column index <= c) scaled by the pivot's 1/sqrt (LL^T; U^-1 has
+  // a unit diagonal) -> rowb (buffer q) and the output
+  auto chain_row = [&](int c, int q, T xv, const T& rs) {
+    if constexpr (INV) {
+      if (lane <= c) {
+        if constexpr (!LDL) xv = xv * rs;
+        rowb[q][lane] = xv;
+        oi.A[c + (size_t)lane * oi.lda] = xv;
+      }
+    }
+  };
+  // ---- phase -1: the chain factors column 0 (and row 0 of L^-1), the bulk publishes column 1
+  // and row 1
+  if (chain) {
+    if (lane == 0) fail = 0;
+#pragma unroll
+    for (int u = 0; u < RC; ++u) {
+      const int r = lane + 64 * u;
+      cv[u] = r < n ? d.A[r] : T(0.0);
+    }
+    const T rs = chain_column(0, 0);
+    chain_row(0, 0, T(1.0), rs);
   } else {
 #pragma unroll
     for (int k = 0; k < KA; ++k)
       if (alo[k] <= 1 && 1 <= ahi[k] && ac[k] == 1) nextc[1][ar[k]] = a[k];
+    if constexpr (INV) {
+#pragma unroll
+      for (int k = 0; k < KX; ++k)
+        if (xR[k] == 0 && xr[k] == 1) nextr[1][xc[k]] = x[k];
+    }
   }
   __syncthreads();
   for (int j = 0; j + 1 < n; ++j) {
     if (fail) break;
     const int p = j & 1, p1 = (j + 1) & 1;
     if (chain) {
-      // column j+1: the published values minus column j's term, the pivot, the scaled column
+      // column j+1 (and row j+1 of L^-1): the published values minus step j's term, the pivot
       const int c = j + 1;
       const T cuj = LDL ? colub[p][c] : colb[p][c];
 #pragma unroll
-      for (int q = 0; q < RC; ++q) {
-        const int r = c + lane + 64 * q;
-        cv[q] = r < n ? nextc[p1][r] - colb[p][r] * cuj : T(0.0);
+      for (int u = 0; u < RC; ++u) {
+        const int r = c + lane + 64 * u;
+        cv[u] = r < n ? nextc[p1][r] - colb[p][r] * cuj : T(0.0);
       }
-      const T dn = readlane0(cv[0]);
-      T s, rs;
-      if constexpr (LDL) {
-        rs = recip_fast(dn);
-      } else {
-        pivot_sqrt(dn, s, rs);
+      T xv = T(0.0);
+      if constexpr (INV) {
+        if (lane <= c) xv = lane <= j ? nextr[p1][lane] - colb[p][c] * rowb[p][lane] : T(1.0);
       }
-#pragma unroll
-      for (int q = 0; q < RC; ++q) {
-        const int r = c + lane + 64 * q;
-        if (r < n) {
-          T o;
-          if constexpr (LDL) {
-            o = r == c ? dn : cv[q] * rs;
-            colub[p1][r] = cv[q];
-          } else {
-            o = r == c ? s : cv[q] * rs;
-          }
-          colb[p1][r] = o;
-          d.A[r + (size_t)c * d.lda] = o;
-        }
-      }
-      if (lane == 0) {
-        if constexpr (LDL) dgl[c] = dn;
-        if (!(dn > T(0.0))) fail = c + 1;
-      }
+      const T rs = chain_column(c, p1);
+      chain_row(c, p1, xv, rs);
     } else {
-      // columns >= j+2 minus column j's term; then the owners of column j+2 publish it
+      // columns >= j+2 (and rows >= j+2 of L^-1) minus step j's term; then the owners of
+      // column j+2 (and of row j+2) publish it
 #pragma unroll
       for (int k = 0; k < KA; ++k)
         if (ahi[k] >= j + 2 && ac[k] >= j + 2)
           a[k] = a[k] - colb[p][ar[k]] * (LDL ? colub[p] : colb[p])[ac[k]];
+      if constexpr (INV) {
+#pragma unroll
+        for (int k = 0; k < KX; ++k)
+          if (xR[k] >= 0 && 8 * xC[k] <= j && j + 2 <= 8 * xR[k] + 7 && xr[k] >= j + 2 && xc[k] <= j)
+            x[k] = x[k] - colb[p][xr[k]] * rowb[p][xc[k]];
+      }
       const int c2 = j + 2;
       if (c2 < n) {
 #pragma unroll
         for (int k = 0; k < KA; ++k)
           if (alo[k] <= c2 && c2 <= ahi[k] && ac[k] == c2) nextc[p][ar[k]] = a[k];
+        if constexpr (INV) {
+#pragma unroll
+          for (int k = 0; k < KX; ++k)
+            if (xR[k] == (c2 >> 3) && xr[k] == c2) nextr[p][xc[k]] = x[k];
+        }
       }
     }
     __syncthreads();
@@ -540,25 +591,35 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
   if (tid == 0 && info) info[blockIdx.x] = fail;
   __syncthreads();
   if constexpr (LDL) {
-    // L = U D^1/2: column c times sqrt d_c, the diagonal sqrt d_c (the square roots side by side)
+    // L = U D^1/2 (column c times sqrt d_c, the diagonal sqrt d_c); L^-1 = D^-1/2 U^-1 (row r
+    // times 1/sqrt d_r): the n square roots side by side
     if (!fail) {
       for (int c = tid; c < n; c += 1024) {
-        T s, r;
-        pivot_sqrt(dgl[c], s, r);
-        colb[0][c] = s;
+        T sq, rq;
+        pivot_sqrt(dgl[c], sq, rq);
+        colb[0][c] = sq;
+        colb[1][c] = rq;
       }
     }
     __syncthreads();
     if (!fail)
       for (int e = tid; e < n * n; e += 1024) {
         const int r = e % n, c = e / n;
-        if (r > c) d.A[r + (size_t)c * d.lda] = d.A[r + (size_t)c * d.lda] * colb[0][c];
-        else if (r == c) d.A[r + (size_t)c * d.lda] = colb[0][c];
+        if (ol.A) {
+          if (r > c) ol.A[r + (size_t)c * ol.lda] = ol.A[r + (size_t)c * ol.lda] * colb[0][c];
+          else if (r == c) ol.A[r + (size_t)c * ol.lda] = colb[0][c];
+        }
+        if constexpr (INV) {
+          if (r >= c) oi.A[r + (size_t)c * oi.lda] = oi.A[r + (size_t)c * oi.lda] * colb[1][r];
+        }
       }
   }
   for (int e = tid; e < n * n; e += 1024) {  // zeros above the diagonal
     const int r = e % n, c = e / n;
-    if (c > r) d.A[r + (size_t)c * d.lda] = T(0.0);
+    if (c > r) {
+      if (ol.A) ol.A[r + (size_t)c * ol.lda] = T(0.0);
+      if constexpr (INV) oi.A[r + (size_t)c * oi.lda] = T(0.0);
+    }
   }
 }
 
