@@ -876,8 +876,12 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
   void go(hipStream_t s, unsigned nb, int* info) const {
     static std::atomic<unsigned long long> attr{0};
     lds_attr_once(attr, (const void*)chol_inv_tiles<NP>, (int)chol_inv_tiles_lds<NP>());
+    // raised wave priority: the factorisation's chains keep their issue slots against the side
+    // streams' GEMM waves on the same SIMDs (CLRSDP_CHOL_PRIO=0: default priority)
+    static const int prio = env_off("CLRSDP_CHOL_PRIO") ? 0 : 1;
     chol_inv_tiles<NP><<<nb, 512, chol_inv_tiles_lds<NP>(), s>>>(
-        reinterpret_cast<const MatDesc<double>*>(din), reinterpret_cast<const MatDesc<double>*>(dout), info);
+        reinterpret_cast<const MatDesc<double>*>(din), reinterpret_cast<const MatDesc<double>*>(dout), info,
+        prio);
   }
 };
 
@@ -2197,17 +2201,22 @@ struct Solver final : HandleBase {
       if (nc2) {
         seg(CLRSDP_INNER_CHOL_S, [&] { ci_S22.launch(stream, info + info_S0 + nc()); });
         if (side_x21) {
+          // X21 on the second side stream when W1's products went there (it is idle by now), so
+          // that the first side stream is free for the right-hand side and chol(Q) as soon as Q
+          // is summed (CLRSDP_X21_AUX2=0: on the first side stream, behind them)
+          static const bool x21_aux2 = !env_off("CLRSDP_X21_AUX2");
+          const hipStream_t xs = split && x21_aux2 ? aux2 : aux;
           const hipStream_t main_s = stream;
           HIPCHK(hipEventRecord(ev_x2, main_s));
-          HIPCHK(hipStreamWaitEvent(aux, ev_x2, 0));
+          HIPCHK(hipStreamWaitEvent(xs, ev_x2, 0));
           {
-            StreamSwitch on_aux(stream, aux);  // restored on scope exit, also when a launch throws
+            StreamSwitch on_side(stream, xs);  // restored on scope exit, also when a launch throws
             seg(CLRSDP_INNER_CHOL_S, [&] {
-              f_x1.launch(aux, 1.0, 0.0);
-              f_x2.launch(aux, -1.0, 0.0);
+              f_x1.launch(xs, 1.0, 0.0);
+              f_x2.launch(xs, -1.0, 0.0);
             });
           }
-          HIPCHK(hipEventRecord(ev_x21, aux));
+          HIPCHK(hipEventRecord(ev_x21, xs));
           pending_x21 = true;
         } else {
           seg(CLRSDP_INNER_CHOL_S, [&] {

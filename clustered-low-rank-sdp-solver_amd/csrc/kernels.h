@@ -398,7 +398,8 @@ constexpr size_t LDS = sizeof(double) * END;  // 96 KB
 constexpr size_t LDS_TRACE = sizeof(double) * BREG;
 }  // namespace chain
 
-template <bool TB1, bool SYM, bool TRACE = false>
+// DBG (timing experiments only, tools/micro/chain_bench.hip): 1 = no MFMAs, 2 = no A loads
+template <bool TB1, bool SYM, bool TRACE = false, int DBG = 0>
 __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, double b1) {
   using namespace chain;
   extern __shared__ __attribute__((aligned(16))) double sm_chain[];
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, d
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     const int k = min(4 * t + lk, n - 1);
-    fa1[t] = gload(A1 + arow + (size_t)k * u.lda1);
+    fa1[t] = (DBG & 2) ? 1e-3 * (t + lane) : gload(A1 + arow + (size_t)k * u.lda1);
   }
   double cr[2][4];
 #pragma unroll
@@ -444,7 +445,8 @@ __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, d
     }
   if constexpr (!TRACE) {
 #pragma unroll
-    for (int t = 0; t < KT; ++t) fa2[t] = gload(A2 + arow + (size_t)min(4 * t + lk, n - 1) * u.lda2);
+    for (int t = 0; t < KT; ++t)
+      fa2[t] = (DBG & 2) ? 1e-3 * (t - lane) : gload(A2 + arow + (size_t)min(4 * t + lk, n - 1) * u.lda2);
   }
   // op(B1) strip into LDS (k-major for TB1, j-major otherwise: conflict-free stores and reads);
   // k >= n zeroed (the A fragments beyond n are clamped copies, their products must vanish)
@@ -459,7 +461,7 @@ __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, d
   // ---------------- stage 1: acc = A1 op(B1)[:, S] (k < K1)
   d4 acc[2];
   acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
-  if (live1) {
+  if (live1 && !(DBG & 1)) {
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       if (4 * t >= K1) break;  // (uniform)
@@ -507,7 +509,7 @@ __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, d
     __syncthreads();
     // ---------------- stage 2: O[:, S] = A2 T
     acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
-    if (live2) {
+    if (live2 && !(DBG & 1)) {
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
         if (4 * t >= n) break;  // (uniform)

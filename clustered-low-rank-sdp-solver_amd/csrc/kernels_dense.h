@@ -3021,8 +3021,14 @@ size_t chol_inv_tiles_lds() { return sizeof(double) * CholTiles<NP>::END + 16; }
 template <int NP>
 __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __restrict__ in,
                                                       const MatDesc<double>* __restrict__ out_inv,
-                                                      int* __restrict__ info) {
+                                                      int* __restrict__ info, int prio = 0) {
   using CT = CholTiles<NP>;
+  // prio: the diagonal chain (wave 0) at priority 3, the workers at 2, above co-resident waves
+  // of other launches (which stay at 0)
+  if (prio) {
+    if (threadIdx.x < 64) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(2);
+  }
   constexpr int NT = CT::NT, NWK = CT::NWK, SLOTS = CT::SLOTS, DSLOTS = CT::DSLOTS;
   constexpr int LDD = CT::LDD, XLD = CT::XLD;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];

@@ -81,6 +81,16 @@ int main() {
     CK(hipFuncSetAttribute((const void*)chain_f64<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chain::LDS));
     auto ch = [&] { chain_f64<false, false><<<P * 4, 512, chain::LDS>>>(c, 1.0, -1.0); };
     const float tp = best_of(pair), tc = best_of(ch);
+    {  // where the chain's time goes: without its MFMAs, without its A loads
+      CK(hipFuncSetAttribute((const void*)chain_f64<false, false, false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chain::LDS));
+      CK(hipFuncSetAttribute((const void*)chain_f64<false, false, false, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chain::LDS));
+      auto c1 = [&] { chain_f64<false, false, false, 1><<<P * 4, 512, chain::LDS>>>(c, 1.0, -1.0); };
+      auto c2 = [&] { chain_f64<false, false, false, 2><<<P * 4, 512, chain::LDS>>>(c, 1.0, -1.0); };
+      auto c3 = [&] { chain_f64<false, false, false, 3><<<P * 4, 512, chain::LDS>>>(c, 1.0, -1.0); };
+      CK(hipFuncSetAttribute((const void*)chain_f64<false, false, false, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chain::LDS));
+      printf("P=%2d  Z chain breakdown: no MFMA %6.2f us, no A loads %6.2f us, neither %6.2f us\n", P,
+             best_of(c1), best_of(c2), best_of(c3));
+    }
     std::vector<double> a(N), b(N);
     CK(hipMemcpy(a.data(), Z1, N * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(b.data(), Z2, N * 8, hipMemcpyDeviceToHost));
