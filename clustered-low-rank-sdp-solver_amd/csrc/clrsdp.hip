@@ -476,26 +476,26 @@ struct ChainPlan {
   }
 };
 
-template <bool DB, int TS>
+template <bool DB, int TS, int PF = 1>
 void launch_uni_db(const UniGemm& u, hipStream_t s, bool ta, bool tb, bool sca, bool sym, int tag,
                    unsigned long long* stamp, double alpha, double beta, const double* ds, double dmult) {
   constexpr int NW = TS == 64 ? 8 : 2, NT = 64 * NW;
   const unsigned tiles = (unsigned)(u.P * (int)cdiv(u.M, TS) * u.tn);
   if (sca) {
-    gemm_f64_uni<false, true, 0, 32, NW, false, true, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    gemm_f64_uni<false, true, 0, 32, NW, false, true, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
   } else if (sym) {
     if (beta != 0.0 || ds) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: beta = 0 only"};
     const unsigned grid = (unsigned)(u.P * u.tsym);
-    if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, true, false, DB, TS><<<grid, NT, 0, s>>>(u, alpha, 0.0);
-    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, true, false, DB, TS><<<grid, NT, 0, s>>>(u, alpha, 0.0);
+    if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, true, false, DB, TS, PF><<<grid, NT, 0, s>>>(u, alpha, 0.0);
+    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, true, false, DB, TS, PF><<<grid, NT, 0, s>>>(u, alpha, 0.0);
     else throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: op(A) = A only"};
   } else {
-    if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
-    else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
-    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
-    else if (ta && !tb) gemm_f64_uni<true, false, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
-    else if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
-    else gemm_f64_uni<true, true, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+    else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else if (ta && !tb) gemm_f64_uni<true, false, 0, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else gemm_f64_uni<true, true, 0, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
   }
   HIPCHK(hipGetLastError());
 }
@@ -509,7 +509,14 @@ void GemmPlan<T>::launch_uni_impl(hipStream_t s, double alpha, double beta, cons
       const char* e = std::getenv("CLRSDP_UNI_DB");
       return !(e && e[0] == '0');
     }();
+    // CLRSDP_GEMM_PF=2: two slabs in flight ahead of the MFMAs instead of one (opt-in: C3
+    // 1205-1210 against 1208-1212 it/s, A/B round 5 -- the k-loop is not load-latency bound)
+    static const bool pf2 = [] {
+      const char* e = std::getenv("CLRSDP_GEMM_PF");
+      return e && e[0] == '2';
+    }();
     if (uts == 32) launch_uni_db<true, 32>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
+    else if (db && pf2) launch_uni_db<true, 64, 2>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
     else if (db) launch_uni_db<true, 64>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
     else launch_uni_db<false, 64>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
   }
@@ -1039,6 +1046,16 @@ struct Solver final : HandleBase {
   long long n_pairs = 0;
   AYDesc* d_ayd = nullptr;
   PairDesc* d_pair = nullptr;
+  // <X + dX, Y + dY> partials from the predictor's dY chain (dotp, dy_dot_cnt of them)
+  T* dotp = nullptr;
+  int dy_dot_cnt = 0;
+  bool dy_dot_ok = false, dy_dot_ready = false;
+  // fp64 cluster solves in two launches (cl_solve_t / cl_solve_dx): one descriptor per cluster,
+  // cls_nrb 64-row blocks per cluster (the partial slabs: nc x cls_nrb x n_y in pslab)
+  std::vector<ClSolveDesc> h_cls;
+  ClSolveDesc* d_cls = nullptr;
+  int cls_nrb = 0;
+  bool cls_on = false;
   bool trivial_tuples = false;
   int n_pair = 0, max_K = 0;
   ScaleDesc* d_scale = nullptr;
@@ -1201,6 +1218,7 @@ struct Solver final : HandleBase {
     }
     if (comm_recv) (void)hipFree(comm_recv);
     if (snap) (void)hipFree(snap);
+    if (dotp) (void)hipFree(dotp);
     (void)hipFree(ksamp);
     (void)hipFree(rsums);
     if (lperm) (void)hipFree(lperm);
@@ -1238,7 +1256,7 @@ struct Solver final : HandleBase {
     Q = dmalloc<T>(n_y * n_y); Qf = dmalloc<T>(n_y * n_y); Qinv = dmalloc<T>(n_y * n_y);
     cvec = dmalloc<T>(nx); x = dmalloc<T>(nx); dx = dmalloc<T>(nx); dvec = dmalloc<T>(nx);
     rhs = dmalloc<T>(nx); tvec = dmalloc<T>(nx); tmpv = dmalloc<T>(nx);
-    pslab = dmalloc<T>((size_t)std::max(nc(), 1) * n_y);
+    pslab = dmalloc<T>((size_t)std::max(nc(), 1) * 4 * n_y);  // (x 4: cl_solve_t's row blocks)
     y = dmalloc<T>(n_y); bvec = dmalloc<T>(n_y); dyv = dmalloc<T>(n_y); pvec = dmalloc<T>(n_y);
     Pres = dmalloc<T>(std::max<int64_t>(nblk_el, 1)); pres = dmalloc<T>(std::max<int64_t>(n_y, 1));
     dres = dmalloc<T>(std::max<int64_t>(nx, 1));
@@ -1412,6 +1430,16 @@ struct Solver final : HandleBase {
         c_Z.set(0, P, Y, R, Xinv, Z);            // Z = X^-1 (P Y - R)
         c_dY.init(n0, nbk, 1, false, false);
         c_dY.set(0, dX, Y, R, Xinv, dY);         // dY = X^-1 (R - dX Y)
+        // the predictor's dY launch also leaves the partials of <X + dX, Y + dY> (CORRECTOR_R's
+        // mu; a flat sum over both triangles, so dY before its symmetrisation gives the same
+        // value); one rank only (CLRSDP_DY_DOT=0: the separate flat_reduce)
+        static const bool dd_env = !env_off("CLRSDP_DY_DOT");
+        dy_dot_cnt = nbk * (int)cdiv(n0, chain::NS);
+        dy_dot_ok = dd_env && world == 1;
+        if (dy_dot_ok) {
+          if (!dotp) dotp = dmalloc<T>(dy_dot_cnt);
+          c_dY.u.DA[0] = X; c_dY.u.DdA[0] = dX; c_dY.u.DB[0] = Y;
+        }
         c_step.init(n0, nbk, 2, true, true);
         c_step.set(0, dX, LX, nullptr, LX, tB);  // L_X^-1 dX L_X^-T
         c_step.set(1, dY, LY, nullptr, LY, tC);  // L_Y^-1 dY L_Y^-T
@@ -1485,6 +1513,9 @@ struct Solver final : HandleBase {
     // per cluster plans
     std::vector<SchurClusterDesc> scd;
     std::vector<SchurBlockDesc> sbd;
+    h_cls.clear();
+    cls_nrb = 0;
+    cls_on = false;
     std::vector<TupleDesc> td;
     std::vector<TupleBlock> tbk;
     int bi = 0;
@@ -1553,6 +1584,12 @@ struct Solver final : HandleBase {
       p_Btx.add(Bc, D, x + xo, D, nullptr, 0, pslab + (int64_t)c * n_y, (int)n_y, (int)n_y, 1, D);
       p_Wt.add(Wc, D, tvec + xo, D, nullptr, 0, pslab + (int64_t)c * n_y, (int)n_y, (int)n_y, 1, D);
       p_Wdy.add(Wc, D, dyv, (int)n_y, tvec + xo, D, dx + xo, D, D, 1, (int)n_y);
+      if constexpr (std::is_same<T, double>::value) {
+        ClSolveDesc cs{};
+        cs.L = Sc; cs.W = Wc; cs.rhs = rhs + xo; cs.t = tvec + xo; cs.dx = dx + xo; cs.D = D;
+        h_cls.push_back(cs);
+        cls_nrb = std::max(cls_nrb, (int)cdiv(D, 64));
+      }
       SchurClusterDesc cdsc;
       cdsc.m = (int)m[j]; cdsc.N = (int)Ns[j]; cdsc.D = D;
       cdsc.blk0 = bi; cdsc.nblk = (int)Lc[j];
@@ -1585,6 +1622,19 @@ struct Solver final : HandleBase {
     q_qinv.ta = true;
     q_qinv.add(Qf, (int)n_y, Qf, (int)n_y, nullptr, 0, Qinv, (int)n_y, (int)n_y, (int)n_y, (int)n_y);
     q_qdy.add(Qinv, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
+    {
+      // (fp64 explicit inverses of S_j (<= 256) and Q; opt-in, CLRSDP_CL_SOLVE=1: at C3 the two
+      // launches ran 14.8 + 21.4 us against 13.4 + 11.8 for the four GEMVs, and slab_qsolve
+      // summing four partial slabs per cluster 13.7 against 9.0 us: 1195-1232 against 1248-1270
+      // it/s, A/B round 5 -- fewer workgroups with longer load chains lose to more, shorter ones)
+      static const bool cl_env = env_on("CLRSDP_CL_SOLVE");
+      const long long cnt = (long long)std::max(nc(), 1) * std::max(cls_nrb, 1);
+      cls_on = cl_env && std::is_same<T, double>::value && reg_S && reg_Q && nc() > 0 &&
+               cls_nrb <= 4 && (long long)cdiv(n_y, 64) * cnt * n_y <= (1LL << 20) &&
+               ((size_t)n_y + 256) * sizeof(double) <= 64 * 1024;
+      for (const ClSolveDesc& cs : h_cls) cls_on = cls_on && cs.D <= 256;
+      if (cls_on) d_cls = descs.own(h_cls);
+    }
     if (nc()) {
       d_scd = descs.own(scd);
       d_sbd = descs.own(sbd);
@@ -1836,6 +1886,7 @@ struct Solver final : HandleBase {
   }
 
   void set_state(const double* xh, const double* Xh, const double* yh, const double* Yh) override {
+    dy_dot_ready = false;  // (a new state: CORRECTOR_R sums <X + dX, Y + dY> itself)
     for (int c = 0; c < nc(); ++c) put(x + c_xoff[c], xh, tot_x, xoff_g[oc[c]], Ds[oc[c]]);
     for (const LBlk& b : lb) {
       put(X + b.off, Xh, tot_blk, blkoff_g[b.gjl], (int64_t)b.n * b.n);
@@ -2371,6 +2422,8 @@ struct Solver final : HandleBase {
     // dY = sym(X^-1 (R - dX Y))
     seg(CLRSDP_INNER_DY, [&] {
       if (c_dY.on) {
+        dy_dot_ready = dy_dot_ok && tag == 4;
+        c_dY.u.dot_part = dy_dot_ready ? reinterpret_cast<double*>(dotp) : nullptr;
         c_dY.launch(stream, -1.0, 1.0);
       } else {
         p_dXY.launch(stream, -1.0, 1.0);
@@ -2389,6 +2442,29 @@ struct Solver final : HandleBase {
     if (lu_sq()) {
       direction_solves_lu(tag);
       return;
+    }
+    if constexpr (std::is_same<T, double>::value) {
+      if (cls_on) {  // t and the partial slabs | dy = Q^-1 (p - sum) | u and dx: three launches
+        const unsigned g = (unsigned)(nc() * cls_nrb);
+        cl_solve_t<<<g, 256, 0, stream>>>(d_cls, cls_nrb, (int)n_y, pslab);
+        const double* src = pslab;
+        int cnt = nc() * cls_nrb;
+        if (world > 1) {
+          slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, cnt, n_y, n_y, xsend);
+          exchange(tag, n_y);
+          src = xrecv;
+          cnt = world;
+        }
+        if (pending_q) {
+          HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
+          pending_q = false;
+        }
+        slab_qsolve<<<cdiv(n_y, 64), 256, ((size_t)n_y + 256) * sizeof(double), stream>>>(
+            src, cnt, n_y, (int)n_y, pvec, 1.0, -1.0, Qinv, (int)n_y, dyv);
+        cl_solve_dx<<<g, 256, 0, stream>>>(d_cls, cls_nrb, (int)n_y, dyv);
+        HIPCHK(hipGetLastError());
+        return;
+      }
     }
     if (reg_S) {
       q_t.launch(stream, 1.0, 0.0);
@@ -2486,7 +2562,9 @@ struct Solver final : HandleBase {
     tl_dx.launch(stream, true);               // dx_j = U_j^-1 (.)
   }
   void st_corrector_r(const clrsdp_params* prm, int pd_feas) {
-    blk_dot(X, Y, dX, dY, 1, SC_DOT_XDY, 5);
+    if (dy_dot_ready) fold(dotp, dy_dot_cnt, 0, SC_DOT_XDY);  // (from the predictor's dY chain)
+    else blk_dot(X, Y, dX, dY, 1, SC_DOT_XDY, 5);
+    dy_dot_ready = false;
     scalars(prm, pd_feas, 1);
     if constexpr (std::is_same<T, double>::value) {
       // R still holds mu_p I - XY from MU_R (the predictor only reads it), so one GEMM:
@@ -2732,16 +2810,23 @@ struct Solver final : HandleBase {
     };
     mark(CLRSDP_STAGE_MU_R);
     stage(CLRSDP_STAGE_MU_R, prm, pd_feas);
-    side(ev_m, [&] {
-      // V^T Y of the Schur stage only needs the state: it runs beside chol_inv(X, Y), which leaves
-      // half the CUs idle, and SCHUR waits for it (ev_ty) before the pairs launch
-      if (fast_schur && !p_ty.h.empty() && exp_knob != 4 && !(schur_fused && fused_y)) {
-        p_ty.launch(stream, 1.0, 0.0);
-        HIPCHK(hipEventRecord(ev_ty, stream));
-        ty_ahead = true;
-      }
-      residuals_P();
-    });
+    // V^T Y of the Schur stage only needs the state: it runs beside chol_inv(X, Y), which leaves
+    // half the CUs idle, and SCHUR waits for it (ev_ty) before the pairs launch
+    const bool ty_side = fast_schur && !p_ty.h.empty() && exp_knob != 4 && !(schur_fused && fused_y);
+    // P = sum x_i A_i - X - C is first read by the side stream's Z after SCHUR: enqueued there
+    // (one fork of the critical path fewer) unless V^T Y needs the fork anyway
+    // (CLRSDP_P_AT_SCHUR=0: beside chol_inv(X, Y) as before)
+    static const bool p_at_schur = !env_off("CLRSDP_P_AT_SCHUR");
+    const bool p_late = p_at_schur && !ty_side;
+    if (!p_late)
+      side(ev_m, [&] {
+        if (ty_side) {
+          p_ty.launch(stream, 1.0, 0.0);
+          HIPCHK(hipEventRecord(ev_ty, stream));
+          ty_ahead = true;
+        }
+        residuals_P();
+      });
     mark(CLRSDP_STAGE_XINV);
     stage(CLRSDP_STAGE_XINV, prm, pd_feas);
     mark(CLRSDP_STAGE_SCHUR);
@@ -2752,6 +2837,7 @@ struct Solver final : HandleBase {
     // residuals; the right-hand side (U = Z V and its column sums) after FACTOR's side products
     // W1^T W1 and B2' (ev_w), which are on the critical path to W2 = L22^-1 B2'
     side(ev_s, [&] {
+      if (p_late) residuals_P();
       direction_Z();
       residuals_rest(true);
       if (keep_res) {
@@ -2957,6 +3043,7 @@ struct Solver final : HandleBase {
     snapped = true;
   }
   void restore_state() override {
+    dy_dot_ready = false;
     if (!snapped) throw ClrsdpError{CLRSDP_E_STATE, "restore_state without save_state"};
     snap_copy(false);
     refresh_xy_part();

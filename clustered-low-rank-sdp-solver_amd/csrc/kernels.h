@@ -136,7 +136,12 @@ constexpr int gemm_f64_smem() {
 // (MPMP.jl:1659) formed while the slab is staged, with scale_cols's operation order
 // DB: double-buffered slabs (two LDS images per operand): the next slab is stored into the
 // other image while no wave reads it, so each k-step needs one barrier instead of two
-template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false, bool DB = false, int TS = 64>
+// PF = 2 (with DB): two slabs in flight ahead of the one the MFMAs read (two register sets,
+// alternating), so a slab's global loads have two k-steps of MFMA work to arrive in instead of
+// one -- the k-loop of a 64-wide tile is latency-bound at one slab ahead (~1 us per 32-k step
+// of MFMAs against the loads' latency under a full launch)
+template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false, bool DB = false, int TS = 64,
+          int PF = 1>
 __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, double* smem,
                                               double alpha, double beta,
                                               const double* __restrict__ dscal, double dmult) {
@@ -179,9 +184,77 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
       for (int q = 0; q < PER; ++q) ra[q] = ra[q] * (wa[q] * wl[q]);
     }
   };
+  auto mfma_slab = [&](const double* Ac, const double* Bc) {
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      double af[2], bf[NI];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) af[mi] = SL::template frag<AK>(Ac, wm * 32 + mi * 16 + lr, kk + lk);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bf[ni] = SL::template frag<BKc>(Bc, wn * WC + ni * 16 + lr, kk + lk);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+    }
+  };
   SL::template load<AK>(ra, d.A, d.lda, m0, M, 0, K, tid);
   SL::template load<BKc>(rb, d.B, d.ldb, n0, N, 0, K, tid);
   load_w(0);
+  if constexpr (PF == 2 && DB) {
+    // register sets: slab s + 1 is in set (s + 1) & 1 while the MFMAs read LDS image s & 1
+    double ra2[PER], rb2[PER], wa2[SCA ? PER : 1], wl2[SCA ? PER : 1];
+    scale_a();
+    SL::template store<AK>(ra, smem, tid, 0, K);
+    SL::template store<BKc>(rb, smem + SL::SZ, tid, 0, K);
+    const int nk = (K + BK - 1) / BK;
+    auto load_set = [&](auto SET, int k0) {
+      constexpr int st = decltype(SET)::value;
+      double(&xa)[PER] = st ? ra2 : ra;
+      double(&xb)[PER] = st ? rb2 : rb;
+      SL::template load<AK>(xa, d.A, d.lda, m0, M, k0, K, tid);
+      SL::template load<BKc>(xb, d.B, d.ldb, n0, N, k0, K, tid);
+      if constexpr (SCA) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+          int i, k;
+          SL::template kk<AK>(tid, q, i, k);
+          const int kc = min(k0 + k, K - 1);
+          (st ? wa2 : wa)[q] = gload(d.sa + kc);
+          (st ? wl2 : wl)[q] = gload(d.sl + kc);
+        }
+      }
+    };
+    auto store_set = [&](auto SET, double* img, int k0) {
+      constexpr int st = decltype(SET)::value;
+      double(&xa)[PER] = st ? ra2 : ra;
+      double(&xb)[PER] = st ? rb2 : rb;
+      if constexpr (SCA) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) xa[q] = xa[q] * ((st ? wa2 : wa)[q] * (st ? wl2 : wl)[q]);
+      }
+      SL::template store<AK>(xa, img, tid, k0, K);
+      SL::template store<BKc>(xb, img + SL::SZ, tid, k0, K);
+    };
+    if (nk > 1) load_set(std::integral_constant<int, 1>{}, BK);  // slab 1 -> set 1
+    __syncthreads();
+    // step s: slab s + 2 -> set s & 1 (free: slab s is in LDS), MFMAs on image s & 1, then
+    // slab s + 1 (set (s + 1) & 1) -> image (s + 1) & 1
+    auto step = [&](auto PAR, int sidx) {
+      constexpr int par = decltype(PAR)::value;
+      if (sidx + 2 < nk) load_set(std::integral_constant<int, par>{}, (sidx + 2) * BK);
+      mfma_slab(smem + par * 2 * SL::SZ, smem + par * 2 * SL::SZ + SL::SZ);
+      if (sidx + 1 < nk) {
+        store_set(std::integral_constant<int, par ^ 1>{}, smem + (par ^ 1) * 2 * SL::SZ, (sidx + 1) * BK);
+        __syncthreads();
+      }
+    };
+    for (int sidx = 0; sidx < nk; sidx += 2) {
+      step(std::integral_constant<int, 0>{}, sidx);
+      if (sidx + 1 < nk) step(std::integral_constant<int, 1>{}, sidx + 1);
+    }
+  } else {
   scale_a();
   SL::template store<AK>(ra, As, tid, 0, K);
   SL::template store<BKc>(rb, Bs, tid, 0, K);
@@ -196,19 +269,7 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
     }
     const double* Ac = DB ? smem + cur * 2 * SL::SZ : As;
     const double* Bc = DB ? smem + cur * 2 * SL::SZ + SL::SZ : Bs;
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      double af[2], bf[NI];
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) af[mi] = SL::template frag<AK>(Ac, wm * 32 + mi * 16 + lr, kk + lk);
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) bf[ni] = SL::template frag<BKc>(Bc, wn * WC + ni * 16 + lr, kk + lk);
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
-    }
+    mfma_slab(Ac, Bc);
     if (!more) break;
     if constexpr (DB) {
       // the other image was last read before the previous barrier
@@ -224,6 +285,7 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
       SL::template store<BKc>(rb, Bs, tid, k0 + BK, K);
       __syncthreads();
     }
+  }
   }
   __syncthreads();  // LDS slabs -> output tile
 #pragma unroll
@@ -310,7 +372,7 @@ __device__ inline void lower_tile(int q, int& tm, int& tn) {
   tn = q - tm * (tm + 1) / 2;
 }
 template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false, bool SCA = false,
-          bool DB = true, int TS = 64>
+          bool DB = true, int TS = 64, int PF = 1>
 __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double alpha, double beta,
                                                         const double* __restrict__ dscal = nullptr,
                                                         double dmult = 0.0,
@@ -334,7 +396,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double 
     lower_tile(q, tm, tc);
     t = tm * u.tn + tc;
   }
-  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA, DB, TS>(d, t, smem, alpha, beta, dscal, dmult);
+  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA, DB, TS, PF>(d, t, smem, alpha, beta, dscal, dmult);
   if constexpr (TAG == 1 || TAG == 3)
     if (stamp) {
       __syncthreads();
@@ -385,6 +447,12 @@ struct ChainGemm {
   double* rout;
   long long sLam, sX;
   double c_in, c_agg;
+  // optional (two-stage, !SYM): sum over the strip of (DA + DdA) .* (DB + O) -> dot_part[block],
+  // the <X + dX, Y + dY> of the corrector's mu (same strides as O); nullptr: off
+  const double* DA[2];
+  const double* DdA[2];
+  const double* DB[2];
+  double* dot_part;
 };
 namespace chain {
 constexpr int NS = 32, KT = 32;            // strip width; k-steps of 4 for n <= 128
@@ -507,6 +575,22 @@ __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, d
         Tm[row * LBK + 16 * u2 + lr] = row < n ? a1 * acc[u2][r] + b1 * cr[u2][r] : 0.0;
       }
     __syncthreads();
+    // the dot epilogue's operands, loaded while stage 2 runs (the store loop's element order)
+    const bool dot = !SYM && u.dot_part != nullptr;
+    double dv[NS / 4][3];
+    if (dot) {
+      const double* DA = u.DA[hs] + pl * u.sO;
+      const double* DdA = u.DdA[hs] + pl * u.sO;
+      const double* DB = u.DB[hs] + pl * u.sO;
+      const int row = min(tid & 127, n - 1);
+#pragma unroll
+      for (int c = 0; c < NS / 4; ++c) {
+        const size_t e = row + (size_t)min(s0 + (tid >> 7) + 4 * c, n - 1) * u.ldo;
+        dv[c][0] = gload(DA + e);
+        dv[c][1] = gload(DdA + e);
+        dv[c][2] = gload(DB + e);
+      }
+    }
     // ---------------- stage 2: O[:, S] = A2 T
     acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
     if (live2 && !(DBG & 1)) {
@@ -528,10 +612,22 @@ __global__ __launch_bounds__(512) void chain_f64(const ChainGemm u, double a1, d
     __syncthreads();
     {  // columns of the strip as 128-row segments (SYM: the rows on and below the diagonal)
       const int row = tid & 127;
+      double dacc = 0.0;
 #pragma unroll
       for (int c = 0; c < NS / 4; ++c) {
         const int cl = (tid >> 7) + 4 * c, col = s0 + cl;
-        if (row < n && col < n && (!SYM || row >= col)) O[row + (size_t)col * u.ldo] = St[row * SP + cl];
+        const double v = St[row * SP + cl];
+        if (row < n && col < n && (!SYM || row >= col)) O[row + (size_t)col * u.ldo] = v;
+        if (dot && row < n && col < n) dacc = fma(dv[c][0] + dv[c][1], dv[c][2] + v, dacc);
+      }
+      if (dot) {  // fixed tree: the wave (xor butterfly), then the 8 waves in order
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) dacc += __shfl_xor(dacc, o);
+        __shared__ double dred[8];
+        if (lane == 0) dred[w] = dacc;
+        __syncthreads();
+        if (tid == 0)
+          u.dot_part[blockIdx.x] = ((dred[0] + dred[1]) + (dred[2] + dred[3])) + ((dred[4] + dred[5]) + (dred[6] + dred[7]));
       }
     }
     if constexpr (SYM) {  // mirror: O[col][row] for row > col, as NS-long row segments

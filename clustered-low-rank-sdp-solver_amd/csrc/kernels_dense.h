@@ -3240,6 +3240,141 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
 #undef CT_TRACE
 
 
+// ------------------------------------------------------------------------------------------
+// The cluster part of the block solve (MPMP.jl:1751-1768) at fp64 with the explicit inverses, as
+// two launches around slab_qsolve instead of four batched GEMVs (q_t, p_Wt | q_Wdy, q_dx):
+//   cl_solve_t:  t = L^-1 rhs and this row block's share of W^T t   (one partial slab per block)
+//   cl_solve_dx: u = t + W dy and dx = L^-T u                        (one column block of dx)
+// L^-1 is the lower triangle of S_j in place (chol_inv_tiles; 2x2-blocked with X21 or not): row
+// i only uses columns <= i, so the stale S12 above the diagonal is never read.  64-row / 64-column
+// blocks, 4 waves; sums in a fixed order (deterministic).
+// ------------------------------------------------------------------------------------------
+struct ClSolveDesc {
+  const double* L;    // D x D, column-major, ld D: L^-1 in the lower triangle
+  const double* W;    // D x n_y, ld D: W = L^-1 B
+  const double* rhs;  // D
+  double* t;          // D: t = L^-1 rhs
+  double* dx;         // D: dx = L^-T (t + W dy)
+  int D, pad;
+};
+
+// Sum over the 64 lanes of each of the N values every lane holds, transposed: log2(N) halving
+// steps (lane bit 5, 4, ... picks the half a lane keeps and adds its partner's copy of) and plain
+// butterfly steps after that, so lane l ends with the total of value l >> (6 - log2 N) in
+// N - 1 + (6 - log2 N) shuffles instead of 6 N.  Fixed order.
+template <int N>
+__device__ __forceinline__ double xpose_sum(double (&v)[N], int lane) {
+  static_for<0, 6>([&](auto Lv) {
+    constexpr int lev = decltype(Lv)::value;
+    constexpr int o = 32 >> lev;
+    constexpr int H = N >> (lev + 1);
+    if constexpr (H >= 1) {
+      const bool hi = (lane & o) != 0;
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        const double send = hi ? v[j] : v[j + H];
+        const double keep = hi ? v[j + H] : v[j];
+        v[j] = keep + __shfl_xor(send, o);
+      }
+    } else {
+      v[0] = v[0] + __shfl_xor(v[0], o);
+    }
+  });
+  return v[0];
+}
+
+// grid: clusters x nrb row blocks; slabs[(cluster * nrb + block) * ny + c] (zeros past D)
+__global__ __launch_bounds__(256) void cl_solve_t(const ClSolveDesc* __restrict__ ds, int nrb,
+                                                  int ny, double* __restrict__ slabs) {
+  __shared__ double part[4][64];
+  const int c = blockIdx.x / nrb, rb = blockIdx.x - c * nrb;
+  const ClSolveDesc d = ds[c];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int D = d.D, r0 = 64 * rb, i = r0 + lane, ic = min(i, D - 1);
+  double* out = slabs + (size_t)blockIdx.x * ny;
+  if (r0 >= D) {  // (clusters of different sizes)
+    for (int e = tid; e < ny; e += 256) out[e] = 0.0;
+    return;
+  }
+  // (1) t_i = sum_{k <= i} L_ik rhs_k, wave w over k in [64 w, 64 w + 64)
+  const int k0 = 64 * w, k1 = min(k0 + 64, min(r0 + 64, D));
+  double acc = 0.0;
+  for (int kb = k0; kb < k1; kb += 16) {
+    double lv[16], rv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int k = min(kb + u, k1 - 1);
+      lv[u] = d.L[ic + (size_t)k * D];
+      rv[u] = d.rhs[k];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (kb + u < k1 && kb + u <= i) acc = fma(lv[u], rv[u], acc);
+  }
+  part[w][lane] = acc;
+  __syncthreads();
+  double t = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  if (i >= D) t = 0.0;
+  else if (w == 0) d.t[i] = t;
+  // (2) sum over this block's rows of W_ic t_i: wave w takes 32 of every 128 columns
+  for (int cb = 32 * w; cb < ny; cb += 128) {
+    double v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const double wv = d.W[ic + (size_t)min(cb + j, ny - 1) * D];
+      v[j] = i < D ? wv * t : 0.0;
+    }
+    const double sm = xpose_sum<32>(v, lane);
+    const int cc = cb + (lane >> 1);
+    if ((lane & 1) == 0 && cc < ny) out[cc] = sm;
+  }
+}
+
+// grid: clusters x nrb column blocks (64 columns of dx each, 16 per wave)
+__global__ __launch_bounds__(256) void cl_solve_dx(const ClSolveDesc* __restrict__ ds, int nrb,
+                                                   int ny, const double* __restrict__ dy) {
+  __shared__ double part[4][64];
+  const int c = blockIdx.x / nrb, cbk = blockIdx.x - c * nrb;
+  const ClSolveDesc d = ds[c];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int D = d.D, j0 = 64 * cbk + 16 * w;
+  if (64 * cbk >= D) return;
+  const int cw0 = (int)((long long)ny * w / 4), cw1 = (int)((long long)ny * (w + 1) / 4);
+  double accx = 0.0;
+  for (int rb = cbk; 64 * rb < D; ++rb) {  // the rows i >= 64 cbk, in order
+    const int i = 64 * rb + lane, ic = min(i, D - 1);
+    // u_i = t_i + W_i dy (this wave's share of the columns; the four shares in order)
+    double sm = 0.0;
+    for (int cb = cw0; cb < cw1; cb += 16) {
+      double wv[16], yv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int cc = min(cb + u, cw1 - 1);
+        wv[u] = d.W[ic + (size_t)cc * D];
+        yv[u] = dy[cc];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (cb + u < cw1) sm = fma(wv[u], yv[u], sm);
+    }
+    part[w][lane] = sm;
+    __syncthreads();
+    const double ui =
+        i < D ? d.t[ic] + ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane])) : 0.0;
+    __syncthreads();  // (part is rewritten for the next row block)
+    // dx_j += sum over this block's rows i >= j of L_ij u_i, the wave's 16 columns
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j = j0 + q;
+      const double l = d.L[ic + (size_t)min(j, D - 1) * D];
+      v[q] = (i < D && j < D && i >= j) ? l * ui : 0.0;
+    }
+    accx += xpose_sum<16>(v, lane);  // lane l: column j0 + (l >> 2)
+  }
+  const int j = j0 + (lane >> 2);
+  if ((lane & 3) == 0 && j < D) d.dx[j] = accx;
+}
+
+
 }  // namespace clrsdp
-
-
