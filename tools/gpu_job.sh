@@ -11,6 +11,7 @@
 #   micro:BIN[:ARGS]        a microbenchmark binary in microbin/ (hipcc line at the top of its tools/micro/*.hip)
 #   bench[:ARGS]            one bench.py line (ARGS with ',' for spaces), log bench_<n>.log
 #   ab:ENV:R[:ARGS]         tools/ab.sh alternating A/B of ENV (ARGS with ',' for spaces)
+#   sweep:ARGS:ENV:ENV...   tools/env_sweep.sh: one bench run per setting (NONE = none)
 #   dist2                   2-rank bench rehearsal on one GPU (CLRSDP_BENCH_ONE_GPU=1)
 #   trace[:ARGS]            rocprofv3 kernel trace of a bench line + per-body listing
 #   measure                 tools/measure_round.sh TAG (PMC passes, bench lines, summaries)
@@ -47,6 +48,11 @@ for step in "$@"; do
       envb=${rest%%:*}; r2=${rest#*:}; R=${r2%%:*}; a=""; [ "$R" != "$r2" ] && a=${r2#*:}
       timeout -k 10 900 bash tools/ab.sh "$envb" $R ${a//,/ } > $OUT/ab_$n.log 2>&1; rc=$?
       echo "ab $envb ${a//,/ } rc=$rc"; cat $OUT/ab_$n.log ;;
+    sweep)
+      # sweep:ARGS:ENV1:ENV2:... (ARGS with ',' for spaces; NONE = no setting)
+      a=${rest%%:*}; envs=${rest#*:}
+      timeout -k 10 1000 bash tools/env_sweep.sh "${a//,/ }" ${envs//:/ } > $OUT/sweep_$n.log 2>&1; rc=$?
+      echo "sweep ${a//,/ } rc=$rc"; cat $OUT/sweep_$n.log ;;
     dist2)
       CLRSDP_BENCH_ONE_GPU=1 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
