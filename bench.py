@@ -184,9 +184,12 @@ def main():
     PTHR = DTHR = 1e-30
     feas = [False]
 
+    last_mu = [1.0]
+
     def step():   # one synchronous loop body
         st = dev.iterate(prm, feas[0])
         feas[0] = max(st.p_err, st.P_err) < PTHR and st.d_err < DTHR
+        last_mu[0] = st.mu
         return st
 
     pipelined = args.loop == "pipelined" or (args.loop == "auto" and world > 1)
@@ -195,14 +198,20 @@ def main():
     # device-side copy, stream-ordered): the instance stagnates near mu ~ 1e-12 after ~100
     # iterations and the fp64 factorisations break down after ~250, so a long --steps window
     # replays iterations 1..RESTART instead.  Every timed step is still one full loop body.
+    # Also back to the snapshot once mu falls below MU_FLOOR (synchronous loop: the last body's
+    # mu): the smaller shards (--clusters 8) reach the stagnation regime (mu ~ 4e-12, dual steps
+    # ~1e-3) by iteration ~60, where a loss of definiteness of Y depends on the rounding of
+    # single operations -- a healthy window for every shard size.
     RESTART = 64
+    MU_FLOOR = 1e-8
     count = [0]
 
     def maybe_restart():
         count[0] += 1
-        if count[0] % RESTART == 0:
+        if count[0] % RESTART == 0 or last_mu[0] < MU_FLOOR:
             dev.restore_state()
             feas[0] = False   # the snapshot is the (infeasible) initial point
+            last_mu[0] = 1.0
 
     def run_bodies(n):
         """n loop bodies as solverank1sdp runs them: the host one body behind the device

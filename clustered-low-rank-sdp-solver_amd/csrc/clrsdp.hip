@@ -294,6 +294,9 @@ struct GemmPlan : PlanBase {
   // sym: every problem square with an exactly symmetric result wanted (gemm_f64_lds SYM: the
   // lower tiles only, each written with its mirror image); fp64, beta = 0
   bool sym = false;
+  // prio: raised wave priority for a critical-path batch that runs beside side-stream work
+  // (gemm_f64_uni / gemm_f64_dyn; set before finalize)
+  bool prio = false;
   void finalize() {
     if (h.empty()) return;
     if (sca && (ta || !tb || !std::is_same<T, double>::value))
@@ -322,9 +325,12 @@ struct GemmPlan : PlanBase {
     } else {
       t2d = tile_major(ntiles);
     }
+    if (prio && dyn)
+      for (auto& g : h) g.flags |= 8;
     d = own(h);
     dt = own(t2d);
     detect_uniform();
+    ug.prio = prio ? 1 : 0;
   }
   // fp64 batches of one shape at constant operand strides take gemm_f64_uni (no descriptor
   // chain before the first operand load); CLRSDP_NO_UNI_GEMM keeps the descriptor kernels
@@ -720,7 +726,12 @@ struct MatPlan : PlanBase {  // potrf / eigmin
         // eigmin_split (round 4: one reflector chain wave + 8 bulk waves) unless
         // CLRSDP_EIG_REG=1 (eigmin_reg: every live wave builds the reflector)
         static const bool reg = env_on("CLRSDP_EIG_REG");
+        // the last 24 columns on the chain wave alone (no barriers): 144.0 against 147.4 us per
+        // batch of 128 blocks of 128, bitwise the same lambda_min on 1048 of 1056 test blocks
+        // (tools/micro/eig_split_bench.hip); CLRSDP_EIG_TAIL=0 keeps the two-barrier loop
+        static const bool etail = !env_off("CLRSDP_EIG_TAIL");
         if (reg) eigmin_reg<<<(unsigned)h.size(), 512, 0, s>>>(d, out);
+        else if (etail) eigmin_split<0, 24><<<(unsigned)h.size(), 576, 0, s>>>(d, out);
         else eigmin_split<0><<<(unsigned)h.size(), 576, 0, s>>>(d, out);
         HIPCHK(hipGetLastError());
         return;
@@ -863,7 +874,8 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
     if constexpr (std::is_same<T, double>::value) {
       if (nmax <= 32) go<32>(s, nb, info);
       else if (nmax <= 64) go<64>(s, nb, info);
-      else go<128>(s, nb, info);
+      else if (nmax <= 128) go<128>(s, nb, info);
+      else go<256>(s, nb, info);
     } else {
       using C = RegCfg<T>;
       static const bool la = !env_off("CLRSDP_CHOL_LA");
@@ -881,12 +893,19 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
   }
   template <int NP>
   void go(hipStream_t s, unsigned nb, int* info) const {
+    // CLRSDP_CHOL_LDS_KB: request at least that much LDS per workgroup, so no 80-KB GEMM
+    // workgroup of a side stream can share the CU with a factorisation (A/B experiment)
+    static const size_t lds = [] {
+      const char* e = std::getenv("CLRSDP_CHOL_LDS_KB");
+      const size_t want = e ? (size_t)std::atoi(e) * 1024 : 0;
+      return std::min<size_t>(std::max(chol_inv_tiles_lds<NP>(), want), 160 * 1024);
+    }();
     static std::atomic<unsigned long long> attr{0};
-    lds_attr_once(attr, (const void*)chol_inv_tiles<NP>, (int)chol_inv_tiles_lds<NP>());
+    lds_attr_once(attr, (const void*)chol_inv_tiles<NP>, (int)lds);
     // raised wave priority: the factorisation's chains keep their issue slots against the side
     // streams' GEMM waves on the same SIMDs (CLRSDP_CHOL_PRIO=0: default priority)
     static const int prio = env_off("CLRSDP_CHOL_PRIO") ? 0 : 1;
-    chol_inv_tiles<NP><<<nb, 512, chol_inv_tiles_lds<NP>(), s>>>(
+    chol_inv_tiles<NP><<<nb, CholTiles<NP>::NTH, lds, s>>>(
         reinterpret_cast<const MatDesc<double>*>(din), reinterpret_cast<const MatDesc<double>*>(dout), info,
         prio);
   }
@@ -943,7 +962,11 @@ struct Solver final : HandleBase {
   std::vector<int64_t> c_xoff, c_Soff, c_Boff;   // per local cluster
   int64_t nx = 0, nblk_el = 0, nV = 0, nK = 0, nT = 0, nBX = 0, nAY = 0, nS = 0, nB = 0, nRS = 0;
   bool anyMgt1 = false, hasC = false;
-  int nc2 = 0;  // clusters factorised as 2x2 blocks (128 < dim_S <= 256, fp64)
+  int nc2 = 0;  // clusters factorised as 2x2 blocks (s_single < dim_S <= 256, fp64)
+  // the largest fp64 S_j factorised (and inverted) by ONE chol_inv_tiles launch: 256 with
+  // CLRSDP_CHOL256=1 (chol_inv_tiles<256>, 768 threads: no 2x2 blocking, no X21 / W1 side
+  // products), else 128
+  const int s_single = (std::is_same<T, double>::value && env_on("CLRSDP_CHOL256")) ? 256 : 128;
   bool s_lower = false;  // the last SCHUR enqueued assembled the lower triangle of S only
 
   // ---------------- device memory
@@ -1165,7 +1188,7 @@ struct Solver final : HandleBase {
       nS += Ds[j] * Ds[j];
       c_Boff.push_back(nB);
       nB += Ds[j] * n_y;
-      if (std::is_same<T, double>::value && Ds[j] > 128 && Ds[j] <= 256) ++nc2;
+      if (std::is_same<T, double>::value && Ds[j] > s_single && Ds[j] <= 256) ++nc2;
       if (m[j] > 1) anyMgt1 = true;
       for (int l = 0; l < Lc[j]; ++l) {
         LBlk b;
@@ -1271,11 +1294,11 @@ struct Solver final : HandleBase {
     {
       int64_t ns = 0;
       for (int c = 0; c < nc(); ++c)
-        if (std::is_same<T, double>::value && Ds[oc[c]] > 128 && Ds[oc[c]] <= 256) ns += 2 * (Ds[oc[c]] - 128) * 128;
+        if (std::is_same<T, double>::value && Ds[oc[c]] > s_single && Ds[oc[c]] <= 256) ns += 2 * (Ds[oc[c]] - 128) * 128;
       Stmp = dmalloc<T>(ns);
       int64_t nb2 = 0;
       for (int c = 0; c < nc(); ++c)
-        if (std::is_same<T, double>::value && Ds[oc[c]] > 128 && Ds[oc[c]] <= 256) nb2 += (Ds[oc[c]] - 128) * n_y;
+        if (std::is_same<T, double>::value && Ds[oc[c]] > s_single && Ds[oc[c]] <= 256) nb2 += (Ds[oc[c]] - 128) * n_y;
       B2p = dmalloc<T>(nb2);
     }
     tmpsc = dmalloc<T>(8);
@@ -1531,7 +1554,7 @@ struct Solver final : HandleBase {
       f_S.add(Sc, D, D);
       T* slab = Qslab + (int64_t)c * n_y * n_y;
       const int ny = (int)n_y;
-      if (!std::is_same<T, double>::value || D <= 128) {
+      if (!std::is_same<T, double>::value || D <= s_single) {
         ci_S.add(Sc, D, D, Sc, D);
         q_W.add(Sc, D, Bc, D, nullptr, 0, Wc, D, D, ny, D);
         if (std::is_same<T, double>::value) {  // (mixed batches are fp64 only)
@@ -1642,6 +1665,12 @@ struct Solver final : HandleBase {
       d_tb = descs.own(tbk);
     }
     if (fast_schur) build_fast_schur();
+    {  // FACTOR's critical-path products run beside the side streams' P, Z and W1 work: raised
+       // wave priority, opt-in with CLRSDP_FACTOR_PRIO=1 (C3 1252-1276 against 1260-1266 it/s,
+       // A/B round 5: the contention is for CUs, not for issue slots)
+      static const bool fp = env_on("CLRSDP_FACTOR_PRIO");
+      f_a.prio = f_b.prio = f_c.prio = f_d.prio = fp;
+    }
     for (GemmPlan<T>* g : {&p_txy, &p_ty, &p_XY, &p_dXdY, &p_xinv, &p_s1x, &p_s1y, &p_s2x, &p_s2y, &p_Q, &p_wA_P,
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
@@ -2037,6 +2066,10 @@ struct Solver final : HandleBase {
   }
   void scalars(const clrsdp_params* prm, int pd_feas, int which) {
     ScalarParams<T> p = prm ? sparams(prm, pd_feas) : ScalarParams<T>{};
+    // CLRSDP_SC_LDS=1: the slots mirrored in LDS for the launch (opt-in: C3 1256-1269 against
+    // 1273-1279 it/s without, A/B round 5)
+    static const int sc_lds = env_on("CLRSDP_SC_LDS") ? 1 : 0;
+    p.lds = sc_lds;
     p.zero_cy = zero_cy ? 1 : 0;
     p.zero_n = zero_info ? info_count - 1 : 0;  // status words of this iteration (not the halt word)
     p.zero_ptr = info;

@@ -38,7 +38,8 @@ template <class T> struct GemmDesc {
   int M, N, K, lda, ldb, ldcin, ldc;
   int tn;     // tiles along N
   int tile0;  // (unused by the TileRef kernels)
-  int flags;  // gemm_f64_dyn: bit 0 op(A) = A^T, bit 1 op(B) = B^T, bit 2 alpha/beta below
+  int flags;  // gemm_f64_dyn: bit 0 op(A) = A^T, bit 1 op(B) = B^T, bit 2 alpha/beta below,
+              // bit 3 raised wave priority
   double alpha, beta;  // gemm_f64_dyn with flags bit 2 (else the launch's)
   const T* sa;  // SCA launches: column k of op(A) is scaled by sa[k] * sl[k] (weighted A)
   const T* sl;
@@ -364,6 +365,7 @@ struct UniGemm {
   const double* sl;
   long long sA, sB, sCin, sC, sSa, sSl;  // per-problem strides (elements)
   int M, N, K, lda, ldb, ldcin, ldc, tn, P, tsym;  // tsym: SYM, lower tiles per problem
+  int prio;  // raised wave priority (critical-path batches beside side-stream work)
 };
 // lower tile q (row-major over the lower triangle) -> (tm, tn)
 __device__ inline void lower_tile(int q, int& tm, int& tn) {
@@ -380,6 +382,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double 
   if constexpr (TAG == 1 || TAG == 3)
     if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   __shared__ double smem[gemm_f64_smem<BK, NW, DB, TS>()];
+  if (u.prio) __builtin_amdgcn_s_setprio(2);
   const int p = blockIdx.x % u.P, q = blockIdx.x / u.P;
   GemmDesc<double> d;
   d.A = u.A + p * u.sA;
@@ -650,6 +653,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_dyn(const GemmDesc<double>* 
   __shared__ double smem[gemm_f64_smem<BK, NW>()];
   const TileRef tr = t2d[blockIdx.x];
   const GemmDesc<double> d = descs[tr.p];
+  if (d.flags & 8) __builtin_amdgcn_s_setprio(2);
   const double al = (d.flags & 4) ? d.alpha : alpha, be = (d.flags & 4) ? d.beta : beta;
   switch (d.flags & 3) {
     case 0: gemm_f64_tile<false, false, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
@@ -3104,6 +3108,7 @@ template <class T> struct ScalarParams {
   int nred;
   int zero_cy;  // which == 3 without C: <C,Y> = 0
   int fold_all;  // fp64: fold_all_f64 (all loads of all folds in flight; CLRSDP_FOLD_ALL=0: off)
+  int lds;       // the slots mirrored in LDS for the launch (one load, the changed ones written back)
   int zero_n;   // zero the status words zero_ptr[0..zero_n) (start of an iteration)
   int* zero_ptr;
   int* halt_ptr;  // which == 0: status word "skip this loop body" (device-decided termination)
@@ -3265,29 +3270,9 @@ __device__ __forceinline__ void fold_all_f64(const ScalarParams<double>& p, doub
     if (q < nred && lane == 0) sc[p.red[q].dst] = acc[q];
 }
 
+// the scalar control logic of one launch, lane 0 (sc: the slots, in LDS or global)
 template <class T>
-__global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, int which) {
-  const int lane = threadIdx.x;
-  for (int e = lane; e < p.zero_n; e += 64) p.zero_ptr[e] = 0;
-  if (sizeof(T) == 8 && p.fold_all) {
-    if constexpr (sizeof(T) == 8) fold_all_f64(p, sc, lane);
-  } else {
-    // compile-time indices into the by-value parameter block (a runtime index makes the
-    // compiler copy the whole block to scratch: 104 B/lane at quad-double)
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      if (q < p.nred) {
-        const T v = fold_wave(p.red[q], lane);
-        if (lane == 0) sc[p.red[q].dst] = v;
-      }
-    }
-  }
-  // any status word set (which == 3): the wave reads them strided, one ballot
-  bool fl = false;
-  if (which == 3)
-    for (int e = lane; e < p.nguard; e += 64) fl = fl || p.guard[e] != 0;
-  const bool failed = __any(fl);
-  if (lane != 0) return;
+__device__ __forceinline__ void scalar_logic(T* sc, const ScalarParams<T>& p, int which, bool failed) {
   const T dim = T(p.dim);
   if (which == 0) {  // mu, mu_p
     const bool pdf = pd_feasible(sc, p);
@@ -3334,6 +3319,55 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* sc, ScalarParams<T> p, in
     sc[SC_POBJ] = sc[SC_DOT_CX] + p.b0;
     sc[SC_DOBJ] = sc[SC_DOT_CY] + sc[SC_DOT_BY] + p.b0;
     control_update(sc, p, true);
+  }
+}
+
+// p.lds: the slots are read once into LDS (one coalesced load, with the guard words' loads in
+// flight beside it), the launch works there, and the slots it may change are written back --
+// instead of lane 0's chain of dependent global reads after its own writes
+template <class T>
+__global__ __launch_bounds__(64) void scalar_kernel(T* scg, ScalarParams<T> p, int which) {
+  const int lane = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) unsigned char scbuf[SC_COUNT * sizeof(T)];
+  T* sc = p.lds ? reinterpret_cast<T*>(scbuf) : scg;
+  bool fl = false;  // any status word set (which == 3): the wave reads them strided, one ballot
+  if (p.lds) {
+    if (which == 3)
+      for (int e = lane; e < p.nguard; e += 64) fl = fl || p.guard[e] != 0;
+    for (int e = lane; e < SC_COUNT; e += 64) sc[e] = scg[e];
+    __syncthreads();
+  }
+  for (int e = lane; e < p.zero_n; e += 64) p.zero_ptr[e] = 0;
+  if (sizeof(T) == 8 && p.fold_all) {
+    if constexpr (sizeof(T) == 8) fold_all_f64(p, sc, lane);
+  } else {
+    // compile-time indices into the by-value parameter block (a runtime index makes the
+    // compiler copy the whole block to scratch: 104 B/lane at quad-double)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      if (q < p.nred) {
+        const T v = fold_wave(p.red[q], lane);
+        if (lane == 0) sc[p.red[q].dst] = v;
+      }
+    }
+  }
+  if (which == 3 && !p.lds)
+    for (int e = lane; e < p.nguard; e += 64) fl = fl || p.guard[e] != 0;
+  const bool failed = __any(fl);
+  if (lane == 0) scalar_logic(sc, p, which, failed);
+  if (p.lds) {  // write back the fold targets and the slots of `which`
+    __syncthreads();
+    unsigned m = 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      if (q < p.nred) m |= 1u << p.red[q].dst;
+    if (which == 0) m |= (1u << SC_MU) | (1u << SC_MU_P);
+    else if (which == 1) m |= (1u << SC_R) | (1u << SC_BETA) | (1u << SC_BETA_C) | (1u << SC_MU_C) | (1u << SC_DMU);
+    else if (which == 2) m |= (1u << SC_ALPHA_P) | (1u << SC_ALPHA_D);
+    else if (which == 3 || which == 4)
+      m |= (1u << SC_DOT_CY) | (1u << SC_POBJ) | (1u << SC_DOBJ) | (1u << SC_GAP) | (1u << SC_PDFEAS) | (1u << SC_HALT);
+    for (int e = lane; e < SC_COUNT; e += 64)
+      if ((m >> e) & 1u) scg[e] = sc[e];
   }
 }
 

@@ -1213,10 +1213,17 @@ __global__ __launch_bounds__(64 * NWV) void eigmin_reg(const MatDesc<double>* __
 __device__ unsigned long long g_eigsplit_stamps[8];
 #endif
 // DBG (timing experiments only): 1 = no update FMAs, 2 = no matvec FMAs, 4 = the chain wave
-// skips the reflector (v_{k+1} = the published row), 8 = the old one-chain 256-way multisection
-template <int DBG = 0>
+// skips the reflector (v_{k+1} = the published row), 8 = the old one-chain 256-way multisection,
+// 128 / 256 = the column loop stops 32 / 64 columns early (what the tail columns cost)
+// TAIL (round 5): the last TAIL columns (TAIL <= 32, n >= TAIL + 8) run on the chain wave alone:
+// the trailing TAIL x TAIL matrix goes through LDS into its registers (row lane & 31 per lane,
+// both half-waves alike) and every step is wave-local -- no barrier, no cross-wave exchange.
+// The two-barrier skeleton costs ~0.8 us per column however small the trailing matrix is
+// (the last 32 columns of a 128 block: 26 us of 145, tools/micro/eig_split_bench.hip).
+template <int DBG = 0, int TAIL = 0>
 __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __restrict__ descs,
                                                      double* __restrict__ out) {
+  static_assert(TAIL == 0 || (TAIL >= 8 && TAIL <= 32), "tail size");
   constexpr int NS = 16, NWB = 8, GS = (DBG & 16) ? 2 : 4;
 #ifdef CLRSDP_EIGSPLIT_STAMPS
   // per column: chain lane 0 (slots 0-2: wait at barrier 1, reflector, wait at barrier 2) and
@@ -1351,7 +1358,12 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
     vi = vb[0][i];
     beta = betab[0];
   }
-  for (int k = 0; k + 2 < n; ++k) {
+  constexpr int KSKIP = (DBG & 128) ? 32 : (DBG & 256) ? 64 : 0;
+  // with the tail: the loop stops at iteration k0 = n - TAIL - 1 (A_{k0} in the registers, the
+  // reflector v_{k0} in vb / betab), the chain wave does iterations k0 .. n - 3
+  const bool tail = TAIL > 0 && n >= TAIL + 8;
+  const int kend = tail ? n - TAIL - 1 + 2 : n;  // loop while k + 2 < kend
+  for (int k = 0; k + 2 + KSKIP < kend; ++k) {
     const int lo = (k + 1) >> 3;  // slots s < lo hold columns <= k only
     const int r = k + 1;
     double pp = 0.0;
@@ -1462,8 +1474,98 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
     }
   }
   if (chain) __builtin_amdgcn_s_setprio(0);
-  // the last diagonal entry: row n-1 as its owners published it at the last step (or at the start)
-  if (tid == 0 && n >= 2) dg[n - 1] = rowb[(n - 1) & 1][n - 1];
+  if constexpr (TAIL > 0) {
+    if (tail) {
+      constexpr int TT = TAIL;
+      __shared__ double Mt[TT][TT + 1];
+      __shared__ double ub[TT], pt[TT];
+      const int k0 = n - TT - 1;
+      // A_{k0}'s trailing block (rows and columns > k0) from the bulk registers, v_{k0} there
+      if (!chain) {
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int j = 2 * c + 8 * sl + e;
+            if (i > k0 && j > k0 && i < n && j < n) Mt[i - k0 - 1][j - k0 - 1] = a[sl][e];
+          }
+      }
+      if (tid < TT) ub[tid] = vb[k0 & 1][k0 + 1 + tid];
+      __syncthreads();
+      if (chain) {
+        // lanes 0..TT-1 hold rows 0..TT-1; the others a dummy copy of row 0, masked out of
+        // every sum and every LDS write
+        const bool lo32 = lane < TT;
+        const int t = lo32 ? lane : 0;
+        double ar[TT];
+#pragma unroll
+        for (int j = 0; j < TT; ++j) ar[j] = Mt[t][j];
+        double bt = betab[k0 & 1], ut = lo32 ? ub[t] : 0.0;
+        static_for<0, TT - 1>([&](auto S) {
+          constexpr int st = decltype(S)::value;  // global iteration k0 + st: apply v, then v'
+          // p = A v over the live rows / columns (>= st), v^T p over the 32 lanes
+          double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+          for (int j = st; j < TT; ++j) {
+            if ((j - st) & 1) p1 = fma(ar[j], ub[j], p1);
+            else p0 = fma(ar[j], ub[j], p0);
+          }
+          const double p = (t >= st && lo32) ? p0 + p1 : 0.0;
+          const double tot = xsum16(row16_sum(ut * p));
+          const double Kc = bt * bt * tot * 0.5;
+          const double wv = fma(bt, p, -(Kc * ut));
+          const double g = fma(Kc, ut, -wv), mh = -(bt * ut);
+          if (lo32) pt[t] = p;
+          // A -= v w^T + w v^T: a_tj += mh p_j + g v_j (the p terms, then the v terms; the
+          // broadcast reads phase by phase, not all hoisted: register pressure)
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int j = st; j < TT; ++j) ar[j] = fma(pt[j], mh, ar[j]);
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int j = st; j < TT; ++j) ar[j] = fma(ub[j], g, ar[j]);
+          asm volatile("" ::: "memory");
+          // the next reflector from column st of the updated matrix (global row r = k0 + 1 + st)
+          const double xr = readlane_d(ar[st], st), x0 = readlane_d(ar[st], st + 1);
+          const double tl = xsum16(row16_sum((t >= st + 2 && lo32) ? ar[st] * ar[st] : 0.0));
+          double b2 = 0.0, v0 = x0, e2r = x0 * x0;
+          if (tl > 0.0) {
+            const double ss = fma(x0, x0, tl);
+            double nrm;
+            if (ss > 0x1p-900) {
+              double rs = __builtin_amdgcn_rsq(ss);
+              rs = rs * fma(-0.5 * ss, rs * rs, 1.5);
+              nrm = ss * rs;
+              nrm = fma(fma(-nrm, nrm, ss), 0.5 * rs, nrm);
+            } else {
+              nrm = sqrt(ss);
+            }
+            const double alpha = x0 > 0.0 ? -nrm : nrm;
+            v0 = x0 - alpha;
+            const double q = fma(v0, v0, tl);
+            double rc = __builtin_amdgcn_rcp(q);
+            rc = fma(fma(-q, rc, 1.0), rc, rc);
+            rc = fma(fma(-q, rc, 1.0), rc, rc);
+            b2 = 2.0 * rc;
+            e2r = alpha * alpha;
+          }
+          ut = (t <= st || !lo32) ? 0.0 : (t == st + 1 ? v0 : ar[st]);
+          bt = b2;
+          if (lo32) ub[t] = ut;
+          if (lane == 0) {
+            dg[k0 + 1 + st] = xr;
+            e2[k0 + 1 + st] = e2r;
+          }
+        });
+        if (lane == TT - 1) dg[n - 1] = ar[TT - 1];  // (the last reflector only flips its sign)
+      }
+    } else if (tid == 0 && n >= 2) {
+      dg[n - 1] = rowb[(n - 1) & 1][n - 1];
+    }
+  } else {
+    // the last diagonal entry: row n-1 as its owners published it at the last step (or at the start)
+    if (tid == 0 && n >= 2) dg[n - 1] = rowb[(n - 1) & 1][n - 1];
+  }
   __syncthreads();
   // Gershgorin interval, scaling and 256-way multisection: as eigmin_reg
   int bnd_ex = 0;
@@ -2996,14 +3098,21 @@ __device__ inline void chol_diag16_bc(double* __restrict__ A, IDX idx, int k0,
 // The critical path per panel is one MFMA tile + the 16-column diagonal factorisation.
 // ------------------------------------------------------------------------------------------
 #ifdef CLRSDP_CHOL_TRACE
-__device__ unsigned long long g_chol2_trace[256 * 8 * 64];
-#define CT_TRACE() do { if ((threadIdx.x & 63) == 0 && tr_i < 64) g_chol2_trace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 64 + tr_i] = __builtin_amdgcn_s_memtime(); ++tr_i; } while (0)
+// [block][wave (up to 16)][point (up to 128)]
+__device__ unsigned long long g_chol2_trace[256 * 16 * 128];
+#define CT_TRACE() do { if ((threadIdx.x & 63) == 0 && tr_i < 128) g_chol2_trace[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 128 + tr_i] = __builtin_amdgcn_s_memtime(); ++tr_i; } while (0)
 #else
 #define CT_TRACE()
 #endif
+#ifndef CLRSDP_CHOL256_NTH
+#define CLRSDP_CHOL256_NTH 768
+#endif
 template <int NP>
 struct CholTiles {
-  static constexpr int NT = NP / 16, NOFF = NT * (NT - 1) / 2, NWK = 7;
+  // NTH threads: one chain wave and NWK workers (512 up to NP = 128; 1024 at NP = 256, so the
+  // 120 off-diagonal tiles are 8 slots per worker within 128 registers)
+  static constexpr int NTH = NP > 128 ? CLRSDP_CHOL256_NTH : 512;
+  static constexpr int NT = NP / 16, NOFF = NT * (NT - 1) / 2, NWK = NTH / 64 - 1;
   static constexpr int SLOTS = (NOFF + NWK - 1) / NWK, DSLOTS = (NT + NWK - 1) / NWK;
   static constexpr int LDD = 18;        // diagonal tiles: column-major 16 x 18
   static constexpr int XLD = NP + 16;   // X row block: 16 x XLD row-major
@@ -3019,7 +3128,7 @@ template <int NP>
 size_t chol_inv_tiles_lds() { return sizeof(double) * CholTiles<NP>::END + 16; }
 
 template <int NP>
-__global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __restrict__ in,
+__global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDesc<double>* __restrict__ in,
                                                       const MatDesc<double>* __restrict__ out_inv,
                                                       int* __restrict__ info, int prio = 0) {
   using CT = CholTiles<NP>;
@@ -3042,56 +3151,113 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
 #endif
   CT_TRACE();
   const MatDesc<double> d = in[blockIdx.x];
-  const int n = d.n, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // (the wave index through readfirstlane: the slot coordinates and every branch on them are
+  // scalar, not per-lane registers)
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63,
+            w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nt = (n + 15) / 16;
   const int lr = lane & 15, lk = lane >> 4;
   const int wk = w - 1;  // worker index, -1 for wave 0
-  // ---- tile coordinates of this worker's slots (wave-uniform)
-  int TI[SLOTS], TJ[SLOTS];
-#pragma unroll
-  for (int q = 0; q < SLOTS; ++q) {
-    const int t = wk + NWK * q;
-    int ti = NT, tj = 0;  // empty slot: row NT is never active
-    if (wk >= 0 && t < CT::NOFF) CT::tile(t, ti, tj);
-    TI[q] = ti;
-    TJ[q] = tj;
-  }
-  // ---- off-diagonal tiles straight into the accumulators (A_ij^T layout, coalesced along
-  // rows), diagonal tiles into LDS with identity padding
-  d4 T[SLOTS];
-#pragma unroll
-  for (int q = 0; q < SLOTS; ++q) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gi = 16 * TI[q] + lr, gj = 16 * TJ[q] + lk + 4 * r;
-      T[q][r] = (TI[q] < nt && gi < n && gj < n) ? gload(d.A + gi + (size_t)gj * d.lda) : 0.0;
+  // The chain wave and the workers run separate copies of the panel loop (the same barriers in
+  // the same order): the workers' accumulator slots are not live in the chain wave's code, so
+  // the register allocation is the larger of the two paths, not their sum (NP = 256: 18 slots
+  // per worker next to the chain's 32-register rows).
+  const MatDesc<double> o = out_inv[blockIdx.x];
+  auto prologue = [&]() {
+    // diagonal tiles into LDS with identity padding; L^-1's tiles are written as they become
+    // final (tile row k after panel k), so no store tail is left for the end; the zero tiles
+    // above the diagonal first (never read: the input is read on and below the diagonal only,
+    // so in place is safe)
+    for (int e = tid; e < NT * 256; e += CT::NTH) {
+      const int t = e >> 8, c = (e >> 4) & 15, r = e & 15;
+      const int gi = 16 * t + r, gj = 16 * t + c;
+      double v = gi == gj ? 1.0 : 0.0;
+      if (t < nt && gi < n && gj < n && r >= c) v = gload(d.A + gi + (size_t)gj * d.lda);
+      Dt[t * 16 * LDD + c * LDD + r] = v;
     }
-  }
-  for (int e = tid; e < NT * 256; e += 512) {
-    const int t = e >> 8, c = (e >> 4) & 15, r = e & 15;
-    const int gi = 16 * t + r, gj = 16 * t + c;
-    double v = gi == gj ? 1.0 : 0.0;
-    if (t < nt && gi < n && gj < n && r >= c) v = gload(d.A + gi + (size_t)gj * d.lda);
-    Dt[t * 16 * LDD + c * LDD + r] = v;
-  }
-  d4 XD[DSLOTS];
-#pragma unroll
-  for (int q = 0; q < DSLOTS; ++q) XD[q] = d4{0.0, 0.0, 0.0, 0.0};
-  if (tid == 0) {
-    flag[0] = 0;  // first failing pivot + 1
-    flag[1] = 0;  // panels whose L_{k+1,k} is in the panel buffer
-    flag[2] = 0;  // worker arrivals at the (b) -> (c) barrier
-  }
-  __syncthreads();
-  CT_TRACE();
-  if (w == 0)
+    for (int j = tid >> 4; j < n; j += CT::NTH / 16)
+      for (int i = (tid & 15); i < (j & ~15); i += 16) o.A[i + (size_t)j * o.lda] = 0.0;
+    if (tid == 0) {
+      flag[0] = 0;  // first failing pivot + 1
+      flag[1] = 0;  // panels whose L_{k+1,k} is in the panel buffer
+      flag[2] = 0;  // worker arrivals at the (b) -> (c) barrier
+    }
+    __syncthreads();
+    CT_TRACE();
+  };
+  if (wk < 0) {
+    // ======================= the chain wave: the diagonal tiles, one panel ahead
+    prologue();
     chol_diag16_bc(Dt, [](int i, int j) { return j * LDD + i; }, 0, Di, flag, lane);
-  __syncthreads();
-  CT_TRACE();
-  for (int k = 0; k < nt; ++k) {
-    if (*flag) break;
-    const double* Dk = Di + 256 * (k & 1);
-    if (wk >= 0) {
+    __syncthreads();
+    CT_TRACE();
+    for (int k = 0; k < nt; ++k) {
+      if (*flag) break;
+      if (k + 1 < nt) {
+        // D_{k+1} -= L L^T (L = L_{k+1,k}) and its factorisation
+        while (__hip_atomic_load(flag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
+          __builtin_amdgcn_s_sleep(1);
+        CT_TRACE();
+        const double* P = Pn + 256 * (k + 1);
+        double* D = Dt + (k + 1) * 16 * LDD;
+        d4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = D[lr * LDD + lk + 4 * r];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double f = P[(4 * r + lk) * 16 + lr];
+          acc = mfma64(-f, f, acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D[lr * LDD + lk + 4 * r] = acc[r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        chol_diag16_bc(D, [](int i, int j) { return j * LDD + i; }, 16 * (k + 1),
+                       Di + 256 * ((k + 1) & 1), flag, lane);
+        CT_TRACE();
+      }
+      __syncthreads();
+      CT_TRACE();
+    }
+  } else {
+    // ======================= the workers
+    // ---- tile coordinates of this worker's slots (wave-uniform)
+    int TI[SLOTS], TJ[SLOTS];
+#pragma unroll
+    for (int q = 0; q < SLOTS; ++q) {
+      const int t = wk + NWK * q;
+      int ti = NT, tj = 0;  // empty slot: row NT is never active
+      if (t < CT::NOFF) CT::tile(t, ti, tj);
+      TI[q] = ti;
+      TJ[q] = tj;
+    }
+    // ---- off-diagonal tiles straight into the accumulators (A_ij^T layout, coalesced along rows)
+    d4 T[SLOTS];
+#pragma unroll
+    for (int q = 0; q < SLOTS; ++q) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = 16 * TI[q] + lr, gj = 16 * TJ[q] + lk + 4 * r;
+        T[q][r] = (TI[q] < nt && gi < n && gj < n) ? gload(d.A + gi + (size_t)gj * d.lda) : 0.0;
+      }
+    }
+    d4 XD[DSLOTS];
+#pragma unroll
+    for (int q = 0; q < DSLOTS; ++q) XD[q] = d4{0.0, 0.0, 0.0, 0.0};
+    prologue();
+    __syncthreads();  // (the chain wave's first diagonal factor)
+    CT_TRACE();
+    for (int k = 0; k < nt; ++k) {
+      if (*flag) break;
+      // an opaque zero per panel: the per-slot LDS and store addresses below are formed where
+      // they are used, not hoisted out of the loop (NP = 256: dozens of loop-invariant
+      // addresses kept live across the panels spilled to scratch)
+      int opq = 0;
+      if constexpr (SLOTS > 6) asm volatile("" : "+s"(opq));
+      double* const Pn_ = Pn + opq;
+      double* const Xr_ = Xr + opq;
+      double* const Dt_ = Dt + opq;
+      double* const oA = o.A + opq;
+      const double* Dk = Di + 256 * (k & 1);
       // ---------------- (b): Linv_kk as the A operand: a[r] = Linv[lr][4r+lk]
       double lopA[4];
 #pragma unroll
@@ -3106,7 +3272,7 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
           d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc = mfma64(lopA[r], T[q][r], acc);  // L_ik^T
-          double* P = Pn + 256 * TI[q];
+          double* P = Pn_ + 256 * TI[q];
 #pragma unroll
           for (int r = 0; r < 4; ++r) P[(lk + 4 * r) * 16 + lr] = acc[r];  // L_ik[lr][lk+4r]
           if (pass == 0) {
@@ -3123,7 +3289,11 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
         for (int r = 0; r < 4; ++r) acc = mfma64(lopA[r], T[q][r], acc);
         T[q] = acc;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Xr[(lk + 4 * r) * XLD + 16 * TJ[q] + lr] = acc[r];
+        for (int r = 0; r < 4; ++r) {
+          Xr_[(lk + 4 * r) * XLD + 16 * TJ[q] + lr] = acc[r];
+          const int gi = 16 * k + lk + 4 * r, gj = 16 * TJ[q] + lr;  // final: (L^-1)_kj
+          if (gi < n && gj < n) oA[gi + (size_t)gj * o.lda] = acc[r];
+        }
       }
       if (wk == k % NWK) {  // X_kk = Linv_kk (accumulator layout: register r = Linv[lk+4r][lr])
 #pragma unroll
@@ -3132,7 +3302,9 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               XD[q][r] = Dk[lr * 16 + lk + 4 * r];
-              Xr[(lk + 4 * r) * XLD + 16 * k + lr] = XD[q][r];
+              Xr_[(lk + 4 * r) * XLD + 16 * k + lr] = XD[q][r];
+              const int gi = 16 * k + lk + 4 * r, gj = 16 * k + lr;  // final: (L^-1)_kk
+              if (gi < n && gj < n) oA[gi + (size_t)gj * o.lda] = XD[q][r];
             }
           }
       }
@@ -3144,7 +3316,7 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
         __builtin_amdgcn_s_sleep(1);
       CT_TRACE();
       // ---------------- (c) trailing update of the rows below k
-      const double* Pk = Pn;
+      const double* Pk = Pn_;
 #pragma unroll
       for (int q = 0; q < SLOTS; ++q) {
         const int ti = TI[q], tj = TJ[q];
@@ -3161,7 +3333,7 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
           d4 acc = tj == k ? d4{0.0, 0.0, 0.0, 0.0} : T[q];
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            acc = mfma64(-Pi[(4 * r + lk) * 16 + lr], Xr[(4 * r + lk) * XLD + 16 * tj + lr], acc);
+            acc = mfma64(-Pi[(4 * r + lk) * 16 + lr], Xr_[(4 * r + lk) * XLD + 16 * tj + lr], acc);
           T[q] = acc;
         }
       }
@@ -3171,7 +3343,7 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
         const int di = wk + NWK * q;
         if (di >= nt || di <= k + 1) continue;
         const double* Pi = Pk + 256 * di;
-        double* D = Dt + di * 16 * LDD;
+        double* D = Dt_ + di * 16 * LDD;
         d4 acc;
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[r] = D[lr * LDD + lk + 4 * r];
@@ -3184,57 +3356,11 @@ __global__ __launch_bounds__(512) void chol_inv_tiles(const MatDesc<double>* __r
         for (int r = 0; r < 4; ++r) D[lr * LDD + lk + 4 * r] = acc[r];
       }
       CT_TRACE();
-    } else if (k + 1 < nt) {
-      // ---------------- wave 0: D_{k+1} -= L L^T (L = L_{k+1,k}) and its factorisation
-      while (__hip_atomic_load(flag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
-        __builtin_amdgcn_s_sleep(1);
-      CT_TRACE();
-      const double* P = Pn + 256 * (k + 1);
-      double* D = Dt + (k + 1) * 16 * LDD;
-      d4 acc;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = D[lr * LDD + lk + 4 * r];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double f = P[(4 * r + lk) * 16 + lr];
-        acc = mfma64(-f, f, acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) D[lr * LDD + lk + 4 * r] = acc[r];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      chol_diag16_bc(D, [](int i, int j) { return j * LDD + i; }, 16 * (k + 1),
-                     Di + 256 * ((k + 1) & 1), flag, lane);
+      __syncthreads();
       CT_TRACE();
     }
-    __syncthreads();
-    CT_TRACE();
   }
   if (tid == 0 && info) info[blockIdx.x] = *flag;
-  // ---- write L^-1: off-diagonal and diagonal X tiles from the registers, zeros above
-  const MatDesc<double> o = out_inv[blockIdx.x];
-  if (wk >= 0) {
-#pragma unroll
-    for (int q = 0; q < SLOTS; ++q) {
-      if (TI[q] >= nt) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = 16 * TI[q] + lk + 4 * r, gj = 16 * TJ[q] + lr;
-        if (gi < n && gj < n) o.A[gi + (size_t)gj * o.lda] = T[q][r];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < DSLOTS; ++q) {
-      const int di = wk + NWK * q;
-      if (di >= nt) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = 16 * di + lk + 4 * r, gj = 16 * di + lr;
-        if (gi < n && gj < n) o.A[gi + (size_t)gj * o.lda] = XD[q][r];
-      }
-    }
-  }
-  for (int j = tid >> 4; j < n; j += 32)
-    for (int i = (tid & 15); i < (j & ~15); i += 16) o.A[i + (size_t)j * o.lda] = 0.0;  // tiles above
   CT_TRACE();
 }
 #undef CT_TRACE

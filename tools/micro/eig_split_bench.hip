@@ -1,4 +1,4 @@
-// eigmin_split (one reflector chain wave + 8 bulk waves) against eigmin_reg on batches of random
+// eigmin_split with its single-wave tail (EIG_TAIL columns) against eigmin_split on batches of random
 // symmetric fp64 blocks: time per launch (best of 5) and the largest |difference| of lambda_min
 // relative to the block's max-norm, over several shapes (n, batch) and scalings.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form eig_split_bench.hip \
@@ -9,6 +9,9 @@
 #include <vector>
 #include <cmath>
 #include "../../clustered-low-rank-sdp-solver_amd/csrc/kernels_dense.h"
+#ifndef EIG_TAIL
+#define EIG_TAIL 24  // the tail variant compared against eigmin_split<0> (the first column)
+#endif
 using namespace clrsdp;
 #define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP %s @%d\n",hipGetErrorString(e),__LINE__); exit(1);} }while(0)
 
@@ -85,7 +88,7 @@ int run(int n, int nb, double scale, int kind, bool check_host) {
   MatDesc<double>* ddin;
   CK(hipMalloc(&ddin, nb * sizeof(MatDesc<double>)));
   CK(hipMemcpy(ddin, din.data(), nb * sizeof(MatDesc<double>), hipMemcpyHostToDevice));
-  const float t_reg = timeit([&] { eigmin_reg<<<nb, 512>>>(ddin, dE); });
+  const float t_reg = timeit([&] { eigmin_split<0, EIG_TAIL><<<nb, 576>>>(ddin, dE); });
   const float t_spl = timeit([&] { eigmin_split<0><<<nb, 576>>>(ddin, dE + nb); });
   CK(hipDeviceSynchronize());
   std::vector<double> ev(2 * nb);
@@ -98,8 +101,8 @@ int run(int n, int nb, double scale, int kind, bool check_host) {
     dmax = fmax(dmax, fabs(ev[b] - ev[nb + b]) / amax);
     nbit += ev[b] == ev[nb + b];
   }
-  printf("n=%3d batch=%3d kind=%d scale=%8.1e  eigmin_reg %7.1f us  eigmin_split %7.1f us  "
-         "max|diff|/|A| %.2e  bitwise-equal %d/%d", n, nb, kind, scale, t_reg, t_spl, dmax, nbit, nb);
+  printf("n=%3d batch=%3d kind=%d scale=%8.1e  eigmin_split<tail %d> %7.1f us  eigmin_split %7.1f us  "
+         "max|diff|/|A| %.2e  bitwise-equal %d/%d", n, nb, kind, scale, EIG_TAIL, t_reg, t_spl, dmax, nbit, nb);
   int bad = dmax > 1e-13;
   if (check_host) {
     std::vector<double> A0(h.begin(), h.begin() + (size_t)n * n);
@@ -160,6 +163,10 @@ int main(int argc, char** argv) {
            timeit([&] { eigmin_split<7><<<nb, 576>>>(dd, dE); }),
            timeit([&] { eigmin_split<16><<<nb, 576>>>(dd, dE); }),
            timeit([&] { eigmin_split<64><<<nb, 576>>>(dd, dE); }));
+    printf("tail cost: full %.1f us | without the last 32 columns %.1f | without the last 64 %.1f\n",
+           timeit([&] { eigmin_split<0><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<128><<<nb, 576>>>(dd, dE); }),
+           timeit([&] { eigmin_split<256><<<nb, 576>>>(dd, dE); }));
     CK(hipFree(dA));
     CK(hipFree(dE));
     CK(hipFree(dd));
