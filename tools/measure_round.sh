@@ -5,7 +5,8 @@
 #      bench lines below carry `traffic` from a counter pass of this very build;
 #   2. bench lines C3 (default, with the CPU baseline), C2, C4 (C2 shape, double-double),
 #      C5 (sphere-packing shape, quad-double);
-#   3. the C3 body at 8/16/32 clusters (the per-rank share of the strong-scaling shards).
+#   3. the C3 body at 8/16/32 clusters (the per-rank share of the strong-scaling shards), and a
+#      kernel trace of the 8-cluster body.
 # Outputs: gpurun_out/meas_$TAG/ and gpurun_out/prof_$TAG/.
 set -euo pipefail
 TAG=${1:-r03}
@@ -31,4 +32,9 @@ done
 for c in 8 16 32; do
   timeout -k 10 120 python3 bench.py --clusters $c --no-cpu --steps 300 > $OUT/clusters_$c.log 2>&1
 done
+# kernel summary and per-body listing of the 8-cluster shard (the N = 8 rank's body)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_clusters8 -o run -- \
+  python3 bench.py --clusters 8 --steps 20 --warmup 3 --no-cpu > $OUT/kt_clusters8.log 2>&1
+python3 tools/prof_summary.py $OUT/kt_clusters8/run_kernel_stats.csv > $OUT/clusters8_kernel_summary.txt
+python3 tools/iter_trace.py $OUT/kt_clusters8/run_kernel_trace.csv > $OUT/clusters8_body_trace.txt
 echo done
