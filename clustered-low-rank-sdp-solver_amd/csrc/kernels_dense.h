@@ -3104,6 +3104,15 @@ __device__ unsigned long long g_chol2_trace[256 * 16 * 128];
 #else
 #define CT_TRACE()
 #endif
+// A workgroup barrier that orders LDS only: the waves' outstanding global stores (final L^-1
+// tiles, read by no wave of the launch) are not waited for, as __syncthreads' release fence
+// would (s_waitcnt vmcnt(0) on every panel's critical path)
+__device__ __forceinline__ void lds_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
 #ifndef CLRSDP_CHOL256_NTH
 #define CLRSDP_CHOL256_NTH 768
 #endif
@@ -3168,11 +3177,26 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
     // final (tile row k after panel k), so no store tail is left for the end; the zero tiles
     // above the diagonal first (never read: the input is read on and below the diagonal only,
     // so in place is safe)
-    for (int e = tid; e < NT * 256; e += CT::NTH) {
+    // (all loads of the diagonal tiles issued before the first LDS store: one memory latency,
+    // not one per pass of the loop)
+    constexpr int DPER = (NT * 256 + CT::NTH - 1) / CT::NTH;
+    double dv[DPER];
+#pragma unroll
+    for (int q = 0; q < DPER; ++q) {
+      const int e = tid + q * CT::NTH;
+      const int t = e >> 8, c = (e >> 4) & 15, r = e & 15;
+      const int gi = min(16 * t + r, n - 1), gj = min(16 * t + c, n - 1);
+      dv[q] = gload(d.A + gi + (size_t)gj * d.lda);
+    }
+    asm volatile("" ::: "memory");  // (the loads stay above: not sunk into the selects below)
+#pragma unroll
+    for (int q = 0; q < DPER; ++q) {
+      const int e = tid + q * CT::NTH;
+      if (e >= NT * 256) continue;
       const int t = e >> 8, c = (e >> 4) & 15, r = e & 15;
       const int gi = 16 * t + r, gj = 16 * t + c;
       double v = gi == gj ? 1.0 : 0.0;
-      if (t < nt && gi < n && gj < n && r >= c) v = gload(d.A + gi + (size_t)gj * d.lda);
+      if (t < nt && gi < n && gj < n && r >= c) v = dv[q];
       Dt[t * 16 * LDD + c * LDD + r] = v;
     }
     for (int j = tid >> 4; j < n; j += CT::NTH / 16)
@@ -3182,21 +3206,24 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
       flag[1] = 0;  // panels whose L_{k+1,k} is in the panel buffer
       flag[2] = 0;  // worker arrivals at the (b) -> (c) barrier
     }
-    __syncthreads();
+    lds_barrier();
     CT_TRACE();
   };
   if (wk < 0) {
     // ======================= the chain wave: the diagonal tiles, one panel ahead
     prologue();
     chol_diag16_bc(Dt, [](int i, int j) { return j * LDD + i; }, 0, Di, flag, lane);
-    __syncthreads();
+    lds_barrier();
     CT_TRACE();
     for (int k = 0; k < nt; ++k) {
       if (*flag) break;
       if (k + 1 < nt) {
         // D_{k+1} -= L L^T (L = L_{k+1,k}) and its factorisation
-        while (__hip_atomic_load(flag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
+        // (the flags order LDS data only: relaxed LDS atomics and compiler fences, so neither
+        // side waits for the workers' outstanding global stores of final L^-1 tiles)
+        while (__hip_atomic_load(flag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
           __builtin_amdgcn_s_sleep(1);
+        __atomic_signal_fence(__ATOMIC_ACQUIRE);
         CT_TRACE();
         const double* P = Pn + 256 * (k + 1);
         double* D = Dt + (k + 1) * 16 * LDD;
@@ -3215,7 +3242,7 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
                        Di + 256 * ((k + 1) & 1), flag, lane);
         CT_TRACE();
       }
-      __syncthreads();
+      lds_barrier();
       CT_TRACE();
     }
   } else {
@@ -3244,7 +3271,7 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
 #pragma unroll
     for (int q = 0; q < DSLOTS; ++q) XD[q] = d4{0.0, 0.0, 0.0, 0.0};
     prologue();
-    __syncthreads();  // (the chain wave's first diagonal factor)
+    lds_barrier();  // (the chain wave's first diagonal factor)
     CT_TRACE();
     for (int k = 0; k < nt; ++k) {
       if (*flag) break;
@@ -3277,7 +3304,8 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
           for (int r = 0; r < 4; ++r) P[(lk + 4 * r) * 16 + lr] = acc[r];  // L_ik[lr][lk+4r]
           if (pass == 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_store(flag + 1, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __atomic_signal_fence(__ATOMIC_RELEASE);
+            if (lane == 0) __hip_atomic_store(flag + 1, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
         }
       }
@@ -3311,9 +3339,11 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
       CT_TRACE();
       // workers-only barrier (wave 0 is busy with the next diagonal tile)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(flag + 2, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      while (__hip_atomic_load(flag + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NWK * (k + 1))
+      __atomic_signal_fence(__ATOMIC_RELEASE);
+      if (lane == 0) __hip_atomic_fetch_add(flag + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      while (__hip_atomic_load(flag + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NWK * (k + 1))
         __builtin_amdgcn_s_sleep(1);
+      __atomic_signal_fence(__ATOMIC_ACQUIRE);
       CT_TRACE();
       // ---------------- (c) trailing update of the rows below k
       const double* Pk = Pn_;
@@ -3356,7 +3386,7 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
         for (int r = 0; r < 4; ++r) D[lr * LDD + lk + 4 * r] = acc[r];
       }
       CT_TRACE();
-      __syncthreads();
+      lds_barrier();
       CT_TRACE();
     }
   }
