@@ -3081,6 +3081,88 @@ __device__ inline void chol_diag16_bc(double* __restrict__ A, IDX idx, int k0,
   }
 }
 
+// chol_diag16_bc software-pipelined (same arithmetic, bit for bit): each column's pivot chain
+// (readlane -> rsq -> Newton -> l_j -> the next pivot column's update) is the critical path, and
+// the rest of the previous column's rank-1 update is issued inside it, in four pieces between
+// its dependent steps (in-order issue: those FMAs fill the chain's latency instead of following
+// it).  The inverse rows are split over the four 16-lane DPP rows: register s of DPP row g holds
+// column 4s + g of this lane's row of X, so a column's inverse update is ceil((j+1)/4) FMAs,
+// not j+1.
+// LD(i, k): element (i, k) of the symmetric input tile (default: the lower triangle of the image)
+template <class IDX, class LD>
+__device__ inline void chol_diag16_pipe(double* __restrict__ A, IDX idx, LD ld, int k0,
+                                        double* __restrict__ Dinv, int* flag, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  double a[16], x[4];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) a[k] = ld(i, k);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) x[s] = (4 * s + g == i) ? 1.0 : 0.0;
+  int bad = 0;
+  double rmine = 1.0, lvp = 0.0, nlp = 0.0, nlrp = 0.0;  // column j-1's l, -l and -l r
+  // piece C (of 4) of column JP's bulk: a[JP+2 ..] -= l l_k, then x[s] (4s <= JP)
+  auto bulk = [&](auto JP, auto C, auto NOP) {
+    constexpr int jp = decltype(JP)::value, c = decltype(C)::value;
+    constexpr int NA = jp < 14 ? 14 - jp : 0, N = NA + jp / 4 + 1;
+    static_for<c * N / 4, (c + 1) * N / 4>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      if constexpr (t < NA) fmac_bcast<jp + 2 + t, false>(a[jp + 2 + t], lvp, nlp);
+      else fmac_bcast<jp, decltype(NOP)::value && t == c * N / 4>(x[t - NA], x[t - NA], nlrp);
+    });
+  };
+  using F = std::false_type;
+  static_for<0, 16>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr auto JP = std::integral_constant<int, (j > 0 ? j - 1 : 0)>{};
+    const double d = readlane_d(a[j], j);
+    bad |= !(d > 0.0);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (j > 0) bulk(JP, std::integral_constant<int, 0>{}, F{});
+    __builtin_amdgcn_sched_barrier(0);
+    double r = __builtin_amdgcn_rsq(d);
+    const double hd = 0.5 * d;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (j > 0) bulk(JP, std::integral_constant<int, 1>{}, F{});
+    __builtin_amdgcn_sched_barrier(0);
+    const double t1 = hd * r;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (j > 0) bulk(JP, std::integral_constant<int, 2>{}, F{});
+    __builtin_amdgcn_sched_barrier(0);
+    const double t2 = 1.5 - t1 * r;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (j > 0) bulk(JP, std::integral_constant<int, 3>{}, F{});
+    __builtin_amdgcn_sched_barrier(0);
+    r = r * t2;
+    const double lv = a[j] * r;
+    const double nl = (i > j) ? -lv : 0.0;
+    const double nlr = nl * r;
+    rmine = (i == j) ? r : rmine;
+    a[j] = lv;
+    if constexpr (j < 15) fmac_bcast<j + 1, true>(a[j + 1], lv, nl);
+    lvp = lv;
+    nlp = nl;
+    nlrp = nlr;
+  });
+  // column 15's bulk: the inverse update only
+  static_for<0, 4>([&](auto C) { bulk(std::integral_constant<int, 15>{}, C, std::true_type{}); });
+#pragma unroll
+  for (int s = 0; s < 4; ++s) x[s] *= rmine;
+  if (lane < 16) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k <= i) A[idx(i, k)] = a[k];
+    if (lane == 0 && bad) *flag = k0 + 1;
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) Dinv[(4 * s + g) * 16 + i] = x[s];
+}
+template <class IDX>
+__device__ inline void chol_diag16_pipe(double* __restrict__ A, IDX idx, int k0,
+                                        double* __restrict__ Dinv, int* flag, int lane) {
+  chol_diag16_pipe(A, idx, [&](int i, int k) { return A[idx(max(i, k), min(i, k))]; }, k0, Dinv, flag,
+                   lane);
+}
+
 // ------------------------------------------------------------------------------------------
 // chol_inv_tiles: A = L L^T and L^-1 for n <= NP (fp64), one 512-thread workgroup per matrix,
 // with the off-diagonal 16x16 tiles resident in the worker waves' MFMA accumulators for the
@@ -3116,13 +3198,16 @@ __device__ __forceinline__ void lds_barrier() {
 #ifndef CLRSDP_CHOL256_NTH
 #define CLRSDP_CHOL256_NTH 768
 #endif
-template <int NP>
+template <int NP, bool SP = false>
 struct CholTiles {
-  // NTH threads: one chain wave and NWK workers (512 up to NP = 128; 1024 at NP = 256, so the
-  // 120 off-diagonal tiles are 8 slots per worker within 128 registers)
+  // NTH threads: one chain wave and NWK workers (512 up to NP = 128; 768 at NP = 256).  SP: the
+  // waves that share SIMD 0 with the chain wave (w = 4, 8, ...) hold no tiles (an f64 MFMA
+  // stream on the chain's SIMD slows its VALU chain by half: tools/micro/diag16_bench.hip),
+  // NWA workers do the MFMA work
   static constexpr int NTH = NP > 128 ? CLRSDP_CHOL256_NTH : 512;
   static constexpr int NT = NP / 16, NOFF = NT * (NT - 1) / 2, NWK = NTH / 64 - 1;
-  static constexpr int SLOTS = (NOFF + NWK - 1) / NWK, DSLOTS = (NT + NWK - 1) / NWK;
+  static constexpr int NWA = SP ? NWK - NWK / 4 : NWK;
+  static constexpr int SLOTS = (NOFF + NWA - 1) / NWA, DSLOTS = (NT + NWA - 1) / NWA;
   static constexpr int LDD = 18;        // diagonal tiles: column-major 16 x 18
   static constexpr int XLD = NP + 16;   // X row block: 16 x XLD row-major
   static constexpr int DT = 0, PN = DT + NT * 16 * LDD, XR = PN + NT * 256, DI = XR + 16 * XLD,
@@ -3136,18 +3221,18 @@ struct CholTiles {
 template <int NP>
 size_t chol_inv_tiles_lds() { return sizeof(double) * CholTiles<NP>::END + 16; }
 
-template <int NP>
+template <int NP, bool SP = false>
 __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDesc<double>* __restrict__ in,
                                                       const MatDesc<double>* __restrict__ out_inv,
                                                       int* __restrict__ info, int prio = 0) {
-  using CT = CholTiles<NP>;
+  using CT = CholTiles<NP, SP>;
   // prio: the diagonal chain (wave 0) at priority 3, the workers at 2, above co-resident waves
   // of other launches (which stay at 0)
   if (prio) {
     if (threadIdx.x < 64) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(2);
   }
-  constexpr int NT = CT::NT, NWK = CT::NWK, SLOTS = CT::SLOTS, DSLOTS = CT::DSLOTS;
+  constexpr int NT = CT::NT, NWK = CT::NWK, NWA = CT::NWA, SLOTS = CT::SLOTS, DSLOTS = CT::DSLOTS;
   constexpr int LDD = CT::LDD, XLD = CT::XLD;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   double* Dt = reinterpret_cast<double*>(smem_raw) + CT::DT;  // diagonal tiles
@@ -3167,20 +3252,23 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
   const int nt = (n + 15) / 16;
   const int lr = lane & 15, lk = lane >> 4;
   const int wk = w - 1;  // worker index, -1 for wave 0
+  // tile-owning worker rank (-1: the chain wave, or a spare wave on the chain's SIMD)
+  const bool spare = SP && w > 0 && (w & 3) == 0;
+  const int wr = spare ? -1 : SP ? w - 1 - w / 4 : wk;
   // The chain wave and the workers run separate copies of the panel loop (the same barriers in
   // the same order): the workers' accumulator slots are not live in the chain wave's code, so
   // the register allocation is the larger of the two paths, not their sum (NP = 256: 18 slots
   // per worker next to the chain's 32-register rows).
   const MatDesc<double> o = out_inv[blockIdx.x];
-  auto prologue = [&]() {
-    // diagonal tiles into LDS with identity padding; L^-1's tiles are written as they become
-    // final (tile row k after panel k), so no store tail is left for the end; the zero tiles
-    // above the diagonal first (never read: the input is read on and below the diagonal only,
-    // so in place is safe)
-    // (all loads of the diagonal tiles issued before the first LDS store: one memory latency,
-    // not one per pass of the loop)
-    constexpr int DPER = (NT * 256 + CT::NTH - 1) / CT::NTH;
-    double dv[DPER];
+  // prologue: the diagonal tiles 1.. into LDS with identity padding (tile 0 is the chain wave's:
+  // it factors D_0 straight from global memory while the other waves load); L^-1's tiles are
+  // written as they become final (tile row k after panel k), so no store tail is left for the
+  // end; the zero tiles above the diagonal first (never read: the input is read on and below the
+  // diagonal only, so in place is safe).  All loads of the diagonal tiles are issued before the
+  // first LDS store: one memory latency, not one per pass of the loop.
+  constexpr int DPER = (NT * 256 + CT::NTH - 1) / CT::NTH;
+  double dv[DPER];
+  auto prologue_load = [&]() {
 #pragma unroll
     for (int q = 0; q < DPER; ++q) {
       const int e = tid + q * CT::NTH;
@@ -3189,10 +3277,12 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
       dv[q] = gload(d.A + gi + (size_t)gj * d.lda);
     }
     asm volatile("" ::: "memory");  // (the loads stay above: not sunk into the selects below)
+  };
+  auto prologue_store = [&]() {
 #pragma unroll
     for (int q = 0; q < DPER; ++q) {
       const int e = tid + q * CT::NTH;
-      if (e >= NT * 256) continue;
+      if (e < 256 || e >= NT * 256) continue;
       const int t = e >> 8, c = (e >> 4) & 15, r = e & 15;
       const int gi = 16 * t + r, gj = 16 * t + c;
       double v = gi == gj ? 1.0 : 0.0;
@@ -3201,18 +3291,24 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
     }
     for (int j = tid >> 4; j < n; j += CT::NTH / 16)
       for (int i = (tid & 15); i < (j & ~15); i += 16) o.A[i + (size_t)j * o.lda] = 0.0;
-    if (tid == 0) {
-      flag[0] = 0;  // first failing pivot + 1
-      flag[1] = 0;  // panels whose L_{k+1,k} is in the panel buffer
-      flag[2] = 0;  // worker arrivals at the (b) -> (c) barrier
-    }
     lds_barrier();
     CT_TRACE();
   };
   if (wk < 0) {
     // ======================= the chain wave: the diagonal tiles, one panel ahead
-    prologue();
-    chol_diag16_bc(Dt, [](int i, int j) { return j * LDD + i; }, 0, Di, flag, lane);
+    if (lane == 0) {  // (before D_0's factorisation, which may set flag[0])
+      flag[0] = 0;  // first failing pivot + 1
+      flag[1] = 0;  // panels whose L_{k+1,k} is in the panel buffer
+      flag[2] = 0;  // worker arrivals at the (b) -> (c) barrier
+    }
+    prologue_load();
+    chol_diag16_pipe(Dt, [](int i, int j) { return j * LDD + i; },
+                     [&](int i, int k) {  // D_0 from global memory, identity-padded past n
+                       const int r = max(i, k), c = min(i, k);
+                       return r < n ? gload(d.A + r + (size_t)c * d.lda) : (i == k ? 1.0 : 0.0);
+                     },
+                     0, Di, flag, lane);
+    prologue_store();
     lds_barrier();
     CT_TRACE();
     for (int k = 0; k < nt; ++k) {
@@ -3238,8 +3334,8 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
 #pragma unroll
         for (int r = 0; r < 4; ++r) D[lr * LDD + lk + 4 * r] = acc[r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        chol_diag16_bc(D, [](int i, int j) { return j * LDD + i; }, 16 * (k + 1),
-                       Di + 256 * ((k + 1) & 1), flag, lane);
+        chol_diag16_pipe(D, [](int i, int j) { return j * LDD + i; }, 16 * (k + 1),
+                         Di + 256 * ((k + 1) & 1), flag, lane);
         CT_TRACE();
       }
       lds_barrier();
@@ -3251,9 +3347,9 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
     int TI[SLOTS], TJ[SLOTS];
 #pragma unroll
     for (int q = 0; q < SLOTS; ++q) {
-      const int t = wk + NWK * q;
+      const int t = wr + NWA * q;
       int ti = NT, tj = 0;  // empty slot: row NT is never active
-      if (t < CT::NOFF) CT::tile(t, ti, tj);
+      if (wr >= 0 && t < CT::NOFF) CT::tile(t, ti, tj);
       TI[q] = ti;
       TJ[q] = tj;
     }
@@ -3270,7 +3366,8 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
     d4 XD[DSLOTS];
 #pragma unroll
     for (int q = 0; q < DSLOTS; ++q) XD[q] = d4{0.0, 0.0, 0.0, 0.0};
-    prologue();
+    prologue_load();
+    prologue_store();
     lds_barrier();  // (the chain wave's first diagonal factor)
     CT_TRACE();
     for (int k = 0; k < nt; ++k) {
@@ -3323,10 +3420,10 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
           if (gi < n && gj < n) oA[gi + (size_t)gj * o.lda] = acc[r];
         }
       }
-      if (wk == k % NWK) {  // X_kk = Linv_kk (accumulator layout: register r = Linv[lk+4r][lr])
+      if (wr == k % NWA) {  // X_kk = Linv_kk (accumulator layout: register r = Linv[lk+4r][lr])
 #pragma unroll
         for (int q = 0; q < DSLOTS; ++q)
-          if (q == k / NWK) {
+          if (q == k / NWA) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               XD[q][r] = Dk[lr * 16 + lk + 4 * r];
@@ -3370,8 +3467,8 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
       // diagonal tiles below the look-ahead one: D_i -= L_ik L_ik^T (in LDS)
 #pragma unroll
       for (int q = 0; q < DSLOTS; ++q) {
-        const int di = wk + NWK * q;
-        if (di >= nt || di <= k + 1) continue;
+        const int di = wr + NWA * q;
+        if (wr < 0 || di >= nt || di <= k + 1) continue;
         const double* Pi = Pk + 256 * di;
         double* D = Dt_ + di * 16 * LDD;
         d4 acc;
