@@ -903,19 +903,11 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
     // raised wave priority: the factorisation's chains keep their issue slots against the side
     // streams' GEMM waves on the same SIMDs (CLRSDP_CHOL_PRIO=0: default priority)
     static const int prio = env_off("CLRSDP_CHOL_PRIO") ? 0 : 1;
-    // CLRSDP_CHOL_SPARE=1: no MFMA tiles on the waves that share the chain wave's SIMD
-    static const bool spare = env_on("CLRSDP_CHOL_SPARE");
-    const auto* in = reinterpret_cast<const MatDesc<double>*>(din);
-    const auto* out = reinterpret_cast<const MatDesc<double>*>(dout);
-    if (spare) {
-      static std::atomic<unsigned long long> attr{0};
-      lds_attr_once(attr, (const void*)chol_inv_tiles<NP, true>, (int)lds);
-      chol_inv_tiles<NP, true><<<nb, CholTiles<NP>::NTH, lds, s>>>(in, out, info, prio);
-    } else {
-      static std::atomic<unsigned long long> attr{0};
-      lds_attr_once(attr, (const void*)chol_inv_tiles<NP>, (int)lds);
-      chol_inv_tiles<NP><<<nb, CholTiles<NP>::NTH, lds, s>>>(in, out, info, prio);
-    }
+    static std::atomic<unsigned long long> attr{0};
+    lds_attr_once(attr, (const void*)chol_inv_tiles<NP>, (int)lds);
+    chol_inv_tiles<NP><<<nb, CholTiles<NP>::NTH, lds, s>>>(
+        reinterpret_cast<const MatDesc<double>*>(din), reinterpret_cast<const MatDesc<double>*>(dout), info,
+        prio);
   }
 };
 

@@ -3198,16 +3198,16 @@ __device__ __forceinline__ void lds_barrier() {
 #ifndef CLRSDP_CHOL256_NTH
 #define CLRSDP_CHOL256_NTH 768
 #endif
-template <int NP, bool SP = false>
+template <int NP>
 struct CholTiles {
-  // NTH threads: one chain wave and NWK workers (512 up to NP = 128; 768 at NP = 256).  SP: the
-  // waves that share SIMD 0 with the chain wave (w = 4, 8, ...) hold no tiles (an f64 MFMA
-  // stream on the chain's SIMD slows its VALU chain by half: tools/micro/diag16_bench.hip),
-  // NWA workers do the MFMA work
+  // NTH threads: one chain wave and NWK workers (512 up to NP = 128; 768 at NP = 256).  Wave 4
+  // (a worker) shares SIMD 0 with the chain wave, and its f64 MFMAs slow the chain's VALU
+  // chain by half (tools/micro/diag16_bench.hip); measured and rejected: no tiles on it (the
+  // MFMA work then has three SIMDs: 32.7 vs 31.3 us at n = 128) or its trailing update held
+  // back until the chain's diagonal factor is done (35.0 vs 31.4 us)
   static constexpr int NTH = NP > 128 ? CLRSDP_CHOL256_NTH : 512;
   static constexpr int NT = NP / 16, NOFF = NT * (NT - 1) / 2, NWK = NTH / 64 - 1;
-  static constexpr int NWA = SP ? NWK - NWK / 4 : NWK;
-  static constexpr int SLOTS = (NOFF + NWA - 1) / NWA, DSLOTS = (NT + NWA - 1) / NWA;
+  static constexpr int SLOTS = (NOFF + NWK - 1) / NWK, DSLOTS = (NT + NWK - 1) / NWK;
   static constexpr int LDD = 18;        // diagonal tiles: column-major 16 x 18
   static constexpr int XLD = NP + 16;   // X row block: 16 x XLD row-major
   static constexpr int DT = 0, PN = DT + NT * 16 * LDD, XR = PN + NT * 256, DI = XR + 16 * XLD,
@@ -3221,18 +3221,18 @@ struct CholTiles {
 template <int NP>
 size_t chol_inv_tiles_lds() { return sizeof(double) * CholTiles<NP>::END + 16; }
 
-template <int NP, bool SP = false>
+template <int NP>
 __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDesc<double>* __restrict__ in,
                                                       const MatDesc<double>* __restrict__ out_inv,
                                                       int* __restrict__ info, int prio = 0) {
-  using CT = CholTiles<NP, SP>;
+  using CT = CholTiles<NP>;
   // prio: the diagonal chain (wave 0) at priority 3, the workers at 2, above co-resident waves
   // of other launches (which stay at 0)
   if (prio) {
     if (threadIdx.x < 64) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(2);
   }
-  constexpr int NT = CT::NT, NWK = CT::NWK, NWA = CT::NWA, SLOTS = CT::SLOTS, DSLOTS = CT::DSLOTS;
+  constexpr int NT = CT::NT, NWK = CT::NWK, SLOTS = CT::SLOTS, DSLOTS = CT::DSLOTS;
   constexpr int LDD = CT::LDD, XLD = CT::XLD;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   double* Dt = reinterpret_cast<double*>(smem_raw) + CT::DT;  // diagonal tiles
@@ -3252,9 +3252,6 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
   const int nt = (n + 15) / 16;
   const int lr = lane & 15, lk = lane >> 4;
   const int wk = w - 1;  // worker index, -1 for wave 0
-  // tile-owning worker rank (-1: the chain wave, or a spare wave on the chain's SIMD)
-  const bool spare = SP && w > 0 && (w & 3) == 0;
-  const int wr = spare ? -1 : SP ? w - 1 - w / 4 : wk;
   // The chain wave and the workers run separate copies of the panel loop (the same barriers in
   // the same order): the workers' accumulator slots are not live in the chain wave's code, so
   // the register allocation is the larger of the two paths, not their sum (NP = 256: 18 slots
@@ -3347,9 +3344,9 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
     int TI[SLOTS], TJ[SLOTS];
 #pragma unroll
     for (int q = 0; q < SLOTS; ++q) {
-      const int t = wr + NWA * q;
+      const int t = wk + NWK * q;
       int ti = NT, tj = 0;  // empty slot: row NT is never active
-      if (wr >= 0 && t < CT::NOFF) CT::tile(t, ti, tj);
+      if (t < CT::NOFF) CT::tile(t, ti, tj);
       TI[q] = ti;
       TJ[q] = tj;
     }
@@ -3420,10 +3417,10 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
           if (gi < n && gj < n) oA[gi + (size_t)gj * o.lda] = acc[r];
         }
       }
-      if (wr == k % NWA) {  // X_kk = Linv_kk (accumulator layout: register r = Linv[lk+4r][lr])
+      if (wk == k % NWK) {  // X_kk = Linv_kk (accumulator layout: register r = Linv[lk+4r][lr])
 #pragma unroll
         for (int q = 0; q < DSLOTS; ++q)
-          if (q == k / NWA) {
+          if (q == k / NWK) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               XD[q][r] = Dk[lr * 16 + lk + 4 * r];
@@ -3467,8 +3464,8 @@ __global__ __launch_bounds__(CholTiles<NP>::NTH) void chol_inv_tiles(const MatDe
       // diagonal tiles below the look-ahead one: D_i -= L_ik L_ik^T (in LDS)
 #pragma unroll
       for (int q = 0; q < DSLOTS; ++q) {
-        const int di = wr + NWA * q;
-        if (wr < 0 || di >= nt || di <= k + 1) continue;
+        const int di = wk + NWK * q;
+        if (di >= nt || di <= k + 1) continue;
         const double* Pi = Pk + 256 * di;
         double* D = Dt_ + di * 16 * LDD;
         d4 acc;

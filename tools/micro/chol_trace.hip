@@ -1,5 +1,5 @@
 // Per-wave timeline of chol_inv_tiles (s_memtime stamps, -DCLRSDP_CHOL_TRACE): where the panel
-// loop spends its cycles, and L^-1 A L^-T = I per matrix.  Usage: chol_trace [n] [batch] [spare]
+// loop spends its cycles, and L^-1 A L^-T = I per matrix.  Usage: chol_trace [n] [batch]
 // (n <= 64: NP = 64, n <= 128: NP = 128, else NP = 256)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -DCLRSDP_CHOL_TRACE \
 //     chol_trace.hip -o ../../microbin/chol_trace && ../../microbin/chol_trace 255 64
@@ -13,21 +13,14 @@ using namespace clrsdp;
 #define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP %s @%d\n",hipGetErrorString(e),__LINE__); exit(1);} }while(0)
 
 template <int NP>
-void launch(unsigned nb, const MatDesc<double>* in, const MatDesc<double>* out, int* info, bool spare) {
-  if (spare) {
-    CK(hipFuncSetAttribute((const void*)chol_inv_tiles<NP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                           (int)chol_inv_tiles_lds<NP>()));
-    chol_inv_tiles<NP, true><<<nb, CholTiles<NP>::NTH, chol_inv_tiles_lds<NP>()>>>(in, out, info, 1);
-  } else {
-    CK(hipFuncSetAttribute((const void*)chol_inv_tiles<NP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                           (int)chol_inv_tiles_lds<NP>()));
-    chol_inv_tiles<NP><<<nb, CholTiles<NP>::NTH, chol_inv_tiles_lds<NP>()>>>(in, out, info, 1);
-  }
+void launch(unsigned nb, const MatDesc<double>* in, const MatDesc<double>* out, int* info) {
+  CK(hipFuncSetAttribute((const void*)chol_inv_tiles<NP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                         (int)chol_inv_tiles_lds<NP>()));
+  chol_inv_tiles<NP><<<nb, CholTiles<NP>::NTH, chol_inv_tiles_lds<NP>()>>>(in, out, info, 1);
 }
 
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 128, nb = argc > 2 ? atoi(argv[2]) : 128;
-  const bool spare = argc > 3 && atoi(argv[3]) != 0;
   const int NTH = n <= 128 ? 512 : CholTiles<256>::NTH, NW = NTH / 64;
   std::vector<double> h((size_t)nb * n * n);
   srand(1);
@@ -56,11 +49,11 @@ int main(int argc, char** argv) {
   float ms = 0;
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipEventRecord(e0));
-    if (n <= 64) launch<64>(nb, ddin, ddout, info, spare);
-    else if (n <= 128) launch<128>(nb, ddin, ddout, info, spare);
-    else launch<256>(nb, ddin, ddout, info, spare);
+    if (n <= 64) launch<64>(nb, ddin, ddout, info);
+    else if (n <= 128) launch<128>(nb, ddin, ddout, info);
+    else launch<256>(nb, ddin, ddout, info);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
-    printf("chol_inv_tiles n=%d batch=%d threads=%d spare=%d: %.1f us\n", n, nb, NTH, (int)spare, ms * 1e3);
+    printf("chol_inv_tiles n=%d batch=%d threads=%d: %.1f us\n", n, nb, NTH, ms * 1e3);
   }
   {
     std::vector<double> o2(h.size());
