@@ -546,6 +546,7 @@ struct TrsmPlan : PlanBase {
   static constexpr int NCV = 4, NCV16 = 16;
   bool vec = false;
   int ncv = NCV;
+  bool four = false;  // four right-hand sides per workgroup whatever their number (latency first)
   void add(const T* L, int ldl, T* B, int ldb, int n, int nrhs) {
     if (n <= 0 || nrhs <= 0) return;
     rmax = std::max(rmax, nrhs);
@@ -564,7 +565,10 @@ struct TrsmPlan : PlanBase {
     const char* e128 = std::getenv("CLRSDP_TRSV128");
     vec = mode == 0 && !std::is_same<T, double>::value && !env_on("CLRSDP_TRSV_BLOCKED") &&
           (nmax <= 64 || (nmax <= 128 && !(e128 && e128[0] == '0')));
-    ncv = rmax <= NCV ? NCV : NCV16;
+    // (CLRSDP_TRSV_NW4=1: four right-hand sides per workgroup whatever their number: one chain
+    // per SIMD, more workgroups)
+    static const bool nw4 = env_on("CLRSDP_TRSV_NW4");
+    ncv = (rmax <= NCV || nw4 || four) ? NCV : NCV16;
     const int nc = vec ? ncv : narrow ? NCN : NCW;
     if constexpr (!std::is_same<T, double>::value) {
       if (vec) {  // (outside any graph capture)
@@ -1037,6 +1041,15 @@ struct Solver final : HandleBase {
   const int exp_knob = std::getenv("CLRSDP_EXP") ? std::atoi(std::getenv("CLRSDP_EXP")) : 0;
   bool pending_x21 = false;  // the solves wait for X21 (side stream, iterate)
   hipEvent_t ev_x2 = nullptr, ev_x21 = nullptr;
+  // multi-word S_j / Q <= 64 in the split form (CLRSDP_MW_SPLIT): potrf on the critical path,
+  // L^-1 by four-wave triangular solves of the identity (S_j: on aux2, off the critical path),
+  // then the same GEMV solves as the explicit-inverse path
+  bool s_split = false, q_split = false, pending_sinv = false;
+  int64_t s_len = 0;
+  T *SLi = nullptr, *SLid = nullptr, *QLi = nullptr, *QLid = nullptr;  // L^-1 and identity images
+  TrsmPlan<T> t_Sinv, t_Qinv;
+  GemmPlan<T> q_t2, q_dx2, q_qinv2;
+  hipEvent_t ev_sp = nullptr, ev_sinv = nullptr;
   MatPlan<T> e_XY;                        // both step-length eigenproblems in one launch
   // LU fallback plans (built on the first switch)
   LuPlan<T> lu_S, lu_Q, lu_X;
@@ -1221,7 +1234,7 @@ struct Solver final : HandleBase {
       else HIPCHK(hipStreamCreateWithFlags(&aux2, hipStreamNonBlocking));
     }
     for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21, &ev_ty, &ev_join,
-                          &ev_fa, &ev_w, &ev_join2})
+                          &ev_fa, &ev_w, &ev_join2, &ev_sp, &ev_sinv})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
     build_plans();
@@ -1252,7 +1265,7 @@ struct Solver final : HandleBase {
     for (auto& e : ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : seg_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_m, ev_x, ev_s, ev_r, ev_qa, ev_q, ev_x2, ev_x21, ev_ty, ev_join, ev_fa, ev_w,
-                         ev_join2, ring_ev[0], ring_ev[1]})
+                         ev_join2, ev_sp, ev_sinv, ring_ev[0], ring_ev[1]})
       if (e) (void)hipEventDestroy(e);
     for (hipGraphExec_t g : gexec)
       if (g) (void)hipGraphExecDestroy(g);
@@ -1343,13 +1356,21 @@ struct Solver final : HandleBase {
       reg_blk = nmax_b <= reg_nmax<T>();
       reg_S = nmax_S <= (std::is_same<T, double>::value ? 2 : 1) * reg_nmax<T>();
       reg_Q = n_y <= reg_nmax<T>();
-      // multi-word S_j / Q up to 64 through the look-ahead factorisation with L^-1 and GEMVs
-      // instead of potrf and the serial multi-word vector solves (four 41-us trsv_wave chains
-      // per direction at C5 for one 90-us longer factorisation each: C5 761 -> 827 it/s, C4
-      // unchanged, round 5; CLRSDP_MW_INV_S=0 / CLRSDP_MW_INV_Q=0 keep potrf + trsv)
+      // multi-word S_j / Q up to 64: GEMV solves with L^-1 instead of the serial multi-word
+      // vector solves (four 41-us trsv_wave chains per direction at C5).  Default, the split
+      // form: potrf on the critical path and L^-1 = L \ I by four-wave solves (S_j's beside W_j
+      // and the Q chain), C5 891 it/s; CLRSDP_MW_SPLIT=0: the look-ahead factorisation with
+      // L^-1 (90 us longer per factorisation, 827 it/s; CLRSDP_MW_INV_S=0 / _Q=0 then keep
+      // potrf + trsv, 761 it/s).  C4 (dim S_j = 127) unchanged.  Round 5 A/B.
       if (!std::is_same<T, double>::value && !env_off("CLRSDP_CHOL_LA")) {
-        if (!env_off("CLRSDP_MW_INV_S")) reg_S = reg_S || nmax_S <= 64;
-        if (!env_off("CLRSDP_MW_INV_Q")) reg_Q = reg_Q || n_y <= 64;
+        static const bool split = !env_off("CLRSDP_MW_SPLIT");
+        if (split) {
+          s_split = !reg_S && nmax_S <= 64;
+          q_split = !reg_Q && n_y <= 64;
+        } else {
+          if (!env_off("CLRSDP_MW_INV_S")) reg_S = reg_S || nmax_S <= 64;
+          if (!env_off("CLRSDP_MW_INV_Q")) reg_Q = reg_Q || n_y <= 64;
+        }
       }
     }
     q_xinv.ta = true;
@@ -1552,6 +1573,31 @@ struct Solver final : HandleBase {
     int bi = 0;
     int64_t s2off = 0, b2off = 0;
     std::vector<MatDesc<T>> s11;  // S11 blocks of the 2x2-blocked clusters (chol_inv in ci_S)
+    if (s_split || q_split) {
+      q_dx2.ta = true;
+      q_qinv2.ta = true;
+      t_W.four = t_Sinv.four = t_Qinv.four = true;
+      auto ident = [&](T*& img, T*& id, const std::vector<std::pair<int64_t, int>>& blocks, int64_t len) {
+        img = dmalloc<T>(len);
+        id = dmalloc<T>(len);
+        std::vector<T> h((size_t)len, T(0.0));
+        for (const auto& b : blocks)
+          for (int i = 0; i < b.second; ++i) h[(size_t)(b.first + (int64_t)i * b.second + i)] = T(1.0);
+        HIPCHK(hipMemcpy(id, h.data(), (size_t)len * sizeof(T), hipMemcpyHostToDevice));
+      };
+      if (s_split) {
+        std::vector<std::pair<int64_t, int>> bl;
+        int64_t len = 1;
+        for (int c = 0; c < nc(); ++c) {
+          const int D = (int)Ds[oc[c]];
+          bl.push_back({c_Soff[c], D});
+          len = std::max(len, c_Soff[c] + (int64_t)D * D);
+        }
+        ident(SLi, SLid, bl, len);
+        s_len = len;
+      }
+      if (q_split) ident(QLi, QLid, {{0, (int)n_y}}, std::max<int64_t>(n_y * n_y, 1));
+    }
     for (int c = 0; c < nc(); ++c) {
       const int j = oc[c];
       const int D = (int)Ds[j];
@@ -1610,6 +1656,12 @@ struct Solver final : HandleBase {
       q_Wdy.add(Wc, D, dyv, (int)n_y, tvec + xo, D, tmpv + xo, D, D, 1, (int)n_y);
       t_W.add(Sc, D, Wc, D, D, (int)n_y);
       t_t.add(Sc, D, tvec + xo, D, D, 1);
+      if (s_split) {
+        T* Li = SLi + c_Soff[c];
+        t_Sinv.add(Sc, D, Li, D, D, D);                                              // L^-1 = L \ I
+        q_t2.add(Li, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D, 1, D);
+        q_dx2.add(Li, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D, 1, D);
+      }
       p_Q.add(Wc, D, Wc, D, nullptr, 0, slab, ny, ny, ny, D);
       p_By.add(Bc, D, y, (int)n_y, nullptr, 0, tmpv + xo, D, D, 1, (int)n_y);
       p_Btx.add(Bc, D, x + xo, D, nullptr, 0, pslab + (int64_t)c * n_y, (int)n_y, (int)n_y, 1, D);
@@ -1653,6 +1705,10 @@ struct Solver final : HandleBase {
     q_qinv.ta = true;
     q_qinv.add(Qf, (int)n_y, Qf, (int)n_y, nullptr, 0, Qinv, (int)n_y, (int)n_y, (int)n_y, (int)n_y);
     q_qdy.add(Qinv, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
+    if (q_split) {
+      t_Qinv.add(Qf, (int)n_y, QLi, (int)n_y, (int)n_y, (int)n_y);                  // L_Q^-1 = L_Q \ I
+      q_qinv2.add(QLi, (int)n_y, QLi, (int)n_y, nullptr, 0, Qinv, (int)n_y, (int)n_y, (int)n_y, (int)n_y);
+    }
     {
       // (fp64 explicit inverses of S_j (<= 256) and Q; opt-in, CLRSDP_CL_SOLVE=1: at C3 the two
       // launches ran 14.8 + 21.4 us against 13.4 + 11.8 for the four GEMVs, and slab_qsolve
@@ -1683,11 +1739,12 @@ struct Solver final : HandleBase {
                            &p_wA_dX, &p_trU_Z, &p_trU_Y, &p_By, &p_Btx, &p_Wt, &p_Wdy, &p_PY,
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
                            &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &f_a, &f_b, &f_c, &f_d, &f_x1, &f_x2, &f_w, &f_w2,
+                           &q_t2, &q_dx2, &q_qinv2,
                            &p_wA_Ps, &p_wA_dXs})
       g->finalize();
     for (CholInvPlan<T>* c : {&ci_XY, &ci_S, &ci_S22, &ci_Q}) c->finalize();
     e_XY.finalize();
-    for (TrsmPlan<T>* t : {&t_Linv, &t_W, &t_t, &t_Q, &t_sX1, &t_sX2, &t_sY1, &t_sY2, &t_dx})
+    for (TrsmPlan<T>* t : {&t_Linv, &t_W, &t_t, &t_Q, &t_sX1, &t_sX2, &t_sY1, &t_sY2, &t_dx, &t_Sinv, &t_Qinv})
       t->finalize();
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q}) f->reg_potrf = true;
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q, &e_X, &e_Y}) f->finalize();
@@ -2328,6 +2385,19 @@ struct Solver final : HandleBase {
       seg(CLRSDP_INNER_CINVB, [&] { q_W.launch(stream, 1.0, 0.0); });
     } else {
       seg(CLRSDP_INNER_CHOL_S, [&] { f_S.potrf(stream, info + info_S0); });
+      if (s_split) {  // L_j^-1 for the GEMV solves, beside W_j and the Q chain
+        const hipStream_t ls = side_x21 && aux2 ? aux2 : stream;  // (a loop body only)
+        if (ls != stream) {
+          HIPCHK(hipEventRecord(ev_sp, stream));
+          HIPCHK(hipStreamWaitEvent(ls, ev_sp, 0));
+        }
+        HIPCHK(hipMemcpyAsync(SLi, SLid, (size_t)s_len * sizeof(T), hipMemcpyDeviceToDevice, ls));
+        t_Sinv.launch(ls, false);
+        if (ls != stream) {
+          HIPCHK(hipEventRecord(ev_sinv, ls));
+          pending_sinv = true;
+        }
+      }
       seg(CLRSDP_INNER_CINVB, [&] {
         vlin(Wm, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
         t_W.launch(stream, false);            // W_j = L_j^-1 B_j
@@ -2366,6 +2436,11 @@ struct Solver final : HandleBase {
     } else {
       vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
       f_Q.potrf(stream, info + info_Q0);
+      if (q_split) {  // Q^-1 = L_Q^-T L_Q^-1 with L_Q^-1 = L_Q \ I
+        HIPCHK(hipMemcpyAsync(QLi, QLid, (size_t)q2 * sizeof(T), hipMemcpyDeviceToDevice, stream));
+        t_Qinv.launch(stream, false);
+        q_qinv2.launch(stream, 1.0, 0.0);
+      }
     }
   }
   void st_residuals(bool use_AY) {
@@ -2507,8 +2582,14 @@ struct Solver final : HandleBase {
         return;
       }
     }
+    if (pending_sinv) {
+      HIPCHK(hipStreamWaitEvent(stream, ev_sinv, 0));
+      pending_sinv = false;
+    }
     if (reg_S) {
       q_t.launch(stream, 1.0, 0.0);
+    } else if (s_split) {
+      q_t2.launch(stream, 1.0, 0.0);
     } else {
       vlin(tvec, rhs, 1.0, nullptr, 0, nullptr, 0, nx);
       t_t.launch(stream, false);
@@ -2549,7 +2630,7 @@ struct Solver final : HandleBase {
     }
     if (!fused_done) {
       // r = p - sum_j W_j^T t_j  (-> uvec with the explicit Q^-1, -> dyv for the two solves)
-      T* rv = reg_Q ? uvec : dyv;
+      T* rv = (reg_Q || q_split) ? uvec : dyv;
       if (world == 1 && nc()) {  // one launch
         slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, rv, pvec, 1.0, -1.0);
       } else {
@@ -2562,7 +2643,7 @@ struct Solver final : HandleBase {
         HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
         pending_q = false;
       }
-      if (reg_Q) {
+      if (reg_Q || q_split) {
         q_qdy.launch(stream, 1.0, 0.0);         // dy = Q^-1 r
       } else {
         t_Q.launch(stream, false);
@@ -2570,9 +2651,9 @@ struct Solver final : HandleBase {
       }
     }
     // dx_j = L_j^-T (t_j + W_j dy)
-    if (reg_S) {
+    if (reg_S || s_split) {
       q_Wdy.launch(stream, 1.0, 1.0);
-      q_dx.launch(stream, 1.0, 0.0);
+      (s_split ? q_dx2 : q_dx).launch(stream, 1.0, 0.0);
     } else {
       p_Wdy.launch(stream, 1.0, 1.0);
       t_dx.launch(stream, true);
@@ -2925,6 +3006,10 @@ struct Solver final : HandleBase {
     if (pending_x21) {
       HIPCHK(hipStreamWaitEvent(stream, ev_x21, 0));
       pending_x21 = false;
+    }
+    if (pending_sinv) {
+      HIPCHK(hipStreamWaitEvent(stream, ev_sinv, 0));
+      pending_sinv = false;
     }
     if (timing == 1) HIPCHK(hipEventRecord(ev[CLRSDP_NUM_STAGES], stream));
   }
