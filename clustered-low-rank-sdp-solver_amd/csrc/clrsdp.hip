@@ -1365,7 +1365,9 @@ struct Solver final : HandleBase {
       if (!std::is_same<T, double>::value && !env_off("CLRSDP_CHOL_LA")) {
         static const bool split = !env_off("CLRSDP_MW_SPLIT");
         if (split) {
-          s_split = !reg_S && nmax_S <= 64;
+          // (double-double S_j up to 128: trsv_wave128 forms L^-1 as it does the vector solves)
+          const int lim = std::is_same<T, mw::dd>::value && !env_off("CLRSDP_TRSV128") ? 128 : 64;
+          s_split = !reg_S && nmax_S <= lim;
           q_split = !reg_Q && n_y <= 64;
         } else {
           if (!env_off("CLRSDP_MW_INV_S")) reg_S = reg_S || nmax_S <= 64;
