@@ -147,6 +147,13 @@ inline void lds_attr_once(std::atomic<unsigned long long>& seen, const void* fn,
 template <class T> struct RegCfg { static constexpr int TR = 4, TC = 8, GR = 32, GC = 16; };
 template <> struct RegCfg<dd> { static constexpr int TR = 1, TC = 4, GR = 64, GC = 16; };  // 1024 threads
 template <> struct RegCfg<qd> { static constexpr int TR = 1, TC = 1, GR = 32, GC = 32; };  // 1024 threads
+// chol_lookahead's switches (CLRSDP_LA_OPTS, kernels_dense.h).  Default 2: one Newton step for
+// the quad-double pivot reciprocal (~2^-208 relative; the second step was a third of the chain:
+// C5 879 -> 930 it/s, round 5 A/B); bit 0 (chain priority) measured nothing
+inline int la_opts() {
+  static const int o = std::getenv("CLRSDP_LA_OPTS") ? std::atoi(std::getenv("CLRSDP_LA_OPTS")) : 2;
+  return o;
+}
 template <class T> constexpr int reg_nmax() { return std::is_same<T, double>::value ? 128 : RegCfg<T>::TR * RegCfg<T>::GR; }
 // multi-word blocks n <= 64 factor with chol_packed (liveness-packed slots, bitwise the same
 // factors as chol_inv_reg); CLRSDP_CHOL_PACKED=0 keeps the tile grid (A/B)
@@ -692,11 +699,11 @@ struct MatPlan : PlanBase {  // potrf / eigmin
       static const bool la = !env_off("CLRSDP_CHOL_LA");
       if (reg_potrf && la && nmax <= (std::is_same<T, mw::dd>::value ? 128 : 64)) {
         if (std::is_same<T, mw::dd>::value && nmax > 64)
-          chol_lookahead<T, false, false, 128><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info);
+          chol_lookahead<T, false, false, 128><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info, la_opts());
         else if (std::is_same<T, mw::qd>::value && chol_ldl_on())
-          chol_lookahead<T, false, true, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info);
+          chol_lookahead<T, false, true, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info, la_opts());
         else
-          chol_lookahead<T, false, false, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info);
+          chol_lookahead<T, false, false, 64><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info, la_opts());
         HIPCHK(hipGetLastError());
         return;
       }
@@ -885,9 +892,9 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
       static const bool la = !env_off("CLRSDP_CHOL_LA");
       if (la && nmax <= 64) {  // the look-ahead factorisation with L^-1 (bitwise chol_packed's)
         if (std::is_same<T, mw::qd>::value && chol_ldl_on())
-          chol_lookahead<T, true, true, 64><<<nb, 1024, 0, s>>>(din, dout, dl, info);
+          chol_lookahead<T, true, true, 64><<<nb, 1024, 0, s>>>(din, dout, dl, info, la_opts());
         else
-          chol_lookahead<T, true, false, 64><<<nb, 1024, 0, s>>>(din, dout, dl, info);
+          chol_lookahead<T, true, false, 64><<<nb, 1024, 0, s>>>(din, dout, dl, info, la_opts());
       } else if (chol_packed_on() && nmax <= 64)
         launch_chol_packed<T, true>(nb, s, din, dout, dl, info);
       else

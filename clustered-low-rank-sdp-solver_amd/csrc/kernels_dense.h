@@ -402,7 +402,10 @@ template <class T, bool INV, bool LDL, int NMAX>
 __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restrict__ in,
                                                        const MatDesc<T>* __restrict__ out_inv,
                                                        const MatDesc<T>* __restrict__ out_l,
-                                                       int* __restrict__ info) {
+                                                       int* __restrict__ info, int opts = 0) {
+  // opts (A/B switches): bit 0 = the chain wave at raised issue priority (its SIMD also runs
+  // three bulk waves); bit 1 = one Newton step for the pivot's reciprocal (from the
+  // double-double one: ~2^-208 relative instead of ~2^-212)
   constexpr int NW = 15;                                 // bulk waves
   constexpr int SA = (NMAX * (NMAX + 1) / 2 + 63) / 64;  // 64-element slots of the triangle
   constexpr int KA = (SA + NW - 1) / NW;
@@ -485,7 +488,17 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
     const T dn = readlane0(cv[0]);
     T s, rs;
     if constexpr (LDL) {
-      rs = recip_fast(dn);
+      if constexpr (std::is_same<T, mw::qd>::value) {
+        if (opts & 2) {
+          rs = T(recip_fast(mw::dd(dn.x[0], dn.x[1])));
+          const T e = T(1.0) - dn * rs;
+          rs = rs + T(mw::dd(rs.x[0], rs.x[1]) * mw::dd(e.x[0], e.x[1]));
+        } else {
+          rs = recip_fast(dn);
+        }
+      } else {
+        rs = recip_fast(dn);
+      }
     } else {
       pivot_sqrt(dn, s, rs);
     }
@@ -524,6 +537,7 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
   // ---- phase -1: the chain factors column 0 (and row 0 of L^-1), the bulk publishes column 1
   // and row 1
   if (chain) {
+    if (opts & 1) __builtin_amdgcn_s_setprio(3);
     if (lane == 0) fail = 0;
 #pragma unroll
     for (int u = 0; u < RC; ++u) {
