@@ -402,8 +402,15 @@ struct GemmPlan : PlanBase {
     const unsigned grid = (unsigned)t2d.size();
     if (gemv) {  // (tb only with K = 1: B[0] is the vector either way)
       // fp64: deep load pipelines (CLRSDP_GEMV_DEEP=0: the 8-deep round-4 loops)
+      // (multi-word, transposed: DEEP selects the thread-per-column form, the quad-double default
+      // -- C5 936 -> 977 it/s; double-double keeps the 16-lane reduction form, 834 against 820
+      // with the column form -- CLRSDP_GEMV_MW_T16=1 / CLRSDP_GEMV_MW_COL=1 swap them; round 5)
       static const bool deep = !env_off("CLRSDP_GEMV_DEEP");
-      if (ta && deep) gemv_batched<T, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
+      static const bool mw_t16 = env_on("CLRSDP_GEMV_MW_T16"), mw_col = env_on("CLRSDP_GEMV_MW_COL");
+      const bool deep_t = std::is_same<T, double>::value ? deep
+                          : std::is_same<T, mw::qd>::value ? !mw_t16
+                                                           : mw_col;
+      if (ta && deep_t) gemv_batched<T, true><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else if (ta) gemv_batched<T, true, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else if (deep) gemv_batched<T, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);
       else gemv_batched<T, false, false><<<grid, 256, 0, s>>>(d, dt, alpha, beta);

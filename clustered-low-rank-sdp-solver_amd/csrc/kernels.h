@@ -862,6 +862,7 @@ __device__ __forceinline__ T row16_sum_t(T v) {
 //   TA: wave w owns 16 outputs (columns); lane (k-offset kk = lane & 15, column c4 = lane >> 4)
 //       streams 4 columns at once (16 consecutive k per column per load instruction), 4 column
 //       groups x 2 k-steps of loads in flight; each column sum is a 16-lane DPP reduction.
+//       Multi-word with DEEP: thread per column and k-group as !TA (the quad-double default).
 template <class T, bool TA, bool DEEP = true>
 __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restrict__ descs,
                                                     const TileRef* __restrict__ t2d, double alpha,
@@ -918,6 +919,28 @@ __global__ __launch_bounds__(256) void gemv_batched(const GemmDesc<T>* __restric
       T v = ((part[0][r] + part[1][r]) + (part[2][r] + part[3][r])) * T(alpha);
       if (beta != 0.0) v += d.Cin[i] * T(beta);
       d.C[i] = v;
+    }
+  } else if constexpr (sizeof(T) > 8 && DEEP) {
+    // multi-word: thread (column r, k-group g) walks down its column (k = g, g+4, ...; the
+    // column is contiguous), the 4 k-groups combined through LDS -- the 16-lane cross-lane
+    // reduction of the fp64 layout costs four multi-word additions and 4 x words shuffles per
+    // column there, more than the products themselves at these sizes (K ~ 50)
+    __shared__ T part[4][64];
+    const int r = tid & 63, g = tid >> 6, j = o0 + r;
+    const T* col = A + (size_t)min(j, d.M - 1) * d.lda;
+    T acc0 = T(0.0), acc1 = T(0.0);
+    int k = g;
+    for (; k + 4 < K; k += 8) {
+      acc0 += col[k] * x[k];
+      acc1 += col[k + 4] * x[k + 4];
+    }
+    if (k < K) acc0 += col[k] * x[k];
+    part[g][r] = acc0 + acc1;
+    __syncthreads();
+    if (g == 0 && j < d.M) {
+      T v = ((part[0][r] + part[1][r]) + (part[2][r] + part[3][r])) * T(alpha);
+      if (beta != 0.0) v += d.Cin[j] * T(beta);
+      d.C[j] = v;
     }
   } else {
     const int lane = tid & 63, w = tid >> 6, kk = lane & 15, c4 = lane >> 4;
