@@ -198,8 +198,8 @@ def main():
     # device-side copy, stream-ordered): the instance stagnates near mu ~ 1e-12 after ~100
     # iterations and the fp64 factorisations break down after ~250, so a long --steps window
     # replays iterations 1..RESTART instead.  Every timed step is still one full loop body.
-    # Also back to the snapshot once mu falls below MU_FLOOR (synchronous loop: the last body's
-    # mu): the smaller shards (--clusters 8) reach the stagnation regime (mu ~ 4e-12, dual steps
+    # Also back to the snapshot once mu falls below MU_FLOOR (the last body's mu read back; in
+    # the pipelined loop the body before it): the smaller shards (--clusters 8) reach the stagnation regime (mu ~ 4e-12, dual steps
     # ~1e-3) by iteration ~60, where a loss of definiteness of Y depends on the rounding of
     # single operations -- a healthy window for every shard size.
     RESTART = 64
@@ -227,10 +227,11 @@ def main():
             maybe_restart()
             inflight += 1
             if inflight == 2:
-                _, ran = dev.iterate_wait()
+                st, ran = dev.iterate_wait()
                 inflight -= 1
                 if not ran:
                     raise RuntimeError("solver terminated inside the benchmark window")
+                last_mu[0] = st.mu   # (one body behind: the MU_FLOOR restart comes a body later)
         while inflight:
             _, ran = dev.iterate_wait()
             inflight -= 1
