@@ -897,7 +897,15 @@ struct CholInvPlan : PlanBase {  // A_b -> L_b^-1 (and optionally L_b)
     } else {
       using C = RegCfg<T>;
       static const bool la = !env_off("CLRSDP_CHOL_LA");
-      if (la && nmax <= 64) {  // the look-ahead factorisation with L^-1 (bitwise chol_packed's)
+      // blocks n <= 32 on 4 waves -- one per SIMD, the chain alone on its SIMD -- instead of 16
+      // (C5's X/Y blocks <= 18: 980 -> 1007 it/s, round 5; CLRSDP_LA_SMALL=0 keeps 16)
+      static const bool la_small = !env_off("CLRSDP_LA_SMALL");
+      if (la && la_small && nmax <= 32) {
+        if (std::is_same<T, mw::qd>::value && chol_ldl_on())
+          chol_lookahead<T, true, true, 32, 3><<<nb, 256, 0, s>>>(din, dout, dl, info, la_opts());
+        else
+          chol_lookahead<T, true, false, 32, 3><<<nb, 256, 0, s>>>(din, dout, dl, info, la_opts());
+      } else if (la && nmax <= 64) {  // the look-ahead factorisation with L^-1 (bitwise chol_packed's)
         if (std::is_same<T, mw::qd>::value && chol_ldl_on())
           chol_lookahead<T, true, true, 64><<<nb, 1024, 0, s>>>(din, dout, dl, info, la_opts());
         else

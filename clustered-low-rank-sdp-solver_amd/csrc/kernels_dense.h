@@ -398,15 +398,15 @@ __device__ __forceinline__ T readlane0(const T& v) {
   for (int q = 0; q < (int)(sizeof(T) / 8); ++q) d[q] = readlane_d(s[q], 0);
   return o;
 }
-template <class T, bool INV, bool LDL, int NMAX>
-__global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restrict__ in,
+template <class T, bool INV, bool LDL, int NMAX, int NW = 15>  // NW bulk waves
+__global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>* __restrict__ in,
                                                        const MatDesc<T>* __restrict__ out_inv,
                                                        const MatDesc<T>* __restrict__ out_l,
                                                        int* __restrict__ info, int opts = 0) {
   // opts (A/B switches): bit 0 = the chain wave at raised issue priority (its SIMD also runs
   // three bulk waves); bit 1 = one Newton step for the pivot's reciprocal (from the
   // double-double one: ~2^-208 relative instead of ~2^-212)
-  constexpr int NW = 15;                                 // bulk waves
+  constexpr int NTH = 64 * (NW + 1);
   constexpr int SA = (NMAX * (NMAX + 1) / 2 + 63) / 64;  // 64-element slots of the triangle
   constexpr int KA = (SA + NW - 1) / NW;
   constexpr int SX = (NMAX / 8) * (NMAX / 8 + 1) / 2;    // 8 x 8 tiles of L^-1
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
     // L = U D^1/2 (column c times sqrt d_c, the diagonal sqrt d_c); L^-1 = D^-1/2 U^-1 (row r
     // times 1/sqrt d_r): the n square roots side by side
     if (!fail) {
-      for (int c = tid; c < n; c += 1024) {
+      for (int c = tid; c < n; c += NTH) {
         T sq, rq;
         pivot_sqrt(dgl[c], sq, rq);
         colb[0][c] = sq;
@@ -617,7 +617,7 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
     }
     __syncthreads();
     if (!fail)
-      for (int e = tid; e < n * n; e += 1024) {
+      for (int e = tid; e < n * n; e += NTH) {
         const int r = e % n, c = e / n;
         if (ol.A) {
           if (r > c) ol.A[r + (size_t)c * ol.lda] = ol.A[r + (size_t)c * ol.lda] * colb[0][c];
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(1024) void chol_lookahead(const MatDesc<T>* __restr
         }
       }
   }
-  for (int e = tid; e < n * n; e += 1024) {  // zeros above the diagonal
+  for (int e = tid; e < n * n; e += NTH) {  // zeros above the diagonal
     const int r = e % n, c = e / n;
     if (c > r) {
       if (ol.A) ol.A[r + (size_t)c * ol.lda] = T(0.0);
