@@ -205,10 +205,13 @@ def main():
     RESTART = 64
     MU_FLOOR = 1e-8
     count = [0]
+    # restarts per cause (period / mu floor), reported in the JSON for the timed window
+    restarts = {"period": 0, "mu_floor": 0}
 
     def maybe_restart():
         count[0] += 1
         if count[0] % RESTART == 0 or last_mu[0] < MU_FLOOR:
+            restarts["period" if count[0] % RESTART == 0 else "mu_floor"] += 1
             dev.restore_state()
             feas[0] = False   # the snapshot is the (infeasible) initial point
             last_mu[0] = 1.0
@@ -262,10 +265,12 @@ def main():
         run_bodies(1)   # (re)capture the graph with the events outside the timed region
         schur_live[:] = [0.0, 0]
     barrier_sync()
+    restarts.update(period=0, mu_floor=0)
     t0 = time.perf_counter()
     run_bodies(args.steps)
     barrier_sync()
     dt = time.perf_counter() - t0
+    timed_restarts = dict(restarts)
     if schur_live[1]:
         step = step_plain
         dev.set_timing(False)
@@ -389,6 +394,11 @@ def main():
                                 "(clrsdp_set_graph(0): the ~100 launches of one loop body enqueued "
                                 "eagerly, as the sharded path does), 10 bodies from the initial point"),
         "eager_body_ms": eager_body_ms,
+        # restarts from the post-warm-up snapshot inside the timed window, by cause: every
+        # RESTART = 64 bodies, or once the last body's mu fell below MU_FLOOR = 1e-8 (the
+        # stagnation regime); every timed step is still one full loop body
+        "restarts": {"period": timed_restarts["period"], "mu_floor": timed_restarts["mu_floor"],
+                     "period_every": RESTART, "mu_floor_below": MU_FLOOR},
         "host_loop": ("pipelined (host one loop body behind, device-side pd_feas/terminate)"
                       if pipelined else
                       "synchronous (one hipGraph replay per loop body)" if graph_on else

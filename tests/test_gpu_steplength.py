@@ -229,3 +229,90 @@ def test_eigmin_refined_fp64_eigenpair(pk, words, n):
             nrm = max(abs(x) for x in B.reshape(-1))
             err = abs(mpmath.mpf(g) - ref) / nrm
             assert err <= EIG_TOL[words], (q, float(g), float(ref), float(err))
+
+
+# --- structured batches (the inputs of tools/micro/eig_split_bench.hip) ---
+#
+# An eigmin_split variant of round 5 (the single-wave tail, build r5r) returned lambda_min off by
+# up to 11.2 ||A|| on near-diagonal and decoupled-16-block inputs and at n = 33/64/127 and batch
+# 256, and the small random batches above did not catch it.  These run the structures of that
+# microbenchmark through clrsdp_eigmin at the batch sizes of the loop bodies.
+
+def _structured(kind, n, rng, scale=1.0):
+    """kind 0 random symmetric, 1 near-diagonal SPD, 2 tridiagonal (d_i = i mod 7, e_i = 1),
+    3 random symmetric decoupled into 16 x 16 diagonal blocks (eig_split_bench.hip:68-80)."""
+    A = rng.random((n, n)) - 0.5
+    A = np.tril(A) + np.tril(A, -1).T
+    if kind == 1:
+        A = 1e-3 * A
+        A[np.diag_indices(n)] = 1.0 + 0.1 * (rng.random(n) - 0.5)
+    elif kind == 2:
+        A = np.zeros((n, n))
+        A[np.diag_indices(n)] = np.arange(n) % 7
+        idx = np.arange(n - 1)
+        A[idx + 1, idx] = A[idx, idx + 1] = 1.0
+    elif kind == 3:
+        blk = np.arange(n) // 16
+        A[blk[:, None] != blk[None, :]] = 0.0
+    return A * scale
+
+
+@pytest.mark.parametrize("batch", [64, 256])
+@pytest.mark.parametrize("n", [33, 64, 127, 128])
+def test_eigmin_structured_batches_fp64(pk, n, batch):
+    """fp64 lambda_min (eigmin_split, the loop body's kernel for n <= 128) of batches cycling
+    through the four structures, against numpy eigvalsh, to 1e-12 of the block's spectral
+    radius."""
+    rng = np.random.default_rng(31 * n + batch)
+    blocks = [_structured(q % 4, n, rng) for q in range(batch)]
+    got = pk.eigmin(blocks, precision_words=1)
+    for q, B in enumerate(blocks):
+        ev = np.linalg.eigvalsh(B)
+        rad = max(abs(ev[0]), abs(ev[-1]))
+        assert abs(got[q] - ev[0]) <= 1e-12 * rad, (q, q % 4, got[q], ev[0], abs(got[q] - ev[0]) / rad)
+
+
+@pytest.mark.parametrize("scale", [1e-200, 1e200])
+def test_eigmin_structured_scaled_fp64(pk, scale):
+    """The same structures at n = 128 scaled to the ends of the fp64 range (the Sturm counts'
+    rescaling)."""
+    rng = np.random.default_rng(5)
+    blocks = [_structured(q % 4, 128, rng, scale) for q in range(64)]
+    got = pk.eigmin(blocks, precision_words=1)
+    for q, B in enumerate(blocks):
+        ev = np.linalg.eigvalsh(B / scale) * scale
+        rad = max(abs(ev[0]), abs(ev[-1]))
+        assert abs(got[q] - ev[0]) <= 1e-12 * rad, (q, q % 4, got[q], ev[0])
+
+
+_MP_REF = {}
+
+
+def _mp_ref_structured(kind, n):
+    """(block, 320-bit lambda_min, max-norm) of one structured block, cached across words."""
+    import mpmath
+    key = (kind, n)
+    if key not in _MP_REF:
+        B = _structured(kind, n, np.random.default_rng(900 + 10 * n + kind))
+        with mpmath.workprec(320):
+            Bm = np.array([[mpmath.mpf(float(x)) for x in row] for row in B], dtype=object)
+            _MP_REF[key] = (B, _mp_eigmin(Bm), float(np.max(np.abs(B))))
+    return _MP_REF[key]
+
+
+@pytest.mark.parametrize("words", [2, 4])
+@pytest.mark.parametrize("n", [33, 64])
+def test_eigmin_structured_batches_multiword(pk, words, n):
+    """Multi-word lambda_min (eigmin_mx with its eigmin_lds2 fallback) on a batch of 64 built
+    from the four structures (16 copies each), against 320-bit mpmath at the word's tolerance;
+    copies of one block must give the same value."""
+    import mpmath
+    refs = [_mp_ref_structured(k, n) for k in range(4)]
+    blocks = [refs[q % 4][0] for q in range(64)]
+    got = pk.eigmin(blocks, precision_words=words)
+    with mpmath.workprec(320):
+        for q in range(64):
+            B, ref, nrm = refs[q % 4]
+            err = abs(mpmath.mpf(got[q]) - ref) / nrm
+            assert err <= EIG_TOL[words], (q, q % 4, float(got[q]), float(ref), float(err))
+            assert got[q] == got[q % 4], (q, got[q], got[q % 4])
