@@ -748,6 +748,10 @@ struct MatPlan : PlanBase {  // potrf / eigmin
         // batch of 128 blocks of 128, bitwise the same lambda_min on 1048 of 1056 test blocks
         // (tools/micro/eig_split_bench.hip); CLRSDP_EIG_TAIL=0 keeps the two-barrier loop
         static const bool etail = !env_off("CLRSDP_EIG_TAIL");
+        // (round 6: eigmin_onebar, one barrier per column with the next reflector's
+        // matrix-vector product under the chain's reflector, measured 203 against 143 us per
+        // batch of 128 blocks of 128 -- the bulk waves are VALU-issue bound -- and stays a
+        // microbenchmark, tools/micro/eig_onebar_bench.hip)
         if (reg) eigmin_reg<<<(unsigned)h.size(), 512, 0, s>>>(d, out);
         else if (etail) eigmin_split<0, 24><<<(unsigned)h.size(), 576, 0, s>>>(d, out);
         else eigmin_split<0><<<(unsigned)h.size(), 576, 0, s>>>(d, out);

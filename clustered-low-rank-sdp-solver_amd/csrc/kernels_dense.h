@@ -1658,6 +1658,349 @@ __global__ __launch_bounds__(576) void eigmin_split(const MatDesc<double>* __res
 #undef ES_STAMP
 }
 
+// ------------------------------------------------------------------------------------------
+// eigmin_onebar (round 6): eigmin_split with ONE barrier per column.  eigmin_split runs per
+// column k: the bulk's p = A_k v_k and its reductions -- barrier -- the chain wave's reflector
+// v_{k+1} beside the bulk's rank-2 update -- barrier; the matrix-vector product and its
+// reductions sit between the two barriers on the critical path.  Here they move under the
+// chain's reflector: v_{k+1} = x~ + v0 e_{k+2}, where x~ = row k+1 of A_{k+1} beyond column
+// k+2 is known as soon as K_k is (x_j = o_j - beta v_r p_j + g_r v_j, the chain's own formula on
+// the same operands, so the bulk's copy has the chain's bits), and only the scalar v0 = x_{k+2}
+// - alpha waits for the reflector.  So after the barrier of column k the bulk waves apply the
+// rank-2 update of column k and at once form, with the updated registers,
+//     q = A_{k+1} x~,   c = A_{k+1} e_{k+2}   (per row, in LDS)
+//     S1 = x~^T q,      S2 = x~^T c           (per-wave partials)
+// while the chain wave builds v0 and beta_{k+1} from the same row.  After the next barrier
+//     p_{k+1} = q + v0 c,   v_{k+1}^T p_{k+1} = S1 + v0 S2 + v0 p_{k+1}[k+2]
+// come out of LDS with no further cross-wave exchange.  Chain and bulk form p, K, w_r, g_r and
+// x~ by identical expressions from identical LDS operands, so v_{k+1} is one vector everywhere.
+// Same layout, scaling, Gershgorin bracket and 512-way multisection as eigmin_split.
+// ------------------------------------------------------------------------------------------
+template <int DBG = 0>
+__global__ __launch_bounds__(576) void eigmin_onebar(const MatDesc<double>* __restrict__ descs,
+                                                      double* __restrict__ out) {
+  constexpr int NS = 16, NWB = 8, GS = 4;
+  __shared__ __attribute__((aligned(16))) double rowb[2][128];
+  __shared__ __attribute__((aligned(16))) double qb[2][128];
+  __shared__ __attribute__((aligned(16))) double cb[2][128];
+  __shared__ __attribute__((aligned(16))) double redw[2][2 * NWB];  // (S1, S2) of each bulk wave
+  __shared__ __attribute__((aligned(16))) double scal[2][2];         // v0, beta of the reflector
+  __shared__ double dg[128], e2[128];
+  __shared__ __attribute__((aligned(16))) double sd[128], se[128];
+  __shared__ double bnd[2];
+  __shared__ unsigned long long masks[8];
+  __shared__ double amaxw[NWB];
+  const MatDesc<double> d = descs[blockIdx.x];
+  const int n = d.n, lda = d.lda, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const bool chain = w == NWB;
+  const int blk = w < 4 ? w : 11 - w;  // bulk row block (pairs 0/7, 1/6, 2/5, 3/4 per SIMD)
+  const int c = lane >> 4, t16 = lane & 15;
+  const int i = blk * 16 + t16;       // bulk: this lane's row
+  const int j0 = 2 * c + 8 * t16;     // this lane's column pair (bulk: broadcast slot; chain: x_j)
+  double a[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) a[s][0] = a[s][1] = 0.0;
+  if (!chain) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * c + 8 * s + e;
+        const int ic = min(i, n - 1), jc = min(j, n - 1);
+        const double v = gload(d.A + ic + (size_t)jc * lda);
+        a[s][e] = (i < n && j < n) ? v : 0.0;
+      }
+    double amax = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) amax = fmax(amax, fmax(fabs(a[s][0]), fabs(a[s][1])));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
+    if (lane == 0) amaxw[w] = amax;
+  }
+  __syncthreads();
+  int ex0;
+  {
+    double amax = amaxw[0];
+#pragma unroll
+    for (int r = 1; r < NWB; ++r) amax = fmax(amax, amaxw[r]);
+    ex0 = (amax > 0.0 && amax < INFINITY) ? __builtin_amdgcn_frexp_exp(amax) : 0;
+  }
+  if (!chain) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      a[s][0] = __builtin_ldexp(a[s][0], -ex0);
+      a[s][1] = __builtin_ldexp(a[s][1], -ex0);
+    }
+  }
+  auto publish_row = [&](int r, double* dst) {  // the owners of row r write its 128 entries
+    if (!chain && blk == (r >> 4) && t16 == (r & 15)) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        *reinterpret_cast<double2*>(dst + 2 * c + 8 * s) = make_double2(a[s][0], a[s][1]);
+    }
+  };
+  // chain: v of the current step at the lane's column pair
+  double cx = 0.0, cy = 0.0;
+  // the reflector of row r from x = row r of the current matrix (chain wave only): v_j = 0
+  // (j <= r), v0 (j = r+1), x_j (j > r+1), H = I - beta v v^T; v0 and beta go to scal[r & 1]
+  auto reflector = [&](int r, double xj0, double xj1, double xr, double x0) {
+    double tl = (j0 >= r + 2 ? xj0 * xj0 : 0.0);
+    tl = fma(j0 + 1 >= r + 2 ? xj1 : 0.0, xj1, tl);
+    tl = xsum32(xsum16(row16_sum(tl)));  // sum_{j >= r+2} x_j^2
+    double bt = 0.0, v0 = x0, e2r = x0 * x0;
+    if (tl > 0.0) {
+      const double ss = fma(x0, x0, tl);
+      double nrm;
+      if (ss > 0x1p-900) {  // Newton-refined hardware rsq / rcp (~1 ulp)
+        double rs = __builtin_amdgcn_rsq(ss);
+        rs = rs * fma(-0.5 * ss, rs * rs, 1.5);
+        nrm = ss * rs;
+        nrm = fma(fma(-nrm, nrm, ss), 0.5 * rs, nrm);
+      } else {
+        nrm = sqrt(ss);
+      }
+      const double alpha = x0 > 0.0 ? -nrm : nrm;
+      v0 = x0 - alpha;
+      const double q = fma(v0, v0, tl);
+      double rc = __builtin_amdgcn_rcp(q);
+      rc = fma(fma(-q, rc, 1.0), rc, rc);
+      rc = fma(fma(-q, rc, 1.0), rc, rc);
+      bt = 2.0 * rc;
+      e2r = alpha * alpha;
+    }
+    cx = j0 <= r ? 0.0 : (j0 == r + 1 ? v0 : xj0);
+    cy = j0 + 1 <= r ? 0.0 : (j0 + 1 == r + 1 ? v0 : xj1);
+    if (lane == 0) {
+      *reinterpret_cast<double2*>(scal[r & 1]) = make_double2(v0, bt);
+      dg[r] = xr;
+      e2[r] = e2r;
+    }
+  };
+  // bulk state carried from step to step: x~ at the column pair and at the own row, and the
+  // own row's q and c (full sums, in every lane of the row)
+  double xt0 = 0.0, xt1 = 0.0, xti = 0.0, qi = 0.0, ci = 0.0;
+  // the bulk's product with the freshly updated registers: q = A x~ (x~ at the pair in xt0/xt1,
+  // zero at columns < r + 2), c = column r + 1, the partials S1 = x~^T q, S2 = x~^T c; to LDS
+  // buffer r & 1 (read by the step that applies reflector r)
+  auto product = [&](int r, int lo, bool live) {
+    double pa[4] = {0.0, 0.0, 0.0, 0.0};
+    double cp = 0.0;
+    const int sc = (r + 1) >> 3;
+    // (the column's entry picked by weights, not by a select of a[s][0] / a[s][1]: a runtime
+    // choice between them became an address select and put a[][] in scratch)
+    const double m1 = ((r + 1) & 1) ? 1.0 : 0.0, m0 = 1.0 - m1;
+    if (live && !(DBG & 2)) {
+      static_for<0, NS / GS>([&](auto G) {
+        constexpr int g = decltype(G)::value;
+        if (GS * g + GS - 1 >= lo) {
+          static_for<GS * g, GS * g + GS>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            fmac_bcast<s, s == GS * g>(pa[2 * (s & 1)], xt0, a[s][0]);
+            fmac_bcast<s, false>(pa[2 * (s & 1) + 1], xt1, a[s][1]);
+            if (s == sc) cp = fma(a[s][1], m1, a[s][0] * m0);
+          });
+        }
+      });
+    }
+    cp = (c == (((r + 1) >> 1) & 3)) ? cp : 0.0;
+    const double qq = xsum32(xsum16((pa[0] + pa[1]) + (pa[2] + pa[3])));
+    const double cc = xsum32(xsum16(cp));
+    double t1 = 0.0, t2 = 0.0;
+    if (c == 0) {
+      qb[r & 1][i] = qq;
+      cb[r & 1][i] = cc;
+      t1 = xti * qq;
+      t2 = xti * cc;
+    }
+    t1 = row16_sum(t1);
+    t2 = row16_sum(t2);
+    if (lane == 0) *reinterpret_cast<double2*>(&redw[r & 1][2 * w]) = make_double2(t1, t2);
+    qi = qq;
+    ci = cc;
+  };
+  publish_row(0, rowb[0]);
+  if (n >= 2) publish_row(1, rowb[1]);
+  __syncthreads();
+  if (chain) {
+    __builtin_amdgcn_s_setprio(3);
+    if (n >= 2) {
+      const double2 xr = *reinterpret_cast<const double2*>(&rowb[0][j0]);
+      reflector(0, xr.x, xr.y, rowb[0][0], rowb[0][1]);
+    } else if (lane == 0) {
+      dg[0] = rowb[0][0];
+    }
+  } else if (n >= 2) {
+    // x~_0 = row 0 beyond column 1; q = A_0 x~_0, c = A_0 e_1
+    const double2 o2 = *reinterpret_cast<const double2*>(&rowb[0][j0]);
+    xt0 = j0 >= 2 ? o2.x : 0.0;
+    xt1 = j0 + 1 >= 2 ? o2.y : 0.0;
+    xti = i >= 2 ? rowb[0][i] : 0.0;
+    product(0, 0, blk * 16 < n);
+  }
+  __syncthreads();
+  for (int k = 0; k + 2 < n; ++k) {
+    const int r = k + 1, par = k & 1, rp = r & 1;
+    const int lo = (k + 1) >> 3;  // slots s < lo hold columns <= k only
+    // ---- scalars of step k, identical in every wave: v0, beta, p_r, v^T p, K, w_r, g_r
+    const double2 sv = *reinterpret_cast<const double2*>(scal[par]);
+    const double v0 = sv.x, bk = sv.y;
+    double rw[2 * NWB];
+#pragma unroll
+    for (int q = 0; q < 2 * NWB; q += 2) {
+      const double2 v2 = *reinterpret_cast<const double2*>(&redw[par][q]);
+      rw[q] = v2.x;
+      rw[q + 1] = v2.y;
+    }
+    const double pr = fma(v0, cb[par][r], qb[par][r]);
+    const double2 q2 = *reinterpret_cast<const double2*>(&qb[par][j0]);
+    const double2 c2 = *reinterpret_cast<const double2*>(&cb[par][j0]);
+    const double2 o = *reinterpret_cast<const double2*>(&rowb[rp][j0]);
+    const double s1t = ((rw[0] + rw[2]) + (rw[4] + rw[6])) + ((rw[8] + rw[10]) + (rw[12] + rw[14]));
+    const double s2t = ((rw[1] + rw[3]) + (rw[5] + rw[7])) + ((rw[9] + rw[11]) + (rw[13] + rw[15]));
+    const double tot = fma(v0, pr, fma(v0, s2t, s1t));
+    const double Kc = bk * bk * tot * 0.5;
+    const double vr = v0;
+    const double wr = fma(bk, pr, -(Kc * vr));
+    const double gr = fma(Kc, vr, -wr), mhr = -(bk * vr);
+    // p_k at the column pair (zero at the dead columns <= k)
+    const double px = j0 > k ? fma(v0, c2.x, q2.x) : 0.0;
+    const double py = j0 + 1 > k ? fma(v0, c2.y, q2.y) : 0.0;
+    if (chain) {
+      // ---- row r of A_{k+1} and the reflector v_{k+1} (cx, cy: v_k at the pair)
+      const double orr = rowb[rp][r], or1 = rowb[rp][r + 1];
+      const double pr1 = fma(v0, cb[par][r + 1], qb[par][r + 1]);
+      const int ix = r + 1;  // v_k[r + 1] from the lane holding that column pair
+      const double vr1 = readlane_d((ix & 1) ? cy : cx, 16 * ((ix >> 1) & 3) + (ix >> 3));
+      const double xj0 = fma(cx, gr, fma(px, mhr, o.x));
+      const double xj1 = fma(cy, gr, fma(py, mhr, o.y));
+      const double xr = fma(vr, gr, fma(pr, mhr, orr));
+      const double x0 = fma(vr1, gr, fma(pr1, mhr, or1));
+      if constexpr (DBG & 4) {  // (timing only: no reflector)
+        cx = xj0;
+        cy = xj1;
+        if (lane == 0) {
+          *reinterpret_cast<double2*>(scal[r & 1]) = make_double2(x0, 0.0);
+          dg[r] = xr;
+          e2[r] = 1.0;
+        }
+      } else {
+        reflector(r, xj0, xj1, xr, x0);
+      }
+    } else {
+      const bool live = blk * 16 + 15 >= k + 2 && blk * 16 < n;
+      if (live) {
+        // v_k at the pair and the own row; p_k at the own row; w_i, g_i, h_i
+        const double vx = j0 == r ? v0 : xt0;
+        const double vy = j0 + 1 == r ? v0 : xt1;
+        const double vi = i == r ? v0 : xti;
+        const double pi = fma(v0, ci, qi);
+        const double wi = fma(bk, pi, -(Kc * vi));
+        const double gi = fma(Kc, vi, -wi), mhi = -(bk * vi);
+        // x~_{k+1} = row r of A_{k+1} beyond column r + 1 (the chain's formula)
+        const double oi = rowb[rp][i];
+        const double nx0 = fma(vx, gr, fma(px, mhr, o.x));
+        const double nx1 = fma(vy, gr, fma(py, mhr, o.y));
+        const double nxi = fma(vi, gr, fma(pi, mhr, oi));
+        // ---- A_{k+1} = A_k - v w^T - w v^T: a_ij += h_i p_j + g_i v_j
+        if (!(DBG & 1)) static_for<0, NS / GS>([&](auto G) {
+          constexpr int g = decltype(G)::value;
+          if (GS * g + GS - 1 >= lo) {
+            static_for<GS * g, GS * g + GS>([&](auto S) {
+              constexpr int s = decltype(S)::value;
+              fmac_bcast<s, s == GS * g>(a[s][0], px, mhi);
+              fmac_bcast<s, false>(a[s][1], py, mhi);
+            });
+            static_for<GS * g, GS * g + GS>([&](auto S) {
+              constexpr int s = decltype(S)::value;
+              fmac_bcast<s, false>(a[s][0], vx, gi);
+              fmac_bcast<s, false>(a[s][1], vy, gi);
+            });
+          }
+        });
+        xt0 = j0 >= r + 2 ? nx0 : 0.0;
+        xt1 = j0 + 1 >= r + 2 ? nx1 : 0.0;
+        xti = i >= r + 2 ? nxi : 0.0;
+        // ---- q = A_{k+1} x~, c = A_{k+1} e_{r+1} and the partials for step k + 1
+        product(r, lo, true);
+        publish_row(k + 2, rowb[par]);
+      } else {
+        // no row beyond k + 1 here: zero q, c and partials (rows >= n stay exactly zero)
+        xt0 = xt1 = xti = 0.0;
+        product(r, lo, false);
+      }
+    }
+    __syncthreads();
+  }
+  if (chain) __builtin_amdgcn_s_setprio(0);
+  // the last diagonal entry: row n-1 as its owners published it at the last step (or at the start)
+  if (tid == 0 && n >= 2) dg[n - 1] = rowb[(n - 1) & 1][n - 1];
+  __syncthreads();
+  // Gershgorin interval, scaling and 512-way multisection: as eigmin_split
+  int bnd_ex = 0;
+  {
+    double lo = INFINITY, hi = -INFINITY;
+    if (tid < n) {
+      double rr = 0.0;
+      if (tid > 0) rr += sqrt(e2[tid - 1]);
+      if (tid + 1 < n) rr += sqrt(e2[tid]);
+      lo = dg[tid] - rr;
+      hi = dg[tid] + rr;
+    }
+    if (w < 2) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o));
+        hi = fmax(hi, __shfl_xor(hi, o));
+      }
+      if (lane == 0) {
+        reinterpret_cast<double*>(masks)[2 * w] = lo;
+        reinterpret_cast<double*>(masks)[2 * w + 1] = hi;
+      }
+    }
+    __syncthreads();
+    const double* m = reinterpret_cast<const double*>(masks);
+    const double l = fmin(m[0], m[2]), h = fmax(m[1], m[3]);
+    const double mag = fmax(fabs(l), fabs(h));
+    const int ex = (mag > 0.0 && mag < INFINITY) ? __builtin_amdgcn_frexp_exp(mag) : 0;
+    bnd_ex = ex;
+    if (tid < 128) {
+      sd[tid] = tid < n ? __builtin_ldexp(dg[tid], -ex) : 4.0;
+      se[tid] = (tid >= 1 && tid < n) ? fmax(__builtin_ldexp(e2[tid - 1], -2 * ex), 0x1p-900) : 0.0;
+    }
+    if (tid == 0) {
+      const double ls = __builtin_ldexp(l, -ex), hs = __builtin_ldexp(h, -ex);
+      const double span = hs - ls;
+      bnd[0] = ls - span * 1e-3 - 1e-300;
+      bnd[1] = hs + span * 1e-3 + 1e-300;
+    }
+  }
+  __syncthreads();
+  double lo = bnd[0], hi = bnd[1];
+  const int nr = (n + 7) & ~7;
+  constexpr double NSIG = 64.0 * NWB + 1.0;
+  for (int it = 0; it < 6; ++it) {
+    const double width = hi - lo;
+    if (w < NWB) {
+      const double sigma = lo + width * ((double)(tid + 1) / NSIG);
+      const bool below = sturm_any_below(sd, se, nr, sigma);
+      const unsigned long long mk = __ballot(below);
+      if (lane == 0) masks[w] = mk;
+    }
+    __syncthreads();
+    int f = -1;
+    for (int q = 0; q < NWB && f < 0; ++q)
+      if (masks[q]) f = q * 64 + __ffsll((long long)masks[q]) - 1;
+    __syncthreads();
+    if (f < 0) {
+      lo = lo + width * ((NSIG - 1.0) / NSIG);
+    } else {
+      hi = lo + width * ((double)(f + 1) / NSIG);
+      if (f > 0) lo = lo + width * ((double)f / NSIG);
+    }
+  }
+  if (tid == 0) out[blockIdx.x] = __builtin_ldexp((lo + hi) * 0.5, bnd_ex + ex0);
+}
+
 #ifdef CLRSDP_EIG_STAMPS
 __device__ unsigned long long g_eig_stamps[8];
 #define EIG_STAMP(slot)                                                     \
