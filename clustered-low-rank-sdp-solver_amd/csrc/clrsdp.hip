@@ -150,8 +150,20 @@ template <> struct RegCfg<qd> { static constexpr int TR = 1, TC = 1, GR = 32, GC
 // chol_lookahead's switches (CLRSDP_LA_OPTS, kernels_dense.h).  Default 2: one Newton step for
 // the quad-double pivot reciprocal (~2^-208 relative; the second step was a third of the chain:
 // C5 879 -> 930 it/s, round 5 A/B); bit 0 (chain priority) measured nothing
+// Only bits 0 and 1 exist; any other value of CLRSDP_LA_OPTS (not a number, other bits) is
+// rejected with a message and the default kept.
 inline int la_opts() {
-  static const int o = std::getenv("CLRSDP_LA_OPTS") ? std::atoi(std::getenv("CLRSDP_LA_OPTS")) : 2;
+  static const int o = [] {
+    const char* e = std::getenv("CLRSDP_LA_OPTS");
+    if (!e) return 2;
+    char* end = nullptr;
+    const long v = std::strtol(e, &end, 10);
+    if (end == e || *end != '\0' || v < 0 || (v & ~3L)) {
+      std::fprintf(stderr, "clrsdp: CLRSDP_LA_OPTS=%s ignored (bits 0 and 1 only); using 2\n", e);
+      return 2;
+    }
+    return (int)v;
+  }();
   return o;
 }
 template <class T> constexpr int reg_nmax() { return std::is_same<T, double>::value ? 128 : RegCfg<T>::TR * RegCfg<T>::GR; }
@@ -496,26 +508,26 @@ struct ChainPlan {
   }
 };
 
-template <bool DB, int TS, int PF = 1>
+template <bool DB, int TS>
 void launch_uni_db(const UniGemm& u, hipStream_t s, bool ta, bool tb, bool sca, bool sym, int tag,
                    unsigned long long* stamp, double alpha, double beta, const double* ds, double dmult) {
   constexpr int NW = TS == 64 ? 8 : 2, NT = 64 * NW;
   const unsigned tiles = (unsigned)(u.P * (int)cdiv(u.M, TS) * u.tn);
   if (sca) {
-    gemm_f64_uni<false, true, 0, 32, NW, false, true, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    gemm_f64_uni<false, true, 0, 32, NW, false, true, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
   } else if (sym) {
     if (beta != 0.0 || ds) throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: beta = 0 only"};
     const unsigned grid = (unsigned)(u.P * u.tsym);
-    if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, true, false, DB, TS, PF><<<grid, NT, 0, s>>>(u, alpha, 0.0);
-    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, true, false, DB, TS, PF><<<grid, NT, 0, s>>>(u, alpha, 0.0);
+    if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, true, false, DB, TS><<<grid, NT, 0, s>>>(u, alpha, 0.0);
+    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, true, false, DB, TS><<<grid, NT, 0, s>>>(u, alpha, 0.0);
     else throw ClrsdpError{CLRSDP_E_ARG, "symmetric GEMM epilogue: op(A) = A only"};
   } else {
-    if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
-    else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
-    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
-    else if (ta && !tb) gemm_f64_uni<true, false, 0, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
-    else if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
-    else gemm_f64_uni<true, true, 0, 32, NW, false, false, DB, TS, PF><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    if (tag == 1 && !ta && tb) gemm_f64_uni<false, true, 1, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+    else if (tag == 3 && !ta && tb) gemm_f64_uni<false, true, 3, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult, stamp);
+    else if (!ta && !tb) gemm_f64_uni<false, false, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else if (ta && !tb) gemm_f64_uni<true, false, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else if (!ta && tb) gemm_f64_uni<false, true, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
+    else gemm_f64_uni<true, true, 0, 32, NW, false, false, DB, TS><<<tiles, NT, 0, s>>>(u, alpha, beta, ds, dmult);
   }
   HIPCHK(hipGetLastError());
 }
@@ -529,14 +541,7 @@ void GemmPlan<T>::launch_uni_impl(hipStream_t s, double alpha, double beta, cons
       const char* e = std::getenv("CLRSDP_UNI_DB");
       return !(e && e[0] == '0');
     }();
-    // CLRSDP_GEMM_PF=2: two slabs in flight ahead of the MFMAs instead of one (opt-in: C3
-    // 1205-1210 against 1208-1212 it/s, A/B round 5 -- the k-loop is not load-latency bound)
-    static const bool pf2 = [] {
-      const char* e = std::getenv("CLRSDP_GEMM_PF");
-      return e && e[0] == '2';
-    }();
     if (uts == 32) launch_uni_db<true, 32>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
-    else if (db && pf2) launch_uni_db<true, 64, 2>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
     else if (db) launch_uni_db<true, 64>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
     else launch_uni_db<false, 64>(ug, s, ta, tb, sca, sym, tag, stamp, alpha, beta, ds, dmult);
   }
@@ -1742,7 +1747,7 @@ struct Solver final : HandleBase {
       // launches ran 14.8 + 21.4 us against 13.4 + 11.8 for the four GEMVs, and slab_qsolve
       // summing four partial slabs per cluster 13.7 against 9.0 us: 1195-1232 against 1248-1270
       // it/s, A/B round 5 -- fewer workgroups with longer load chains lose to more, shorter ones)
-      static const bool cl_env = env_on("CLRSDP_CL_SOLVE");
+      const bool cl_env = env_on("CLRSDP_CL_SOLVE");  // (per handle: tests switch it)
       const long long cnt = (long long)std::max(nc(), 1) * std::max(cls_nrb, 1);
       cls_on = cl_env && std::is_same<T, double>::value && reg_S && reg_Q && nc() > 0 &&
                cls_nrb <= 4 && (long long)cdiv(n_y, 64) * cnt * n_y <= (1LL << 20) &&
@@ -2159,10 +2164,6 @@ struct Solver final : HandleBase {
   }
   void scalars(const clrsdp_params* prm, int pd_feas, int which) {
     ScalarParams<T> p = prm ? sparams(prm, pd_feas) : ScalarParams<T>{};
-    // CLRSDP_SC_LDS=1: the slots mirrored in LDS for the launch (opt-in: C3 1256-1269 against
-    // 1273-1279 it/s without, A/B round 5)
-    static const int sc_lds = env_on("CLRSDP_SC_LDS") ? 1 : 0;
-    p.lds = sc_lds;
     p.zero_cy = zero_cy ? 1 : 0;
     p.zero_n = zero_info ? info_count - 1 : 0;  // status words of this iteration (not the halt word)
     p.zero_ptr = info;
@@ -3011,6 +3012,8 @@ struct Solver final : HandleBase {
     }
     HIPCHK(hipEventRecord(ev_q, aux));
     pending_q = true;
+    if (capturing && inject_capture_fail)
+      throw ClrsdpError{CLRSDP_E_HIP, "injected capture failure (CLRSDP_INJECT_CAPTURE_FAIL)"};
     mark(CLRSDP_STAGE_RESIDUALS);
     HIPCHK(hipStreamWaitEvent(main_s, ev_r, 0));
     residuals_finish();
@@ -3091,8 +3094,11 @@ struct Solver final : HandleBase {
       hipGraph_t graph = nullptr;
       HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
       try {
+        capturing = true;
         enqueue_iteration(prm, pd_feas);
+        capturing = false;
       } catch (...) {
+        capturing = false;
         // join the side stream (it may have been forked into the capture) so that the capture
         // ends cleanly and the streams stay usable
         if (aux != stream && hipEventRecord(ev_join, aux) == hipSuccess)
@@ -3115,8 +3121,23 @@ struct Solver final : HandleBase {
   // A sharded body whose capture fails (CLRSDP_GRAPH_RCCL with an RCCL that cannot be captured)
   // is enqueued eagerly instead, and the handle stays eager from then on; one rank rethrows (its
   // capture has no collective in it, so a failure there is a real error)
+  // CLRSDP_INJECT_CAPTURE_FAIL=1 (tests only, read per handle): the first capture of a loop body
+  // throws half-way through its enqueue, after the side streams were forked and the pending
+  // flags set, and the body takes the sharded path's eager fallback even at one rank
+  bool inject_capture_fail = env_on("CLRSDP_INJECT_CAPTURE_FAIL");
+  bool capturing = false;
+  // the per-body enqueue state a failed (partial) capture may have left set; an eager re-enqueue
+  // must not wait on events recorded only inside the aborted capture
+  void reset_body_state() {
+    pending_q = pending_x21 = pending_sinv = false;
+    ty_ahead = false;
+    w_split = false;
+    dy_dot_ready = false;
+    alpha_fused = false;
+    fuse_alpha = false;
+  }
   void launch_graph_or_eager(const clrsdp_params* prm, int pd_feas) {
-    if (world == 1) {
+    if (world == 1 && !inject_capture_fail) {
       launch_graph(prm, pd_feas);
       return;
     }
@@ -3126,6 +3147,8 @@ struct Solver final : HandleBase {
       std::fprintf(stderr, "clrsdp: graph capture of the sharded loop body failed (%s); "
                            "enqueueing it eagerly from now on\n", e.msg.c_str());
       graph_rccl = false;
+      inject_capture_fail = false;
+      reset_body_state();
       enqueue_iteration(prm, pd_feas);
     }
   }

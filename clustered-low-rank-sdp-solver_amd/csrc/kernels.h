@@ -67,12 +67,16 @@ __device__ inline double gload(const double* p) { return *(gdptr)p; }
 namespace lds_gemm {
 // Staging of one R x BK slab of an operand (NTH threads, R*BK/NTH elements per thread; R = 64,
 // or 32 for the small-tile GEMM).  kcontig: element (i, k) at P[k + i*ld], kept in LDS as
-// S[i*(BK+2) + k]; else at P[i + k*ld], kept as S[k*LM + i] (LM = R + 16: the four k-rows of a
+// S[i*(BK+1) + k]; else at P[i + k*ld], kept as S[k*LM + i] (LM = R + 16: the four k-rows of a
 // fragment read start 32 banks apart).  Rows i beyond `rows` are clamped (their products are
 // never stored); k beyond K is zeroed.
+// The k-contiguous pitch is odd (round 6; BK + 2 before): hipcc reads two k-steps of a fragment
+// with one ds_read2_b64 (k, k + 4), whose 16-lane groups bank by dword mod 32, and an even pitch
+// put rows i and i + 8 of a group on one bank (2-way: the 0.15 / 0.30 SQ_LDS_BANK_CONFLICT
+// shares of gemm_f64_uni / gemm_f64_dyn in round 5)
 constexpr int LSM = 80;
 template <int BK, int NTH = 256, int R = 64> struct Slab {
-  static constexpr int PER = R * BK / NTH, LSK = BK + 2, LM = R + 16;
+  static constexpr int PER = R * BK / NTH, LSK = BK + 1, LM = R + 16;
   static_assert(PER * NTH == R * BK, "slab split");
   static constexpr int SZ = R * LSK > BK * LM ? R * LSK : BK * LM;  // doubles per image
   template <bool kcontig>
@@ -137,12 +141,9 @@ constexpr int gemm_f64_smem() {
 // (MPMP.jl:1659) formed while the slab is staged, with scale_cols's operation order
 // DB: double-buffered slabs (two LDS images per operand): the next slab is stored into the
 // other image while no wave reads it, so each k-step needs one barrier instead of two
-// PF = 2 (with DB): two slabs in flight ahead of the one the MFMAs read (two register sets,
-// alternating), so a slab's global loads have two k-steps of MFMA work to arrive in instead of
-// one -- the k-loop of a 64-wide tile is latency-bound at one slab ahead (~1 us per 32-k step
-// of MFMAs against the loads' latency under a full launch)
-template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false, bool DB = false, int TS = 64,
-          int PF = 1>
+// (round 6: the opt-in two-slab prefetch, CLRSDP_GEMM_PF=2, measured within noise in round 5
+// and is gone)
+template <bool TA, bool TB, int BK, int NW, bool SYM, bool SCA = false, bool DB = false, int TS = 64>
 __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, double* smem,
                                               double alpha, double beta,
                                               const double* __restrict__ dscal, double dmult) {
@@ -203,59 +204,24 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
   SL::template load<AK>(ra, d.A, d.lda, m0, M, 0, K, tid);
   SL::template load<BKc>(rb, d.B, d.ldb, n0, N, 0, K, tid);
   load_w(0);
-  if constexpr (PF == 2 && DB) {
-    // register sets: slab s + 1 is in set (s + 1) & 1 while the MFMAs read LDS image s & 1
-    double ra2[PER], rb2[PER], wa2[SCA ? PER : 1], wl2[SCA ? PER : 1];
-    scale_a();
-    SL::template store<AK>(ra, smem, tid, 0, K);
-    SL::template store<BKc>(rb, smem + SL::SZ, tid, 0, K);
-    const int nk = (K + BK - 1) / BK;
-    auto load_set = [&](auto SET, int k0) {
-      constexpr int st = decltype(SET)::value;
-      double(&xa)[PER] = st ? ra2 : ra;
-      double(&xb)[PER] = st ? rb2 : rb;
-      SL::template load<AK>(xa, d.A, d.lda, m0, M, k0, K, tid);
-      SL::template load<BKc>(xb, d.B, d.ldb, n0, N, k0, K, tid);
-      if constexpr (SCA) {
+  // the epilogue's C_in (beta != 0) and diagonal scalar, loaded now, behind the first slab: in
+  // the epilogue each C_in load sat between stores to C that may alias it (R -= dX dY is in
+  // place), so the compiler waited for every one of them in turn (CPT serial round trips)
+  const int rl = tid % TS, row = m0 + rl, c0 = tid / TS;
+  constexpr int CPT = TS * TS / NTH, CST = NTH / TS;
+  double cin[SYM ? 1 : CPT];
+  double dsv = 0.0;
+  if constexpr (!SYM) {
+    if (beta != 0.0) {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-          int i, k;
-          SL::template kk<AK>(tid, q, i, k);
-          const int kc = min(k0 + k, K - 1);
-          (st ? wa2 : wa)[q] = gload(d.sa + kc);
-          (st ? wl2 : wl)[q] = gload(d.sl + kc);
-        }
+      for (int c = 0; c < CPT; ++c) {
+        const int col = min(n0 + c0 + CST * c, N - 1);
+        cin[c] = gload(d.Cin + min(row, M - 1) + (size_t)col * d.ldcin);
       }
-    };
-    auto store_set = [&](auto SET, double* img, int k0) {
-      constexpr int st = decltype(SET)::value;
-      double(&xa)[PER] = st ? ra2 : ra;
-      double(&xb)[PER] = st ? rb2 : rb;
-      if constexpr (SCA) {
-#pragma unroll
-        for (int q = 0; q < PER; ++q) xa[q] = xa[q] * ((st ? wa2 : wa)[q] * (st ? wl2 : wl)[q]);
-      }
-      SL::template store<AK>(xa, img, tid, k0, K);
-      SL::template store<BKc>(xb, img + SL::SZ, tid, k0, K);
-    };
-    if (nk > 1) load_set(std::integral_constant<int, 1>{}, BK);  // slab 1 -> set 1
-    __syncthreads();
-    // step s: slab s + 2 -> set s & 1 (free: slab s is in LDS), MFMAs on image s & 1, then
-    // slab s + 1 (set (s + 1) & 1) -> image (s + 1) & 1
-    auto step = [&](auto PAR, int sidx) {
-      constexpr int par = decltype(PAR)::value;
-      if (sidx + 2 < nk) load_set(std::integral_constant<int, par>{}, (sidx + 2) * BK);
-      mfma_slab(smem + par * 2 * SL::SZ, smem + par * 2 * SL::SZ + SL::SZ);
-      if (sidx + 1 < nk) {
-        store_set(std::integral_constant<int, par ^ 1>{}, smem + (par ^ 1) * 2 * SL::SZ, (sidx + 1) * BK);
-        __syncthreads();
-      }
-    };
-    for (int sidx = 0; sidx < nk; sidx += 2) {
-      step(std::integral_constant<int, 0>{}, sidx);
-      if (sidx + 1 < nk) step(std::integral_constant<int, 1>{}, sidx + 1);
     }
-  } else {
+    if (dscal) dsv = gload(dscal);
+  }
+  {
   scale_a();
   SL::template store<AK>(ra, As, tid, 0, K);
   SL::template store<BKc>(rb, Bs, tid, 0, K);
@@ -299,8 +265,6 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
   __syncthreads();
   // thread -> row rl of the tile (consecutive threads, consecutive rows: coalesced), columns
   // cl = tid / TS + (NTH / TS) c
-  const int rl = tid % TS, row = m0 + rl, c0 = tid / TS;
-  constexpr int CPT = TS * TS / NTH, CST = NTH / TS;
   if constexpr (SYM) {
 #pragma unroll 4
     for (int c = 0; c < CPT; ++c) {
@@ -315,15 +279,17 @@ __device__ __forceinline__ void gemm_f64_tile(const GemmDesc<double>& d, int t, 
     }
     return;
   }
-  if (row < M) {
-#pragma unroll 4
-    for (int c = 0; c < CPT; ++c) {
-      const int cl = c0 + CST * c, col = n0 + cl;
-      if (col < N) {
-        double v = alpha * smem[rl * TP + cl];
-        if (beta != 0.0) v += beta * d.Cin[row + (size_t)col * d.ldcin];
-        if (dscal && row == col) v += dmult * *dscal;  // fused "+ s I" (square diagonal blocks)
-        d.C[row + (size_t)col * d.ldc] = v;
+  if constexpr (!SYM) {
+    if (row < M) {
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const int cl = c0 + CST * c, col = n0 + cl;
+        if (col < N) {
+          double v = alpha * smem[rl * TP + cl];
+          if (beta != 0.0) v += beta * cin[c];
+          if (dscal && row == col) v += dmult * dsv;  // fused "+ s I" (square diagonal blocks)
+          d.C[row + (size_t)col * d.ldc] = v;
+        }
       }
     }
   }
@@ -374,7 +340,7 @@ __device__ inline void lower_tile(int q, int& tm, int& tn) {
   tn = q - tm * (tm + 1) / 2;
 }
 template <bool TA, bool TB, int TAG = 0, int BK = 32, int NW = 8, bool SYM = false, bool SCA = false,
-          bool DB = true, int TS = 64, int PF = 1>
+          bool DB = true, int TS = 64>
 __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double alpha, double beta,
                                                         const double* __restrict__ dscal = nullptr,
                                                         double dmult = 0.0,
@@ -399,7 +365,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_uni(const UniGemm u, double 
     lower_tile(q, tm, tc);
     t = tm * u.tn + tc;
   }
-  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA, DB, TS, PF>(d, t, smem, alpha, beta, dscal, dmult);
+  gemm_f64_tile<TA, TB, BK, NW, SYM, SCA, DB, TS>(d, t, smem, alpha, beta, dscal, dmult);
   if constexpr (TAG == 1 || TAG == 3)
     if (stamp) {
       __syncthreads();
@@ -3131,7 +3097,6 @@ template <class T> struct ScalarParams {
   int nred;
   int zero_cy;  // which == 3 without C: <C,Y> = 0
   int fold_all;  // fp64: fold_all_f64 (all loads of all folds in flight; CLRSDP_FOLD_ALL=0: off)
-  int lds;       // the slots mirrored in LDS for the launch (one load, the changed ones written back)
   int zero_n;   // zero the status words zero_ptr[0..zero_n) (start of an iteration)
   int* zero_ptr;
   int* halt_ptr;  // which == 0: status word "skip this loop body" (device-decided termination)
@@ -3345,21 +3310,13 @@ __device__ __forceinline__ void scalar_logic(T* sc, const ScalarParams<T>& p, in
   }
 }
 
-// p.lds: the slots are read once into LDS (one coalesced load, with the guard words' loads in
-// flight beside it), the launch works there, and the slots it may change are written back --
-// instead of lane 0's chain of dependent global reads after its own writes
+// (the opt-in LDS mirror of the slots, CLRSDP_SC_LDS=1, measured within noise in round 5 and is
+// gone, round 6)
 template <class T>
 __global__ __launch_bounds__(64) void scalar_kernel(T* scg, ScalarParams<T> p, int which) {
   const int lane = threadIdx.x;
-  __shared__ __attribute__((aligned(16))) unsigned char scbuf[SC_COUNT * sizeof(T)];
-  T* sc = p.lds ? reinterpret_cast<T*>(scbuf) : scg;
+  T* sc = scg;
   bool fl = false;  // any status word set (which == 3): the wave reads them strided, one ballot
-  if (p.lds) {
-    if (which == 3)
-      for (int e = lane; e < p.nguard; e += 64) fl = fl || p.guard[e] != 0;
-    for (int e = lane; e < SC_COUNT; e += 64) sc[e] = scg[e];
-    __syncthreads();
-  }
   for (int e = lane; e < p.zero_n; e += 64) p.zero_ptr[e] = 0;
   if (sizeof(T) == 8 && p.fold_all) {
     if constexpr (sizeof(T) == 8) fold_all_f64(p, sc, lane);
@@ -3374,24 +3331,10 @@ __global__ __launch_bounds__(64) void scalar_kernel(T* scg, ScalarParams<T> p, i
       }
     }
   }
-  if (which == 3 && !p.lds)
+  if (which == 3)
     for (int e = lane; e < p.nguard; e += 64) fl = fl || p.guard[e] != 0;
   const bool failed = __any(fl);
   if (lane == 0) scalar_logic(sc, p, which, failed);
-  if (p.lds) {  // write back the fold targets and the slots of `which`
-    __syncthreads();
-    unsigned m = 0;
-#pragma unroll
-    for (int q = 0; q < 6; ++q)
-      if (q < p.nred) m |= 1u << p.red[q].dst;
-    if (which == 0) m |= (1u << SC_MU) | (1u << SC_MU_P);
-    else if (which == 1) m |= (1u << SC_R) | (1u << SC_BETA) | (1u << SC_BETA_C) | (1u << SC_MU_C) | (1u << SC_DMU);
-    else if (which == 2) m |= (1u << SC_ALPHA_P) | (1u << SC_ALPHA_D);
-    else if (which == 3 || which == 4)
-      m |= (1u << SC_DOT_CY) | (1u << SC_POBJ) | (1u << SC_DOBJ) | (1u << SC_GAP) | (1u << SC_PDFEAS) | (1u << SC_HALT);
-    for (int e = lane; e < SC_COUNT; e += 64)
-      if ((m >> e) & 1u) scg[e] = sc[e];
-  }
 }
 
 // x += alpha_p dx, y += alpha_d dy (guarded), then <c,x>, <b,y> and the objectives

@@ -385,7 +385,11 @@ __global__ __launch_bounds__(NT) void chol_packed(const MatDesc<T>* __restrict__
 // The chain's step (one multi-word FMA per lane, the pivot, one product per lane) and the bulk's
 // update run side by side: a phase costs max(chain, bulk) + one barrier, where chol_packed's
 // step costs chain + bulk + two barriers.  Every element sees the same operations in the same
-// order as in chol_packed (column j's term at step j), so the factors are bitwise chol_packed's.
+// order as in chol_packed (column j's term at step j), so the factors are bitwise chol_packed's
+// -- except at quad-double with opts bit 1 (the default): the LDL pivot reciprocal then takes one
+// Newton step from the double-double one (~2^-208 relative instead of chol_packed's ~2^-212), so
+// those factors agree with chol_packed's to that level, not bitwise
+// (tests/test_gpu_lu.py::test_chol_lookahead_qd_one_newton_step).
 // LDL (quad-double): A = U D U^T, then L = U D^1/2 with all n square roots side by side.
 // MPMP.jl:1433-1442 / 1499-1505 (the factorisations of S_j and Q; the reference's approx_lu!).
 // ------------------------------------------------------------------------------------------
