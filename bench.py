@@ -92,6 +92,32 @@ def schur_pmc_traffic(config, precision, world, clusters=0):
     return d.get("traffic_bytes_per_iteration"), f"{src} (build {cur})"
 
 
+def schur_pmc_issued(config, precision, world, clusters=0):
+    """The fp64 MFMA work the Schur kernel actually issues, as a fraction of peak
+    (SQ_INSTS_VALU_MFMA_F64 x 2048 flop over its average duration, tools/pmc_kernels.py), from the
+    newest committed profiles/rNN_kernels_pmc.json taken on this very build, beside `frac`, which
+    prices the launch on the reference's redundant algorithmic flop count.  The
+    fused kernel skips the lower tiles and the symmetric half of the pairing, so it issues fewer
+    flops than that count.  None (with the reason) otherwise."""
+    import glob
+    if config != "c3" or precision != 1 or world != 1 or clusters not in (0, 64):
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_kernels_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    import _clrsdp_pkg
+    cur = _clrsdp_pkg.load_build().source_hash()
+    src = os.path.relpath(files[-1], ROOT)
+    if d.get("source_hash") != cur:
+        return None, f"stale: {src} was counted on build {d.get('source_hash')}, this is build {cur}"
+    k = d.get("kernels", {}).get("schur_fused_f64")
+    if not k:
+        return None, f"{src} holds no schur_fused_f64 record"
+    return k.get("issued_frac_of_peak"), f"{src} (build {cur}): schur_fused_f64 MFMA instructions issued"
+
+
 def cpu_baseline(pk, cons, b, bi, precision=1, budget_s=15.0):
     """Time the C++/OpenMP restatement of the reference algorithm (oracle/cpu_restatement.cpp:
     the same loop body as MPMP.jl:755-887 with approx_lu! for S_j and Q, threaded over the
@@ -335,6 +361,7 @@ def main():
                      "pairs) of first workgroup start to last workgroup end, inside the replayed "
                      "graph, averaged over the timed region")
     traffic, traffic_src = schur_pmc_traffic(args.config, args.precision, world, args.clusters)
+    issued, issued_src = schur_pmc_issued(args.config, args.precision, world, args.clusters)
     achieved = fl / sch_s / 1e12   # in flops of the word type (multi-word flops when w > 1)
     peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]
     # the library's default (clrsdp.hip use_graph / graph_ok): replay at world 1 unless
@@ -374,7 +401,9 @@ def main():
                      "peak_source": "MI355X fp64 matrix spec" if args.precision == 1 else
                                     "measured %s multiply-add ceiling x 2 (profiles/r01_mw_peak.log)"
                                     % DTYPES[args.precision],
-                     "frac": achieved / peak, "traffic": traffic,
+                     "frac": achieved / peak,
+                     "issued_frac": issued, "issued_frac_source": issued_src,
+                     "traffic": traffic,
                      "traffic_source": traffic_src,
                      "alg_bytes_per_iteration": by,
                      "schur_ms_per_iteration": sch_s * 1e3,
