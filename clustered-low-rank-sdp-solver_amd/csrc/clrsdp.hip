@@ -1783,6 +1783,8 @@ struct Solver final : HandleBase {
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q, &e_X, &e_Y}) f->finalize();
   }
 
+  bool schur_grp2 = !env_off("CLRSDP_SCHUR_GRP2");  // (per handle: tests switch it)
+  bool any_grp2 = false;
   void build_fast_schur() {
     if constexpr (std::is_same<T, double>::value) {
       p_txy.tag = 1;
@@ -1802,25 +1804,34 @@ struct Solver final : HandleBase {
       int bi = 0;
       for (int c = 0; c < nc(); ++c) {
         const int j = oc[c];
-        bool direct = Lc[j] == 1;
-        for (int l = 0; l < Lc[j] && direct; ++l) {
+        bool direct = Lc[j] == 1, grp2 = Lc[j] == 1;
+        for (int l = 0; l < Lc[j] && (direct || grp2); ++l) {
           const LBlk& b = lb[bi + l];
-          for (int k = 0; k < b.N; ++k) direct = direct && ranks_all[rkoff_g[b.gjl] + k] == 1;
+          for (int k = 0; k < b.N; ++k) {
+            direct = direct && ranks_all[rkoff_g[b.gjl] + k] == 1;
+            grp2 = grp2 && ranks_all[rkoff_g[b.gjl] + k] == 2;
+          }
         }
+        // every sample of rank 2 (C2): the pairs kernel sums the 2 x 2 groups into S itself
+        // (CLRSDP_SCHUR_GRP2=0: G and schur_gsum, for A/B)
+        grp2 = grp2 && schur_grp2;
         for (int l = 0; l < Lc[j]; ++l) {
           const LBlk& b = lb[bi + l];
           if (b.K == 0) continue;
           PairTileDesc t;
           t.Vt = Vt + b.voff; t.TXt = TX + b.toff; t.TYt = TY + b.toff; t.lam = lam + b.koff;
-          t.G = direct ? S + c_Soff[c] : BX + b.boff;
-          t.ldG = b.K;
+          t.G = (direct || grp2) ? S + c_Soff[c] : BX + b.boff;
+          t.ldG = grp2 ? (int)Ds[j] : b.K;
+          t.grp = grp2 ? 2 : 1;
+          t.pad = 0;
           t.AY = AY + b.ayoff;
           t.K = b.K; t.del = b.del; t.tile0 = 0;
           const int nt = cdiv(b.K, 64);
           pnt.push_back(nt * (nt + 1) / 2);
           ptd.push_back(t);
         }
-        if (!direct) {
+        if (grp2) any_grp2 = true;
+        if (!direct && !grp2) {
           SchurClusterDesc g;
           g.m = 1; g.N = (int)Ns[j]; g.D = (int)Ds[j]; g.blk0 = bi; g.nblk = (int)Lc[j];
           g.pair0 = 0; g.S_off = c_Soff[c];
@@ -1857,6 +1868,7 @@ struct Solver final : HandleBase {
           f.Vt = t.Vt; f.Xinv = Xinv + b.off; f.TYt = t.TYt; f.Y = Y + b.off; f.lam = t.lam;
           f.G = t.G; f.AY = t.AY;
           f.K = t.K; f.del = t.del; f.ldG = t.ldG; f.ldx = b.n; f.ldy = b.n;
+          f.grp = t.grp; f.pad = 0;
           fpd.push_back(f);
           fnt.push_back(cdiv(b.K, 64));
         }

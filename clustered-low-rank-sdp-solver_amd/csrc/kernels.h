@@ -1994,6 +1994,11 @@ struct PairTileDesc {
   double* G;          // K x K (ld ldG): S itself when L = 1 and every rank is 1
   double* AY;         // K
   int K, del, ldG, tile0;
+  // grp = 2 (round 6): L = 1 and every sample of rank 2, the vectors ordered (k, rho): G is S
+  // itself (ld ldG = D) and each 2 x 2 group of the tile is summed in the epilogue,
+  // S[a, b] = sum_{rho1, rho2} G[2a + rho1, 2b + rho2] (MPMP.jl:1373-1398 at m = 1) -- no K x K
+  // intermediate and no schur_gsum launch.  grp = 1: G written per (p, q) as before.
+  int grp, pad;
 };
 
 template <int BK = 16>
@@ -2086,6 +2091,36 @@ __global__ __launch_bounds__(256) void schur_pairs_f64(const PairTileDesc* __res
         if (I == J && pl == ql && p0 + pl < K) d.AY[p0 + pl] = yv;
       }
   __syncthreads();
+  if (d.grp == 2) {
+    // the 32 x 32 tile of S at (p0 / 2, q0 / 2): S[a, b] = sum of the 2 x 2 group of
+    // lambda_p lambda_q T[p][q]; a diagonal tile (I == J) takes a <= b and mirrors it (the
+    // quarter its skipped wave left holds a > b only).  Two passes, each with consecutive threads
+    // on consecutive rows of what they store: S[a, b] (thread -> a) and S[b, a] (thread -> b)
+    const int D = d.K >> 1, a0 = p0 >> 1, b0 = q0 >> 1;
+    auto gsum = [&](int al, int bl) {
+      const int p = 2 * al, q = 2 * bl;
+      return (lamS[p] * lamS[64 + q] * Tt[p * TP + q] + lamS[p] * lamS[64 + q + 1] * Tt[p * TP + q + 1]) +
+             (lamS[p + 1] * lamS[64 + q] * Tt[(p + 1) * TP + q] +
+              lamS[p + 1] * lamS[64 + q + 1] * Tt[(p + 1) * TP + q + 1]);
+    };
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int al = tid & 31, bl = (tid >> 5) + 8 * c;
+      const int a = a0 + al, bb = b0 + bl;
+      if (a < D && bb < D && (I < J || al <= bl)) d.G[a + (size_t)bb * d.ldG] = gsum(al, bl);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int bl = tid & 31, al = (tid >> 5) + 8 * c;
+      const int a = a0 + al, bb = b0 + bl;
+      if (a < D && bb < D && (I < J || al < bl)) d.G[bb + (size_t)a * d.ldG] = gsum(al, bl);
+    }
+    if (stamp) {
+      __syncthreads();
+      if (threadIdx.x == 0) atomicMax(stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    return;
+  }
   // G[p, q] for p <= q: lane -> p, wave -> 16 columns q;  mirror G[q, p] for p < q: lane -> q
   {
     const int pl = lane, p = p0 + pl;
@@ -2156,6 +2191,7 @@ struct FusedPairDesc {
   double* G;           // K x K, ld ldG
   double* AY;          // K
   int K, del, ldG, ldx, ldy;
+  int grp, pad;        // grp = 2: S itself, the 2 x 2 rank groups summed (PairTileDesc::grp)
 };
 namespace schur_fused {
 constexpr int BK = 32;                  // phase-1 k-slab
@@ -2386,7 +2422,28 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     // (p, q) and its mirror (q, p) from the staging tile as 64-row column segments (lower
     // triangle only unless full: the tile whose row block is the larger one, and p >= q of a
     // diagonal tile)
-    {
+    if (d.grp == 2) {
+      // rank 2: the 32 x 32 tile of S at (a0 / 2, b0 / 2), each entry the sum of its 2 x 2 group
+      // of the staged tile; the same triangle rules as below, in S's coordinates
+      const int D = K >> 1, sa0 = a0 >> 1, sb0 = b0 >> 1;
+      const bool w_pq = full || a > b, w_qp = full || b > a;
+      auto gs = [&](int al, int bl) {
+        const int p = 2 * al, q = 2 * bl;
+        return (St[st_idx(p, q)] + St[st_idx(p, q + 1)]) + (St[st_idx(p + 1, q)] + St[st_idx(p + 1, q + 1)]);
+      };
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int al = tid & 31, bl = (tid >> 5) + 16 * c;
+        if (sa0 + al < D && sb0 + bl < D && (diag ? full && al <= bl : w_pq))
+          d.G[(sa0 + al) + (size_t)(sb0 + bl) * d.ldG] = gs(al, bl);
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int bl = tid & 31, al = (tid >> 5) + 16 * c;
+        if (sb0 + bl < D && sa0 + al < D && (diag ? bl > al || (!full && bl == al) : w_qp))
+          d.G[(sb0 + bl) + (size_t)(sa0 + al) * d.ldG] = gs(al, bl);
+      }
+    } else {
       const int il = tid & 63;
       const bool w_pq = full || a > b, w_qp = full || b > a;
 #pragma unroll

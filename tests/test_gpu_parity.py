@@ -136,6 +136,22 @@ def test_stage_parity_fp64_64x64_tiles(pk, oracle, cfg, monkeypatch):
     _stage_compare(pk, oracle, cons, b)
 
 
+@pytest.mark.parametrize("cfg", [dict(J=3, delta=4, rank=2, n_y=5), dict(J=2, delta=64, rank=2, n_y=64),
+                                 dict(J=3, delta=100, rank=2, n_y=40)],
+                         ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+@pytest.mark.parametrize("grp2", ["0", "1", "1-fused"])
+def test_stage_parity_fp64_rank2_group_sums(pk, oracle, cfg, grp2, monkeypatch):
+    """Rank-2 clusters (C2: every sample a pair of vectors): schur_pairs_f64 summing each 2 x 2
+    group of the pairing tile straight into S ("1", the default; K = 14, 254 and 398 -- a partial
+    last tile and dim_S 199), the same in schur_fused_f64's epilogue ("1-fused"), against the G
+    arena + schur_gsum path ("0"): every stage against the oracle (the 4-term formula,
+    MPMP.jl:1373-1398)."""
+    monkeypatch.setenv("CLRSDP_SCHUR_GRP2", grp2[0])
+    monkeypatch.setenv("CLRSDP_SCHUR_FUSED", "1" if grp2 == "1-fused" else "0")
+    cons, b = pk.synth(seed=4, **cfg)
+    _stage_compare(pk, oracle, cons, b)
+
+
 @pytest.mark.parametrize("fused", ["0", "1", "1-ty"])
 @pytest.mark.parametrize("cfg", CONFIGS_GPU[-4:-1], ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_stage_parity_fp64_schur_paths(pk, oracle, cfg, fused, monkeypatch):

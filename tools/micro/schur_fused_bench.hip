@@ -56,6 +56,8 @@ int main() {
   std::vector<FusedPairDesc> fd;
   for (int j = 0; j < J; ++j) {
     PairTileDesc t;
+    t.grp = 1;
+    t.pad = 0;
     t.Vt = Vt + (size_t)j * K * D; t.TXt = TX + (size_t)j * K * D; t.TYt = TY + (size_t)j * K * D;
     t.lam = lam + (size_t)j * K; t.G = G0 + (size_t)j * K * K; t.AY = AY0 + (size_t)j * K;
     t.K = K; t.del = D; t.ldG = K; t.tile0 = 0;
@@ -64,6 +66,7 @@ int main() {
     f.Vt = t.Vt; f.Xinv = Xi + (size_t)j * D * D; f.TYt = t.TYt; f.lam = t.lam;
     f.G = G1 + (size_t)j * K * K; f.AY = AY1 + (size_t)j * K; f.K = K; f.del = D; f.ldG = K; f.ldx = D;
     f.Y = Xi + (size_t)j * D * D; f.ldy = D;  // (any symmetric matrix: timing only)
+    f.grp = 1; f.pad = 0;
     fd.push_back(f);
   }
   std::vector<TileRef> pt, ft;
