@@ -1446,6 +1446,14 @@ struct Solver final : HandleBase {
       f_Y.add(LY + b.off, n, n);
       ci_XY.add(X + b.off, n, n, LX + b.off, n);
       q_xinv.add(LX + b.off, n, LX + b.off, n, nullptr, n, Xinv + b.off, n, n, n, n);
+      if constexpr (std::is_same<T, double>::value) {
+        p_xir.add_op(true, false, 1.0, 0.0, LX + b.off, n, LX + b.off, n, nullptr, n, Xinv + b.off, n, n, n, n);
+        p_xir.add_op(false, false, -1.0, 0.0, X + b.off, n, Y + b.off, n, nullptr, n, R + b.off, n, n, n, n);
+        if (!p_xir.h.empty()) {
+          p_xir.h.back().flags |= 16;  // + mu_p I
+          p_xir.h.back().sa = sc + SC_MU_P;
+        }
+      }
       // step length: L^-1 dM L^-T for X and Y in the same two launches (Y's middle product in Z)
       q_sx1.add(LX + b.off, n, dX + b.off, n, nullptr, n, tA + b.off, n, n, n, n);
       q_sx1.add(LY + b.off, n, dY + b.off, n, nullptr, n, Z + b.off, n, n, n, n);
@@ -1773,7 +1781,7 @@ struct Solver final : HandleBase {
                            &p_Z, &p_dXY, &p_dY, &q_xinv, &q_sx1, &q_sx2, &q_sy1, &q_sy2, &q_W,
                            &q_t, &q_Wdy, &q_dx, &q_q1, &q_q2, &q_qinv, &q_qdy, &f_a, &f_b, &f_c, &f_d, &f_x1, &f_x2, &f_w, &f_w2,
                            &q_t2, &q_dx2, &q_qinv2,
-                           &p_wA_Ps, &p_wA_dXs})
+                           &p_wA_Ps, &p_wA_dXs, &p_xir})
       g->finalize();
     for (CholInvPlan<T>* c : {&ci_XY, &ci_S, &ci_S22, &ci_Q}) c->finalize();
     e_XY.finalize();
@@ -2242,8 +2250,14 @@ struct Solver final : HandleBase {
   // ---------------- stages
   void st_mu_r(const clrsdp_params* prm, int pd_feas) {
     mu_scalars(prm, pd_feas);
-    mu_r_gemm();
+    if (!fuse_r) mu_r_gemm();
   }
+  // (round 6) a loop body at fp64 forms R = mu_p I - XY in XINV's launch, beside
+  // X^-1 = L^-T L^-1: a mixed batch (gemm_f64_dyn, the mu_p diagonal from the scalar slot) instead
+  // of a 128^3 GEMM launch of its own on the critical path before chol_inv(X, Y) -- R is first
+  // read by the predictor's Z after SCHUR.  CLRSDP_FUSE_R=0 keeps the separate launch.
+  bool fuse_r = false;
+  GemmPlan<T> p_xir;
   // mu = <X,Y>/dim, mu_p (and the status words cleared, the halt word decided)
   void mu_scalars(const clrsdp_params* prm, int pd_feas) {
     blk_dot(X, Y, nullptr, nullptr, 0, SC_DOT_XY, 1, upart);
@@ -2277,10 +2291,17 @@ struct Solver final : HandleBase {
   void st_xinv() {
     if (reg_blk) {  // L_X^-1 and L_Y^-1 on chip in one launch, X^-1 = L^-T L^-1 on MFMA
       ci_XY.launch(stream, info);
-      if (lu_x()) xinv_lu();
-      else q_xinv.launch(stream, 1.0, 0.0);
+      if (lu_x()) {
+        xinv_lu();
+        if (fuse_r) mu_r_gemm();
+      } else if (fuse_r) {
+        p_xir.launch(stream, 1.0, 0.0);  // {X^-1 = L^-T L^-1 | R = mu_p I - XY}
+      } else {
+        q_xinv.launch(stream, 1.0, 0.0);
+      }
       return;
     }
+    if (fuse_r) mu_r_gemm();
     blk_lin(LX, X, 1.0, nullptr, 0.0);
     f_X.potrf(stream, info);
     if (lu_x()) {
@@ -2513,14 +2534,19 @@ struct Solver final : HandleBase {
     if (nx > 0) vec_reduce<T><<<1, vec_reduce_threads<T>(), 0, stream>>>(dvec, nullptr, nx, 2, tmpsc + 1);
     else fill(tmpsc + 1, 0.0, 1);
   }
-  void residuals_finish() {
+  // defer (a loop body at one rank): the three error maxima are only read by the log and the
+  // loop control at UPDATE, so their folds ride in CORRECTOR_R's scalar launch instead of a launch
+  // of their own on the critical path before the predictor's solves (their sources, tmpsc and p,
+  // are not written again before it; with world > 1 they come from the exchange buffer, which the
+  // solves' all-gathers overwrite, so they are flushed here)
+  void residuals_finish(bool defer = false) {
     const int64_t k = n_y + 2;
     if (world == 1 && nc()) {  // p = b - sum_j B_j^T x_j in one launch; maxima folded
       slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, pvec, bvec, 1.0, -1.0);
       fold(tmpsc, 1, 2, SC_ERR_PMAT);
       fold(tmpsc + 1, 1, 2, SC_ERR_DVEC);
       fold(pvec, (int)n_y, 4, SC_ERR_PVEC);
-      flush_scalars();
+      if (!defer) flush_scalars();
       return;
     }
     if (nc()) slab_sum4<T><<<cdiv(n_y, 64), 256, 0, stream>>>(pslab, nc(), n_y, n_y, xsend);
@@ -2971,6 +2997,8 @@ struct Solver final : HandleBase {
       StreamSwitch on_aux(stream, aux);
       work();
     };
+    static const bool fr = !env_off("CLRSDP_FUSE_R");
+    fuse_r = fr && std::is_same<T, double>::value && timing != 1 && !p_xir.h.empty();
     mark(CLRSDP_STAGE_MU_R);
     stage(CLRSDP_STAGE_MU_R, prm, pd_feas);
     // V^T Y of the Schur stage only needs the state: it runs beside chol_inv(X, Y), which leaves
@@ -2992,6 +3020,7 @@ struct Solver final : HandleBase {
       });
     mark(CLRSDP_STAGE_XINV);
     stage(CLRSDP_STAGE_XINV, prm, pd_feas);
+    fuse_r = false;
     mark(CLRSDP_STAGE_SCHUR);
     stage(CLRSDP_STAGE_SCHUR, prm, pd_feas);
     // (Z waits for SCHUR although it could start after XINV: beside the MFMA-bound Schur
@@ -3028,7 +3057,8 @@ struct Solver final : HandleBase {
       throw ClrsdpError{CLRSDP_E_HIP, "injected capture failure (CLRSDP_INJECT_CAPTURE_FAIL)"};
     mark(CLRSDP_STAGE_RESIDUALS);
     HIPCHK(hipStreamWaitEvent(main_s, ev_r, 0));
-    residuals_finish();
+    static const bool defer_res = !env_off("CLRSDP_DEFER_RES");  // (round 6; =0 for A/B)
+    residuals_finish(defer_res && timing != 1);
     if (keep_res) copy_guarded(pres, pvec, n_y);
     HIPCHK(hipGetLastError());
     mark(CLRSDP_STAGE_PREDICTOR);
@@ -3147,6 +3177,7 @@ struct Solver final : HandleBase {
     dy_dot_ready = false;
     alpha_fused = false;
     fuse_alpha = false;
+    fuse_r = false;
   }
   void launch_graph_or_eager(const clrsdp_params* prm, int pd_feas) {
     if (world == 1 && !inject_capture_fail) {

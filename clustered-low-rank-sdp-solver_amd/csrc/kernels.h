@@ -621,11 +621,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_f64_dyn(const GemmDesc<double>* 
   const GemmDesc<double> d = descs[tr.p];
   if (d.flags & 8) __builtin_amdgcn_s_setprio(2);
   const double al = (d.flags & 4) ? d.alpha : alpha, be = (d.flags & 4) ? d.beta : beta;
+  // flags bit 4: "+ s I" on the diagonal of a square problem, s = *d.sa (the descriptor's scaled-A
+  // pointer, unused by these unscaled products): R = mu_p I - XY in XINV's mixed batch
+  const double* ds = (d.flags & 16) ? d.sa : nullptr;
+  const double dm = (d.flags & 16) ? 1.0 : 0.0;
   switch (d.flags & 3) {
-    case 0: gemm_f64_tile<false, false, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
-    case 1: gemm_f64_tile<true, false, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
-    case 2: gemm_f64_tile<false, true, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
-    default: gemm_f64_tile<true, true, BK, NW, false>(d, tr.t, smem, al, be, nullptr, 0.0); break;
+    case 0: gemm_f64_tile<false, false, BK, NW, false>(d, tr.t, smem, al, be, ds, dm); break;
+    case 1: gemm_f64_tile<true, false, BK, NW, false>(d, tr.t, smem, al, be, ds, dm); break;
+    case 2: gemm_f64_tile<false, true, BK, NW, false>(d, tr.t, smem, al, be, ds, dm); break;
+    default: gemm_f64_tile<true, true, BK, NW, false>(d, tr.t, smem, al, be, ds, dm); break;
   }
 }
 
