@@ -1053,6 +1053,12 @@ struct Solver final : HandleBase {
   GemmPlan<T> q_xinv, q_sx1, q_sx2, q_sy1, q_sy2, q_W, q_t, q_Wdy, q_dx, q_q1, q_q2, q_qinv, q_qdy;
   // fp64, uniform blocks: Z, dY and the step-length products as one strip-chain launch each
   ChainPlan c_Z, c_dY, c_step, c_trZ;
+  ChainPlan c_stepX, c_stepY;             // the step-length congruences apart (xy_ov)
+  MatPlan<T> e_Xs, e_Ys;                  // their eigen launches apart
+  bool xy_ov_ok = false;   // the overlapped step length is configured (small batches, opt-in)
+  bool xy_ov_body = false; // enqueue_iteration: the corrector may fork the X step length
+  bool xy_ov = false;      // it did: STEP runs the Y half and joins ev_stx
+  hipEvent_t ev_dxo = nullptr, ev_stx = nullptr;
   // fp64 FACTOR with every dim_S <= 256 (fac2): f_a = {W = L^-1 B | L21^T = L11^-1 S12, W1} and
   // f_b = {W^T W | S22 - L21 L21^T, W1^T W1, B2 - L21 W1} as mixed batches, then (dim_S > 128)
   // chol_inv(S22), f_c: W2 = L22^-1 B2', f_d: slab += W2^T W2 (measured 1% faster than one
@@ -1265,7 +1271,7 @@ struct Solver final : HandleBase {
       else HIPCHK(hipStreamCreateWithFlags(&aux2, hipStreamNonBlocking));
     }
     for (hipEvent_t* e : {&ev_m, &ev_x, &ev_s, &ev_r, &ev_qa, &ev_q, &ev_x2, &ev_x21, &ev_ty, &ev_join,
-                          &ev_fa, &ev_w, &ev_join2, &ev_sp, &ev_sinv})
+                          &ev_fa, &ev_w, &ev_join2, &ev_sp, &ev_sinv, &ev_dxo, &ev_stx})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     allocate();
     build_plans();
@@ -1536,6 +1542,23 @@ struct Solver final : HandleBase {
         c_step.init(n0, nbk, 2, true, true);
         c_step.set(0, dX, LX, nullptr, LX, tB);  // L_X^-1 dX L_X^-T
         c_step.set(1, dY, LY, nullptr, LY, tC);  // L_Y^-1 dY L_Y^-T
+        // the X and Y halves apart, for the overlapped step length of small batches (below)
+        c_stepX.init(n0, nbk, 1, true, true);
+        c_stepX.set(0, dX, LX, nullptr, LX, tB);
+        c_stepY.init(n0, nbk, 1, true, true);
+        c_stepY.set(0, dY, LY, nullptr, LY, tC);
+        for (const LBlk& b : lb) {
+          e_Xs.add(tB + b.off, b.n, b.n);
+          e_Ys.add(tC + b.off, b.n, b.n);
+        }
+        e_Xs.finalize();
+        e_Ys.finalize();
+        // CLRSDP_XY_OVERLAP=1 (round 6): with at most
+        // CLRSDP_XY_OVERLAP_MAX (32) local blocks the X step length (its congruence and eigen
+        // launch) runs on the side stream as soon as the corrector's dX exists, beside dY and
+        // the Y step length.  Measured, not the default.
+        const char* eo = std::getenv("CLRSDP_XY_OVERLAP_MAX");
+        xy_ov_ok = env_on("CLRSDP_XY_OVERLAP") && nb() <= (eo ? std::atoi(eo) : 32);
       }
     }
     n_blk_m = (int)bdm.size();
@@ -2602,6 +2625,15 @@ struct Solver final : HandleBase {
     seg(CLRSDP_INNER_SOLVE, [&] { direction_solves(tag); });
     // dX = P + sum_i dx_i A_i
     seg(CLRSDP_INNER_DX, [&] { weighted_A(dx, p_wA_dX, dX, 1.0); });
+    if (tag == 6 && xy_ov_body && xy_ov_ok && aux != stream) {
+      // the X step length beside dY and the Y one (STEP joins it)
+      HIPCHK(hipEventRecord(ev_dxo, stream));
+      HIPCHK(hipStreamWaitEvent(aux, ev_dxo, 0));
+      c_stepX.launch(aux, 1.0, 0.0);
+      e_Xs.eigmin(aux, eigX);
+      HIPCHK(hipEventRecord(ev_stx, aux));
+      xy_ov = true;
+    }
     // dY = sym(X^-1 (R - dX Y))
     seg(CLRSDP_INNER_DY, [&] {
       if (c_dY.on) {
@@ -2767,13 +2799,20 @@ struct Solver final : HandleBase {
   void st_step(const clrsdp_params* prm, int pd_feas) {
     if (reg_blk) {
       // L_X^-1, L_Y^-1 from the X^-1 stage;  M = L^-1 dM L^-T on MFMA; one eigen launch
-      if (c_step.on) {
-        c_step.launch(stream, 1.0, 0.0);          // X and Y blocks together, one launch
+      if (xy_ov) {  // (the X half is on the side stream since dX)
+        c_stepY.launch(stream, 1.0, 0.0);
+        e_Ys.eigmin(stream, eigY);
+        HIPCHK(hipStreamWaitEvent(stream, ev_stx, 0));
+        xy_ov = false;
       } else {
-        q_sx1.launch(stream, 1.0, 0.0);           // X and Y blocks together
-        q_sx2.launch(stream, 1.0, 0.0);
+        if (c_step.on) {
+          c_step.launch(stream, 1.0, 0.0);        // X and Y blocks together, one launch
+        } else {
+          q_sx1.launch(stream, 1.0, 0.0);         // X and Y blocks together
+          q_sx2.launch(stream, 1.0, 0.0);
+        }
+        e_XY.eigmin(stream, eigX);
       }
-      e_XY.eigmin(stream, eigX);
     } else {
       // X: L_X from the X^-1 stage
       blk_lin(tA, dX, 1.0, nullptr, 0.0);
@@ -3067,11 +3106,17 @@ struct Solver final : HandleBase {
     // launch; the per-stage timing mode keeps it so STEP's time includes alpha)
     static const bool fa = !env_off("CLRSDP_FUSE_ALPHA");
     fuse_alpha = fa && timing != 1;
+    xy_ov_body = timing != 1;
     for (int s = CLRSDP_STAGE_CORRECTOR_R; s < CLRSDP_NUM_STAGES; ++s) {
       mark(s);
       stage(s, prm, pd_feas);
     }
     fuse_alpha = false;
+    xy_ov_body = false;
+    if (xy_ov) {  // (STEP did not run: join the side stream anyway)
+      HIPCHK(hipStreamWaitEvent(stream, ev_stx, 0));
+      xy_ov = false;
+    }
     if (pending_q) {
       HIPCHK(hipStreamWaitEvent(stream, ev_q, 0));
       pending_q = false;
@@ -3178,6 +3223,7 @@ struct Solver final : HandleBase {
     alpha_fused = false;
     fuse_alpha = false;
     fuse_r = false;
+    xy_ov_body = xy_ov = false;
   }
   void launch_graph_or_eager(const clrsdp_params* prm, int pd_feas) {
     if (world == 1 && !inject_capture_fail) {

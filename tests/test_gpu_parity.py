@@ -718,3 +718,28 @@ def test_failed_capture_falls_back_eagerly(pk, monkeypatch):
         finally:
             dev.close()
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_overlapped_step_length_equals_joint(pk, monkeypatch):
+    """CLRSDP_XY_OVERLAP=1 (small batches): the X step length (its congruence and eigen launch)
+    on the side stream from the corrector's dX on, beside dY and the Y step length; the same
+    kernels per block, so five loop bodies give bitwise the iterates of the joint launches."""
+    cons, b = pk.synth(seed=6, J=3, delta=128, rank=1, n_y=16)
+    bi = pk.get_block_info(cons)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    outs = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("CLRSDP_XY_OVERLAP", ov)
+        dev = pk.DeviceSolver(cons, b, bi)
+        try:
+            dev.set_state(*pk.initial_point(bi, 10.0, 10.0))
+            for _ in range(5):
+                st = dev.iterate(P, False)
+            x, X, y, Y = dev.get_state()
+            outs.append((np.concatenate([np.ravel(x), np.ravel(y)] +
+                                        [np.ravel(m) for bj in X + Y for m in bj]),
+                         st.alpha_p, st.alpha_d))
+        finally:
+            dev.close()
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert outs[0][1:] == outs[1][1:]
