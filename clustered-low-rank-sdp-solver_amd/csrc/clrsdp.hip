@@ -316,6 +316,11 @@ struct GemmPlan : PlanBase {
   // prio: raised wave priority for a critical-path batch that runs beside side-stream work
   // (gemm_f64_uni / gemm_f64_dyn; set before finalize)
   bool prio = false;
+  // upper (multi-word, round 6): every problem square with a symmetric product of which only the
+  // tiles on and above the diagonal are wanted (the Schur pairings V^T X^-1 V, V^T Y V of m = 1
+  // blocks: schur_assemble reads (min, max)); the launch lists those tiles only -- half the
+  // VALU-bound multi-word work
+  bool upper = false;
   void finalize() {
     if (h.empty()) return;
     if (sca && (ta || !tb || !std::is_same<T, double>::value))
@@ -341,6 +346,12 @@ struct GemmPlan : PlanBase {
       for (int t = 0; t < mx; ++t)
         for (size_t p = 0; p < h.size(); ++p)
           if (t < ntiles[p] && t / h[p].tn >= t % h[p].tn) t2d.push_back(TileRef{(int)p, t});
+    } else if (upper && !gemv && !std::is_same<T, double>::value) {
+      int mx = 0;
+      for (int n : ntiles) mx = std::max(mx, n);
+      for (int t = 0; t < mx; ++t)
+        for (size_t p = 0; p < h.size(); ++p)
+          if (t < ntiles[p] && t / h[p].tn <= t % h[p].tn) t2d.push_back(TileRef{(int)p, t});
     } else {
       t2d = tile_major(ntiles);
     }
@@ -997,6 +1008,7 @@ struct Solver final : HandleBase {
   std::vector<int64_t> c_xoff, c_Soff, c_Boff;   // per local cluster
   int64_t nx = 0, nblk_el = 0, nV = 0, nK = 0, nT = 0, nBX = 0, nAY = 0, nS = 0, nB = 0, nRS = 0;
   bool anyMgt1 = false, hasC = false;
+  bool mw_pair_upper = false;  // BX / BY hold their upper triangles only (schur_assemble reads (min, max))
   int nc2 = 0;  // clusters factorised as 2x2 blocks (s_single < dim_S <= 256, fp64)
   // the largest fp64 S_j factorised (and inverted) by ONE chol_inv_tiles launch: 256 with
   // CLRSDP_CHOL256=1 (chol_inv_tiles<256>, 768 threads: no 2x2 blocking, no X21 / W1 side
@@ -1423,6 +1435,10 @@ struct Solver final : HandleBase {
     q_q2.ta = true;
     p_xinv.ta = true;
     p_s2x.ta = p_s2y.ta = true;
+    // (multi-word, every block m = 1: only the upper tiles of the symmetric pairings; CLRSDP_MW_PAIR_UPPER=0
+    // computes both triangles)
+    mw_pair_upper = !std::is_same<T, double>::value && !anyMgt1 && !env_off("CLRSDP_MW_PAIR_UPPER");
+    p_s2x.upper = p_s2y.upper = mw_pair_upper;
     p_Q.ta = true;
     p_wA_P.tb = p_wA_dX.tb = true;
     p_Btx.ta = true;
@@ -2381,7 +2397,7 @@ struct Solver final : HandleBase {
     if (nb()) extract_AY<T><<<nb(), 256, 0, stream>>>(d_ayd, BY, AY);
     if (n_pairs)
       schur_assemble<T><<<cdiv(n_pairs, 256), 256, 0, stream>>>(d_scd, nc(), d_sbd, rsums, lam, BX,
-                                                                 BY, S, n_pairs);
+                                                                 BY, S, n_pairs, mw_pair_upper ? 1 : 0);
   }
   void st_factor() {
     factor_local();

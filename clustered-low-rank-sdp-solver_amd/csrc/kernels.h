@@ -1931,7 +1931,8 @@ __global__ __launch_bounds__(256) void schur_assemble(const SchurClusterDesc* __
                                                       const T* __restrict__ lam,
                                                       const T* __restrict__ BX,
                                                       const T* __restrict__ BY,
-                                                      T* __restrict__ S, long long npairs) {
+                                                      T* __restrict__ S, long long npairs,
+                                                      int upper = 0) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= npairs) return;
   int lo = 0, hi = ncl - 1;  // find the cluster: last c with pair0 <= g
@@ -1965,6 +1966,11 @@ __global__ __launch_bounds__(256) void schur_assemble(const SchurClusterDesc* __
     const T* lb = lam + B.lam_off;
     for (int p1 = rsum[k1]; p1 < rsum[k1 + 1]; ++p1) {
       for (int p2 = rsum[k2]; p2 < rsum[k2 + 1]; ++p2) {
+        if (upper) {  // m = 1 with BX, BY symmetric and only their upper triangles formed
+          const int lo = min(p1, p2), hi = max(p1, p2);
+          tot += bx[lo + (size_t)hi * ld] * by[lo + (size_t)hi * ld] * lb[p1] * lb[p2];
+          continue;
+        }
         const int r1s = p1 + K * r1, s1s = p1 + K * s1, r2s = p2 + K * r2, s2s = p2 + K * s2;
         T t = bx[s1s + (size_t)r2s * ld] * by[s2s + (size_t)r1s * ld];
         t += bx[r1s + (size_t)r2s * ld] * by[s2s + (size_t)s1s * ld];
