@@ -703,9 +703,26 @@ struct MatPlan : PlanBase {  // potrf / eigmin
   // CLRSDP_REG_POTRF=0 keeps potrf_batched.
   bool reg_potrf = false;
   int* redo = nullptr;  // eigmin_mx's per-block fallback flags
+  // blocked multi-word potrf across workgroups (potrf_blk_*, kernels_dense.h; round 6): taken
+  // for the double-double blocks above 64 (CLRSDP_POTRF_BLK=0 keeps chol_lookahead there).
+  // 16-column panels: n = 127 x 16 blocks 230 -> 155 us (32-column panels: 201 us), while at
+  // n <= 64 the one-CU chol_lookahead stays ahead (52 against 73 us; tools/micro/potrf_blk_bench)
+  static constexpr int BLK_NB = 16;
+  BlkPotrfDesc<T>* bd = nullptr;
+  bool blk = false;
   void finalize() {
     if (h.empty()) return;
     d = own(h);
+    if constexpr (std::is_same<T, mw::dd>::value) {
+      blk = nmax > 64 && !env_off("CLRSDP_POTRF_BLK");
+      if (blk) {
+        T* li = own(std::vector<T>(h.size() * BLK_NB * BLK_NB, T(0.0)));
+        std::vector<BlkPotrfDesc<T>> b(h.size());
+        for (size_t q = 0; q < h.size(); ++q)
+          b[q] = BlkPotrfDesc<T>{h[q].A, li + q * BLK_NB * BLK_NB, h[q].n, h[q].lda};
+        bd = own(b);
+      }
+    }
     if (!std::is_same<T, double>::value) redo = own(std::vector<int>(h.size(), 1));
     const char* e = std::getenv("CLRSDP_REG_POTRF");
     // (double-double blocks 65..128: chol_packed only, CLRSDP_CHOL_PACKED128=0 keeps
@@ -716,6 +733,22 @@ struct MatPlan : PlanBase {  // potrf / eigmin
   }
   void potrf(hipStream_t s, int* info) const {
     if (h.empty()) return;
+    if constexpr (std::is_same<T, mw::dd>::value) {
+      if (blk) {
+        constexpr int NB = BLK_NB, DT = NB / 16;
+        const unsigned nm = (unsigned)h.size();
+        potrf_blk_first<T, false, NB><<<nm, 256, 0, s>>>(bd, info, la_opts());
+        for (int k0 = 0; k0 + NB < nmax; k0 += NB) {
+          const int rows = nmax - k0 - NB, ntr = cdiv(rows, 16);
+          int tiles = 0;  // lower 16-tiles of the trailing matrix outside the next diagonal block
+          for (int I = DT; I < ntr; ++I) tiles += I + 1;
+          potrf_blk_trsm<T, NB><<<dim3((unsigned)ntr, nm), 256, 0, s>>>(bd, k0);
+          potrf_blk_update<T, false, NB><<<dim3(1u + tiles, nm), 256, 0, s>>>(bd, k0, info, la_opts());
+        }
+        HIPCHK(hipGetLastError());
+        return;
+      }
+    }
     if constexpr (!std::is_same<T, double>::value) {
       // the look-ahead potrf (chol_lookahead: the pivot chain beside the trailing update, bitwise
       // chol_packed's factors); CLRSDP_CHOL_LA=0 keeps chol_packed

@@ -373,6 +373,26 @@ __global__ __launch_bounds__(NT) void chol_packed(const MatDesc<T>* __restrict__
   }
 }
 
+// chol_lookahead's per-column timestamps (tools/micro/potrf_blk_bench.hip; compiled out in the
+// library): [block][wave 0 / 1][column][point]
+#ifdef CLRSDP_LA_TRACE
+__device__ unsigned long long g_la_trace[64 * 2 * 128 * 4];
+#define LA_STAMP(q) do { if (lane == 0 && w < 2 && j < 128 && blockIdx.x < 64 && blockIdx.y == 0) \
+  g_la_trace[((blockIdx.x * 2 + w) * 128 + j) * 4 + (q)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define LA_STAMP(q)
+#endif
+// A workgroup barrier that orders LDS only: the waves' outstanding global stores (final L / L^-1
+// entries, read by no wave of the launch before a full barrier) are not waited for, as
+// __syncthreads' release fence would (s_waitcnt vmcnt(0) on every column's or panel's critical
+// path)
+__device__ __forceinline__ void lds_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 // ------------------------------------------------------------------------------------------
 // chol_lookahead: the multi-word potrf (A = L L^T in place, INV = false) of chol_packed with a
 // one-column look-ahead, so the serial pivot chain no longer waits for the trailing update.
@@ -402,11 +422,12 @@ __device__ __forceinline__ T readlane0(const T& v) {
   for (int q = 0; q < (int)(sizeof(T) / 8); ++q) d[q] = readlane_d(s[q], 0);
   return o;
 }
-template <class T, bool INV, bool LDL, int NMAX, int NW = 15>  // NW bulk waves
-__global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>* __restrict__ in,
-                                                       const MatDesc<T>* __restrict__ out_inv,
-                                                       const MatDesc<T>* __restrict__ out_l,
-                                                       int* __restrict__ info, int opts = 0) {
+// The body on one matrix d (in place when ol.A == d.A), callable from other kernels of
+// 64 (NW + 1) threads (potrf_blk_update, round 6); returns the failure column + 1 or 0 to
+// every thread.
+template <class T, bool INV, bool LDL, int NMAX, int NW>
+__device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const MatDesc<T>& oi,
+                                                   const MatDesc<T>& ol, int opts) {
   // opts (A/B switches): bit 0 = the chain wave at raised issue priority (its SIMD also runs
   // three bulk waves); bit 1 = one Newton step for the pivot's reciprocal (from the
   // double-double one: ~2^-208 relative instead of ~2^-212)
@@ -424,9 +445,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>
   __shared__ T nextr[INV ? 2 : 1][INV ? NMAX : 1];  // row j+1 of L^-1 as the bulk leaves it
   __shared__ T dgl[LDL ? NMAX : 1];
   __shared__ int fail;
-  const MatDesc<T> d = in[blockIdx.x];
-  const MatDesc<T> ol = out_l ? out_l[blockIdx.x] : MatDesc<T>{nullptr, 0, 0};
-  const MatDesc<T> oi = INV ? out_inv[blockIdx.x] : MatDesc<T>{nullptr, 0, 0};
   const int n = d.n, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const bool chain = w == 0;
   const int wb = w - 1;
@@ -560,8 +578,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>
         if (xR[k] == 0 && xr[k] == 1) nextr[1][xc[k]] = x[k];
     }
   }
-  __syncthreads();
+  lds_barrier();  // (the chain's L / L^-1 stores are read back only after the loop's full barrier)
   for (int j = 0; j + 1 < n; ++j) {
+    LA_STAMP(0);
     if (fail) break;
     const int p = j & 1, p1 = (j + 1) & 1;
     if (chain) {
@@ -577,8 +596,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>
       if constexpr (INV) {
         if (lane <= c) xv = lane <= j ? nextr[p1][lane] - colb[p][c] * rowb[p][lane] : T(1.0);
       }
+      LA_STAMP(1);
       const T rs = chain_column(c, p1);
+      LA_STAMP(2);
       chain_row(c, p1, xv, rs);
+      LA_STAMP(3);
     } else {
       // columns >= j+2 (and rows >= j+2 of L^-1) minus step j's term; then the owners of
       // column j+2 (and of row j+2) publish it
@@ -603,15 +625,16 @@ __global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>
             if (xR[k] == (c2 >> 3) && xr[k] == c2) nextr[p][xc[k]] = x[k];
         }
       }
+      LA_STAMP(3);
     }
-    __syncthreads();
+    lds_barrier();
   }
-  if (tid == 0 && info) info[blockIdx.x] = fail;
   __syncthreads();
+  const int failed = fail;
   if constexpr (LDL) {
     // L = U D^1/2 (column c times sqrt d_c, the diagonal sqrt d_c); L^-1 = D^-1/2 U^-1 (row r
     // times 1/sqrt d_r): the n square roots side by side
-    if (!fail) {
+    if (!failed) {
       for (int c = tid; c < n; c += NTH) {
         T sq, rq;
         pivot_sqrt(dgl[c], sq, rq);
@@ -620,7 +643,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>
       }
     }
     __syncthreads();
-    if (!fail)
+    if (!failed)
       for (int e = tid; e < n * n; e += NTH) {
         const int r = e % n, c = e / n;
         if (ol.A) {
@@ -639,6 +662,146 @@ __global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>
       if constexpr (INV) oi.A[r + (size_t)c * oi.lda] = T(0.0);
     }
   }
+  return failed;
+}
+template <class T, bool INV, bool LDL, int NMAX, int NW = 15>  // NW bulk waves
+__global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>* __restrict__ in,
+                                                       const MatDesc<T>* __restrict__ out_inv,
+                                                       const MatDesc<T>* __restrict__ out_l,
+                                                       int* __restrict__ info, int opts = 0) {
+  const MatDesc<T> d = in[blockIdx.x];
+  const MatDesc<T> ol = out_l ? out_l[blockIdx.x] : MatDesc<T>{nullptr, 0, 0};
+  const MatDesc<T> oi = INV ? out_inv[blockIdx.x] : MatDesc<T>{nullptr, 0, 0};
+  const int f = chol_lookahead_body<T, INV, LDL, NMAX, NW>(d, oi, ol, opts);
+  if (threadIdx.x == 0 && info) info[blockIdx.x] = f;
+}
+
+// ------------------------------------------------------------------------------------------
+// Blocked multi-word potrf across workgroups (round 6).  chol_lookahead keeps a whole block on
+// one CU: at C4 (16 Schur blocks of 127, double-double) 16 of 256 CUs run the ~n^3/6 trailing
+// update and a column costs ~1.8 us (the bulk's multi-word FMAs, not the pivot chain).  Here
+// the block is cut into NB-column panels k (k0 = NB k) and each panel costs three steps, the
+// last two spread over many workgroups:
+//   diag  (1 WG / matrix): L_kk and L_kk^-1 of the (updated) NB x NB diagonal block
+//         (chol_lookahead_body, 256 threads);
+//   trsm  (rows / 16 WGs): the panel below it, L_ik = A_ik L_kk^-T (a product with L_kk^-1 in
+//         LDS, no serial chain), and zeros in the block row above the diagonal;
+//   update(lower 16 x 16 tiles of the trailing matrix): A_ij -= L_ik L_jk^T; the workgroup 0 of
+//         each matrix updates the next diagonal block itself and goes straight on to its diag
+//         step, so one launch does both (update k + diag k+1).
+// Launches for n = 127, NB = 32: diag, trsm, {update, diag} x 3 with trsm between = 7.  The
+// factor is LL^T with every element's panel contributions summed panel by panel (a different
+// order from chol_lookahead's column by column: agreement to the multi-word rounding, not bitwise).
+// MPMP.jl:1433-1442 (the factorisation of S_j).
+// ------------------------------------------------------------------------------------------
+template <class T>
+struct BlkPotrfDesc {
+  T* A;      // the matrix (column-major, lower triangle in, L out, zeros above)
+  T* Linv;   // NB x NB scratch: L_kk^-1 of the current panel (ld NB)
+  int n, lda;
+};
+
+// the diagonal step of panel k (k0 = NB k) on matrix m: L_kk, L_kk^-1; failure -> info[m]
+template <class T, bool LDL, int NB>
+__device__ __forceinline__ void potrf_blk_diag(const BlkPotrfDesc<T>& b, int k0, int* info, int m,
+                                               int opts) {
+  const int nb = min(NB, b.n - k0);
+  const MatDesc<T> dk{b.A + k0 + (size_t)k0 * b.lda, nb, b.lda};
+  const MatDesc<T> oi{b.Linv, nb, NB};
+  const int f = chol_lookahead_body<T, true, LDL, NB, 3>(dk, oi, dk, opts);
+  if (threadIdx.x == 0 && info && f) info[m] = k0 + f;
+}
+
+template <class T, bool LDL, int NB>
+__global__ __launch_bounds__(256) void potrf_blk_first(const BlkPotrfDesc<T>* __restrict__ bd,
+                                                       int* __restrict__ info, int opts) {
+  const BlkPotrfDesc<T> b = bd[blockIdx.x];
+  if (threadIdx.x == 0 && info) info[blockIdx.x] = 0;
+  __syncthreads();
+  potrf_blk_diag<T, LDL, NB>(b, 0, info, blockIdx.x, opts);
+}
+
+// trsm of panel k: blockIdx.y = matrix, blockIdx.x = 16-row chunk of rows k0 + NB .. n-1
+// (chunk 0 also zeros the NB rows k0.. above the diagonal in the columns right of the panel)
+template <class T, int NB>
+__global__ __launch_bounds__(256) void potrf_blk_trsm(const BlkPotrfDesc<T>* __restrict__ bd, int k0) {
+  const BlkPotrfDesc<T> b = bd[blockIdx.y];
+  const int r0 = k0 + NB + 16 * blockIdx.x, tid = threadIdx.x;
+  if (blockIdx.x == 0)
+    for (int e = tid; e < NB * max(0, b.n - k0 - NB); e += 256) {
+      const int r = k0 + e % NB, c = k0 + NB + e / NB;
+      if (r < b.n) b.A[r + (size_t)c * b.lda] = T(0.0);
+    }
+  if (r0 >= b.n) return;
+  __shared__ T li[NB][NB + 1];  // L_kk^-1, [c][t]
+  __shared__ T ar[NB][17];      // the 16 rows of A_ik, [t][row]
+  for (int e = tid; e < NB * NB; e += 256) {
+    const int c = e % NB, t = e / NB;
+    li[c][t] = b.Linv[c + (size_t)t * NB];
+  }
+  for (int e = tid; e < NB * 16; e += 256) {
+    const int rr = e % 16, t = e / 16;
+    ar[t][rr] = r0 + rr < b.n ? b.A[r0 + rr + (size_t)(k0 + t) * b.lda] : T(0.0);
+  }
+  __syncthreads();
+  const int rr = tid % 16;
+  for (int c = tid / 16; c < NB; c += 16) {  // L_ik[r, c] = sum_{t <= c} A_ik[r, t] L_kk^-1[c, t]
+    T acc = T(0.0);
+    for (int t = 0; t <= c; ++t) acc = acc + ar[t][rr] * li[c][t];
+    if (r0 + rr < b.n && k0 + c < b.n) b.A[r0 + rr + (size_t)(k0 + c) * b.lda] = acc;
+  }
+}
+
+// update of panel k (A_ij -= L_ik L_jk^T over the lower 16 x 16 tiles of rows / columns
+// k1 = k0 + NB .. n-1) fused with the diagonal step of panel k+1: blockIdx.y = matrix,
+// blockIdx.x = 0 updates the diagonal block k+1 and factors it, blockIdx.x >= 1 the other tiles
+// (lower tiles (I, J), I >= J, of the trailing matrix, the ones inside the diagonal block skipped)
+template <class T, bool LDL, int NB>
+__global__ __launch_bounds__(256) void potrf_blk_update(const BlkPotrfDesc<T>* __restrict__ bd,
+                                                        int k0, int* __restrict__ info, int opts) {
+  const BlkPotrfDesc<T> b = bd[blockIdx.y];
+  const int k1 = k0 + NB, tid = threadIdx.x;
+  if (k1 >= b.n) return;
+  __shared__ T lr[NB][17], lc[NB][17];  // rows of L_ik, L_jk: [t][row]
+  const int ntr = (b.n - k1 + 15) / 16;  // 16-tiles of the trailing matrix
+  constexpr int DT = NB / 16;            // 16-tiles per diagonal block
+  auto upd_tile = [&](int I, int J) {    // tile (I, J) of the trailing matrix, I >= J
+    const int ri = k1 + 16 * I, cj = k1 + 16 * J;
+    for (int e = tid; e < NB * 16; e += 256) {
+      const int rr = e % 16, t = e / 16;
+      lr[t][rr] = ri + rr < b.n ? b.A[ri + rr + (size_t)(k0 + t) * b.lda] : T(0.0);
+      lc[t][rr] = cj + rr < b.n ? b.A[cj + rr + (size_t)(k0 + t) * b.lda] : T(0.0);
+    }
+    __syncthreads();
+    const int rr = tid % 16, cc = tid / 16, r = ri + rr, c = cj + cc;
+    if (r < b.n && c < b.n && r >= c) {
+      T acc = b.A[r + (size_t)c * b.lda];
+#pragma unroll 8
+      for (int t = 0; t < NB; ++t) acc = acc - lr[t][rr] * lc[t][cc];
+      b.A[r + (size_t)c * b.lda] = acc;
+    }
+    __syncthreads();
+  };
+  if (blockIdx.x == 0) {
+    for (int I = 0; I < DT && I < ntr; ++I)
+      for (int J = 0; J <= I; ++J) upd_tile(I, J);
+    potrf_blk_diag<T, LDL, NB>(b, k1, info, blockIdx.y, opts);
+    return;
+  }
+  // tile index q = blockIdx.x - 1 over the lower tiles outside the diagonal block, row by row
+  int q = blockIdx.x - 1, I = DT, J = 0;
+  int before = DT * (DT + 1) / 2;  // tiles of rows < DT (all inside the diagonal block)
+  // rows I >= DT hold I + 1 tiles each
+  int rem = q;
+  I = DT;
+  while (I < ntr && rem >= I + 1) {
+    rem -= I + 1;
+    ++I;
+  }
+  (void)before;
+  if (I >= ntr) return;
+  J = rem;
+  upd_tile(I, J);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3547,15 +3710,6 @@ __device__ unsigned long long g_chol2_trace[256 * 16 * 128];
 #else
 #define CT_TRACE()
 #endif
-// A workgroup barrier that orders LDS only: the waves' outstanding global stores (final L^-1
-// tiles, read by no wave of the launch) are not waited for, as __syncthreads' release fence
-// would (s_waitcnt vmcnt(0) on every panel's critical path)
-__device__ __forceinline__ void lds_barrier() {
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
 #ifndef CLRSDP_CHOL256_NTH
 #define CLRSDP_CHOL256_NTH 768
 #endif

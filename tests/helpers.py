@@ -187,13 +187,16 @@ def compare_summary(arr, rec, scale=0.0):
     import mpmath
     a = np.asarray(arr, dtype=object).ravel()
     assert len(a) == rec["n"], (len(a), rec["n"])
-    den = max(mpmath.mpf(rec["amax"]), mpmath.mpf(scale), mpmath.mpf(1e-300))
-    err = max([abs(mpmath.mpf(a[i]) - mpmath.mpf(v)) / den for i, v in zip(rec["idx"], rec["val"])]
-              + [mpmath.mpf(0)])
-    l1 = max(mpmath.mpf(rec["l1"]), mpmath.mpf(scale) * len(a), mpmath.mpf(1e-300))
-    for q, sv in enumerate(rec["sketch"]):
-        s = mpmath.fsum(int(w) * mpmath.mpf(v) for w, v in zip(sketch_weights(len(a), q), a))
-        err = max(err, abs(s - mpmath.mpf(sv)) / l1)
+    # the fixture strings are parsed and the differences taken at 320 bits whatever the global
+    # mpmath.mp.prec is (a test run that starts with this comparison has it at 53)
+    with mpmath.workprec(320):
+        den = max(mpmath.mpf(rec["amax"]), mpmath.mpf(scale), mpmath.mpf(1e-300))
+        err = max([abs(mpmath.mpf(a[i]) - mpmath.mpf(v)) / den
+                   for i, v in zip(rec["idx"], rec["val"])] + [mpmath.mpf(0)])
+        l1 = max(mpmath.mpf(rec["l1"]), mpmath.mpf(scale) * len(a), mpmath.mpf(1e-300))
+        for q, sv in enumerate(rec["sketch"]):
+            s = mpmath.fsum(int(w) * mpmath.mpf(v) for w, v in zip(sketch_weights(len(a), q), a))
+            err = max(err, abs(s - mpmath.mpf(sv)) / l1)
     return float(err)
 
 

@@ -105,6 +105,31 @@ def _indefinite_Y_state(oracle, cons, b, bi):
     return x, X, y, Y2
 
 
+@pytest.mark.parametrize("blk", ["1", "0"], ids=["blocked", "one-cu"])
+def test_cholesky_fails_dd_c2_shape(pk, oracle, blk, monkeypatch):
+    """Double-double S_j of 127 (the config-4 cluster shape) on the indefinite-Y state: both
+    Cholesky factorisations of S_j -- the blocked potrf across workgroups (potrf_blk_*, default
+    above n = 64) and the one-CU chol_lookahead (CLRSDP_POTRF_BLK=0) -- report the failure
+    (CLRSDP_E_NOT_PD_S), as the fp64 path does."""
+    from clrsdp_amd import _lib as L
+    monkeypatch.setenv("CLRSDP_POTRF_BLK", blk)
+    cons, b = pk.synth(seed=5, J=2, delta=64, rank=2, n_y=64)
+    bi = oracle.get_block_info(cons)
+    x, X, y, Y = _indefinite_Y_state(oracle, cons, b, bi)
+    P = pk.make_params("0.3", "0.1", "0.7", 0)
+    dev = pk.DeviceSolver(cons, b, pk.get_block_info(cons), precision_words=2)
+    try:
+        dev.set_factorization(0)
+        dev.set_state(x, X, y, Y)
+        for s in (L.STAGE_MU_R, L.STAGE_XINV, L.STAGE_SCHUR):
+            _run(dev, s, P, L)
+        with pytest.raises(L.ClrsdpError) as ei:
+            dev.run_stage(L.STAGE_FACTOR, P, False)
+        assert ei.value.code == L.E_NOT_PD_S
+    finally:
+        dev.close()
+
+
 @pytest.mark.parametrize("cfg", [dict(J=2, delta=6, rank=1, n_y=4), dict(J=2, delta=64, rank=2, n_y=64)],
                          ids=["small", "c2shape"])
 def test_cholesky_fails_lu_matches_oracle(pk, oracle, cfg):

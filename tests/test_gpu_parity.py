@@ -244,17 +244,20 @@ def test_stage_parity_sphere_packing_shape_qd(pk, oracle):
     _stage_compare(pk, oracle, consm, ar.asarray(b), iters_before=3, words=4, ar=ar, tol=1e-45)
 
 
-@pytest.mark.parametrize("upper", ["1", "0"])
+@pytest.mark.parametrize("variant", ["default", "full-pairs", "one-cu-potrf"])
 @pytest.mark.parametrize("bits", [128, 256])
-def test_stage_parity_dd_c4_shape(pk, bits, upper, monkeypatch):
+def test_stage_parity_dd_c4_shape(pk, bits, variant, monkeypatch):
     """Config 4 at its own cluster shape (J = 2, delta = 64, rank 2, n_y = 64, dim_S = 127,
     blocks of 64) at double-double against the 128- and 256-bit oracle: drives
     potrf_batched<dd> / trsm_batched<dd> (dim_S > 64), chol_inv_reg<dd> and eigmin_lds<dd> at
     n = 64 (MPMP.jl:1433-1465, 762-801, 1829-1898).  dd carries ~106 bits; 1e-25 relative
     (scale-aware) leaves ~6 orders for the conditioning of S_j at this state.  Both forms of the
     Schur pairings: only the upper tiles of V^T X^-1 V, V^T Y V with schur_assemble reading
-    (min, max) (the m = 1 default, round 6) and the full products (CLRSDP_MW_PAIR_UPPER=0)."""
-    monkeypatch.setenv("CLRSDP_MW_PAIR_UPPER", upper)
+    (min, max) (the m = 1 default, round 6) and the full products (CLRSDP_MW_PAIR_UPPER=0); both
+    factorisations of S_j: the blocked potrf across workgroups (potrf_blk_*, the default above
+    n = 64, round 6) and the one-CU chol_lookahead (CLRSDP_POTRF_BLK=0)."""
+    monkeypatch.setenv("CLRSDP_MW_PAIR_UPPER", "0" if variant == "full-pairs" else "1")
+    monkeypatch.setenv("CLRSDP_POTRF_BLK", "0" if variant == "one-cu-potrf" else "1")
     _stage_compare_fixture(pk, "c4dd", 2, 1e-25, bits)
 
 
