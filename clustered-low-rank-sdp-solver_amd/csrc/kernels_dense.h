@@ -374,14 +374,26 @@ __global__ __launch_bounds__(NT) void chol_packed(const MatDesc<T>* __restrict__
 }
 
 // chol_lookahead's per-column timestamps (tools/micro/potrf_blk_bench.hip; compiled out in the
-// library): [block][wave 0 / 1][column][point]
+// library): [block][wave][column][point]
 #ifdef CLRSDP_LA_TRACE
-__device__ unsigned long long g_la_trace[64 * 2 * 128 * 4];
-#define LA_STAMP(q) do { if (lane == 0 && w < 2 && j < 128 && blockIdx.x < 64 && blockIdx.y == 0) \
-  g_la_trace[((blockIdx.x * 2 + w) * 128 + j) * 4 + (q)] = __builtin_amdgcn_s_memtime(); } while (0)
+__device__ unsigned long long g_la_trace[64 * 16 * 128 * 4];
+#define LA_STAMP(q) do { if (lane == 0 && w < 16 && j < 128 && blockIdx.x < 64 && blockIdx.y == 0) \
+  g_la_trace[((blockIdx.x * 16 + w) * 128 + j) * 4 + (q)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define LA_STAMP(q)
 #endif
+// a - b c in the factorisations' trailing updates: mw::fms_fast at double-double (its bound and
+// the reason it suffices there are in mwfloat.h), the plain expression otherwise.
+// CLRSDP_FMS_EXACT (compile time) keeps the accurate form everywhere.
+template <class T>
+__device__ __forceinline__ T fms_upd(const T& a, const T& b, const T& c) { return a - b * c; }
+#ifndef CLRSDP_FMS_EXACT
+template <>
+__device__ __forceinline__ mw::dd fms_upd<mw::dd>(const mw::dd& a, const mw::dd& b, const mw::dd& c) {
+  return mw::fms_fast(a, b, c);
+}
+#endif
+
 // A workgroup barrier that orders LDS only: the waves' outstanding global stores (final L / L^-1
 // entries, read by no wave of the launch before a full barrier) are not waited for, as
 // __syncthreads' release fence would (s_waitcnt vmcnt(0) on every column's or panel's critical
@@ -590,11 +602,11 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
 #pragma unroll
       for (int u = 0; u < RC; ++u) {
         const int r = c + lane + 64 * u;
-        cv[u] = r < n ? nextc[p1][r] - colb[p][r] * cuj : T(0.0);
+        cv[u] = r < n ? fms_upd(nextc[p1][r], colb[p][r], cuj) : T(0.0);
       }
       T xv = T(0.0);
       if constexpr (INV) {
-        if (lane <= c) xv = lane <= j ? nextr[p1][lane] - colb[p][c] * rowb[p][lane] : T(1.0);
+        if (lane <= c) xv = lane <= j ? fms_upd(nextr[p1][lane], colb[p][c], rowb[p][lane]) : T(1.0);
       }
       LA_STAMP(1);
       const T rs = chain_column(c, p1);
@@ -607,12 +619,12 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
 #pragma unroll
       for (int k = 0; k < KA; ++k)
         if (ahi[k] >= j + 2 && ac[k] >= j + 2)
-          a[k] = a[k] - colb[p][ar[k]] * (LDL ? colub[p] : colb[p])[ac[k]];
+          a[k] = fms_upd(a[k], colb[p][ar[k]], (LDL ? colub[p] : colb[p])[ac[k]]);
       if constexpr (INV) {
 #pragma unroll
         for (int k = 0; k < KX; ++k)
           if (xR[k] >= 0 && 8 * xC[k] <= j && j + 2 <= 8 * xR[k] + 7 && xr[k] >= j + 2 && xc[k] <= j)
-            x[k] = x[k] - colb[p][xr[k]] * rowb[p][xc[k]];
+            x[k] = fms_upd(x[k], colb[p][xr[k]], rowb[p][xc[k]]);
       }
       const int c2 = j + 2;
       if (c2 < n) {
@@ -747,7 +759,7 @@ __global__ __launch_bounds__(256) void potrf_blk_trsm(const BlkPotrfDesc<T>* __r
   const int rr = tid % 16;
   for (int c = tid / 16; c < NB; c += 16) {  // L_ik[r, c] = sum_{t <= c} A_ik[r, t] L_kk^-1[c, t]
     T acc = T(0.0);
-    for (int t = 0; t <= c; ++t) acc = acc + ar[t][rr] * li[c][t];
+    for (int t = 0; t <= c; ++t) acc = fms_upd(acc, -ar[t][rr], li[c][t]);
     if (r0 + rr < b.n && k0 + c < b.n) b.A[r0 + rr + (size_t)(k0 + c) * b.lda] = acc;
   }
 }
@@ -777,7 +789,7 @@ __global__ __launch_bounds__(256) void potrf_blk_update(const BlkPotrfDesc<T>* _
     if (r < b.n && c < b.n && r >= c) {
       T acc = b.A[r + (size_t)c * b.lda];
 #pragma unroll 8
-      for (int t = 0; t < NB; ++t) acc = acc - lr[t][rr] * lc[t][cc];
+      for (int t = 0; t < NB; ++t) acc = fms_upd(acc, lr[t][rr], lc[t][cc]);
       b.A[r + (size_t)c * b.lda] = acc;
     }
     __syncthreads();

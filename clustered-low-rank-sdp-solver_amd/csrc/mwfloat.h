@@ -82,6 +82,26 @@ MW_HD dd operator*(const dd& a, double b) {
   p1 = quick_two_sum(p1, p2, p2);
   return dd(p1, p2);
 }
+// a - b c for the trailing updates of the factorisations (round 6): the product's words are not
+// renormalised and the subtraction is the QD library's "sloppy" double-double addition (one
+// two-sum of the leading words, the low words added plainly): 15 operations against 27 for
+// a - (b * c) with the accurate addition.  Its error is below ~2 u^2 (|a| + |b c|) (u = 2^-53)
+// -- an absolute bound, not one relative to the result -- which is the componentwise bound the
+// backward-error analysis of Cholesky asks of every update, so the factor stays backward stable
+// at double-double precision while the bulk update (VALU-issue bound) runs ~1.8x fewer
+// instructions.
+MW_HD dd fms_fast(const dd& a, const dd& b, const dd& c) {
+  MW_EXACT
+  double p2;
+  const double p1 = two_prod(b.hi, c.hi, p2);
+  p2 = fma(b.hi, c.lo, p2);
+  p2 = fma(b.lo, c.hi, p2);
+  double e;
+  double s = two_sum(a.hi, -p1, e);
+  e += a.lo - p2;
+  s = quick_two_sum(s, e, e);
+  return dd(s, e);
+}
 MW_HD dd operator/(const dd& a, const dd& b) {
   MW_EXACT
   // long division: q1 = a/b, r = a - q1 b, q2 = r/b, r -= q2 b, q3 = r/b
