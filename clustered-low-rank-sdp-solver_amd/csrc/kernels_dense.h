@@ -416,12 +416,12 @@ __device__ __forceinline__ void lds_barrier() {
 //          liveness-packed slots, 15 waves), then the owners of column j+2 publish it.
 // The chain's step (one multi-word FMA per lane, the pivot, one product per lane) and the bulk's
 // update run side by side: a phase costs max(chain, bulk) + one barrier, where chol_packed's
-// step costs chain + bulk + two barriers.  Every element sees the same operations in the same
-// order as in chol_packed (column j's term at step j), so the factors are bitwise chol_packed's
-// -- except at quad-double with opts bit 1 (the default): the LDL pivot reciprocal then takes one
-// Newton step from the double-double one (~2^-208 relative instead of chol_packed's ~2^-212), so
-// those factors agree with chol_packed's to that level, not bitwise
-// (tests/test_gpu_lu.py::test_chol_lookahead_qd_one_newton_step).
+// step costs chain + bulk + two barriers.  Every element sees its terms in the same order as in
+// chol_packed (column j's term at step j); the factors agree with chol_packed's to the multi-word
+// rounding, not bitwise: at double-double every update is fms_upd's one-two-sum form (round 6),
+// and at quad-double with opts bit 1 (the default) the LDL pivot reciprocal takes one Newton
+// step from the double-double one (~2^-208 relative instead of chol_packed's ~2^-212)
+// (tests/test_gpu_parity.py::test_chol_lookahead_qd_one_newton_step).
 // LDL (quad-double): A = U D U^T, then L = U D^1/2 with all n square roots side by side.
 // MPMP.jl:1433-1442 / 1499-1505 (the factorisations of S_j and Q; the reference's approx_lu!).
 // ------------------------------------------------------------------------------------------
@@ -437,7 +437,7 @@ __device__ __forceinline__ T readlane0(const T& v) {
 // The body on one matrix d (in place when ol.A == d.A), callable from other kernels of
 // 64 (NW + 1) threads (potrf_blk_update, round 6); returns the failure column + 1 or 0 to
 // every thread.
-template <class T, bool INV, bool LDL, int NMAX, int NW>
+template <class T, bool INV, bool LDL, int NMAX, int NW, bool SKIP0 = false>
 __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const MatDesc<T>& oi,
                                                    const MatDesc<T>& ol, int opts) {
   // opts (A/B switches): bit 0 = the chain wave at raised issue priority (its SIMD also runs
@@ -445,9 +445,13 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
   // double-double one: ~2^-208 relative instead of ~2^-212)
   constexpr int NTH = 64 * (NW + 1);
   constexpr int SA = (NMAX * (NMAX + 1) / 2 + 63) / 64;  // 64-element slots of the triangle
-  constexpr int KA = (SA + NW - 1) / NW;
+  // SKIP0: the bulk waves on the chain's SIMD (w % 4 == 0) stay idle, the others take their
+  // slots -- the chain then issues alone on its SIMD (quad-double: its pivot is thousands of
+  // cycles of dependent work, and the three bulk waves beside it finished last)
+  constexpr int NWB = SKIP0 ? NW - NW / 4 : NW;  // bulk waves with slots
+  constexpr int KA = (SA + NWB - 1) / NWB;
   constexpr int SX = (NMAX / 8) * (NMAX / 8 + 1) / 2;    // 8 x 8 tiles of L^-1
-  constexpr int KX = INV ? (SX + NW - 1) / NW : 1;
+  constexpr int KX = INV ? (SX + NWB - 1) / NWB : 1;
   constexpr int RC = (NMAX + 63) / 64;                   // chain rows per lane
   static_assert(!INV || NMAX <= 64, "the chain holds one row of L^-1 per lane");
   __shared__ T colb[2][NMAX];    // scaled column j (LDL: of U), by parity
@@ -459,7 +463,8 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
   __shared__ int fail;
   const int n = d.n, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const bool chain = w == 0;
-  const int wb = w - 1;
+  const bool idle = chain || (SKIP0 && (w & 3) == 0);
+  const int wb = SKIP0 ? w - 1 - (w >> 2) : w - 1;  // rank among the bulk waves with slots
   auto wave_max = [](int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
@@ -471,9 +476,9 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
   const int ne = n * (n + 1) / 2;
 #pragma unroll
   for (int k = 0; k < KA; ++k) {
-    const int e = 64 * (wb + NW * k) + lane;
+    const int e = 64 * (wb + NWB * k) + lane;
     int r = -1, c = -1;
-    if (!chain && e < ne) {
+    if (!idle && e < ne) {
       int rem = e;
       c = 0;
       while (rem >= n - c) {
@@ -486,8 +491,8 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
     ac[k] = c;
     a[k] = T(0.0);
     if (c >= 0) a[k] = d.A[r + (size_t)c * d.lda];
-    ahi[k] = chain ? -1 : wave_max(c);
-    alo[k] = chain ? NMAX : -wave_max(c >= 0 ? -c : -NMAX);
+    ahi[k] = idle ? -1 : wave_max(c);
+    alo[k] = idle ? NMAX : -wave_max(c >= 0 ? -c : -NMAX);
   }
   // ---- bulk tiles of L^-1 (chol_packed's 8 x 8 tiles, R >= C), identity to start
   T x[KX];
@@ -496,8 +501,8 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
     const int nt8 = (n + 7) / 8;
 #pragma unroll
     for (int k = 0; k < KX; ++k) {
-      int t = wb + NW * k, C = 0;
-      bool tv = !chain;
+      int t = wb + NWB * k, C = 0;
+      bool tv = !idle;
       if (tv) {
         while (C < nt8 && t >= nt8 - C) {
           t -= nt8 - C;
@@ -676,7 +681,7 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
   }
   return failed;
 }
-template <class T, bool INV, bool LDL, int NMAX, int NW = 15>  // NW bulk waves
+template <class T, bool INV, bool LDL, int NMAX, int NW = 15, bool SKIP0 = false>  // NW bulk waves
 __global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>* __restrict__ in,
                                                        const MatDesc<T>* __restrict__ out_inv,
                                                        const MatDesc<T>* __restrict__ out_l,
@@ -684,7 +689,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void chol_lookahead(const MatDesc<T>
   const MatDesc<T> d = in[blockIdx.x];
   const MatDesc<T> ol = out_l ? out_l[blockIdx.x] : MatDesc<T>{nullptr, 0, 0};
   const MatDesc<T> oi = INV ? out_inv[blockIdx.x] : MatDesc<T>{nullptr, 0, 0};
-  const int f = chol_lookahead_body<T, INV, LDL, NMAX, NW>(d, oi, ol, opts);
+  const int f = chol_lookahead_body<T, INV, LDL, NMAX, NW, SKIP0>(d, oi, ol, opts);
   if (threadIdx.x == 0 && info) info[blockIdx.x] = f;
 }
 

@@ -131,7 +131,7 @@ void run(const char* name, int n, int nmat) {
 }
 
 #ifdef CLRSDP_LA_TRACE
-template <class T, bool INV, bool LDL, int NMAX, int NW>
+template <class T, bool INV, bool LDL, int NMAX, int NW, bool SKIP0 = false>
 void trace_run(const char* name, int n, int nmat) {
   const size_t nn = (size_t)n * n;
   std::vector<T> h(nn * nmat);
@@ -167,16 +167,17 @@ void trace_run(const char* name, int n, int nmat) {
   int* info;
   CK(hipMalloc(&info, nmat * sizeof(int)));
   const float t = timeit([] {}, [&] {
-    chol_lookahead<T, INV, LDL, NMAX, NW><<<nmat, 64 * (NW + 1)>>>(ddin, INV ? ddinv : nullptr, ddout, info, 2);
+    chol_lookahead<T, INV, LDL, NMAX, NW, SKIP0><<<nmat, 64 * (NW + 1)>>>(ddin, INV ? ddinv : nullptr, ddout, info, 2);
   });
-  std::vector<unsigned long long> tr(64 * 2 * 128 * 4);
+  std::vector<unsigned long long> tr(64 * 16 * 128 * 4);
   CK(hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(g_la_trace), tr.size() * 8));
-  double acc[2][4] = {{0}};
+  double acc[2][4] = {{0}}, wk[16] = {0};
   int cnt = 0;
   const int nb = nmat < 64 ? nmat : 64;
   for (int b = 0; b < nb; ++b)
     for (int j = 0; j + 2 < n && j < 127; ++j) {
-      auto T0 = [&](int w, int jj, int q) { return (double)tr[((b * 2 + w) * 128 + jj) * 4 + q]; };
+      auto T0 = [&](int w, int jj, int q) { return (double)tr[((b * 16 + w) * 128 + jj) * 4 + q]; };
+      for (int w = 1; w <= NW; ++w) wk[w] += T0(w, j, 3) - T0(w, j, 0);
       acc[0][0] += T0(0, j, 1) - T0(0, j, 0);      // LDS reads + update of column j+1
       acc[0][1] += T0(0, j, 2) - T0(0, j, 1);      // pivot + scaled column out
       acc[0][2] += T0(0, j, 3) - T0(0, j, 2);      // row of L^-1
@@ -186,11 +187,19 @@ void trace_run(const char* name, int n, int nmat) {
       acc[1][2] += T0(0, j + 1, 0) - T0(0, j, 0);  // whole column
       ++cnt;
     }
-  printf("%s %s n=%d batch=%d NMAX=%d NW=%d: %.1f us | chain: update %.0f pivot %.0f row %.0f wait %.0f | bulk work %.0f wait %.0f | column %.0f cycles\n",
-         name, INV ? "INV" : "potrf", n, nmat, NMAX, NW, t, acc[0][0] / cnt, acc[0][1] / cnt, acc[0][2] / cnt,
+  printf("%s %s%s n=%d batch=%d NMAX=%d NW=%d: %.1f us | chain: update %.0f pivot %.0f row %.0f wait %.0f | bulk work %.0f wait %.0f | column %.0f cycles\n",
+         name, INV ? "INV" : "potrf", SKIP0 ? " skip0" : "", n, nmat, NMAX, NW, t, acc[0][0] / cnt, acc[0][1] / cnt, acc[0][2] / cnt,
          acc[0][3] / cnt, acc[1][0] / cnt, acc[1][1] / cnt, acc[1][2] / cnt);
+  printf("   bulk work per wave:");
+  for (int w = 1; w <= NW; ++w) printf(" %.0f", wk[w] / cnt);
+  printf("\n");
 }
 int main(int argc, char** argv) {
+  trace_run<qd, false, true, 64, 15, true>("qd", 51, 7);
+  trace_run<qd, true, true, 64, 15>("qd", 32, 32);
+  trace_run<qd, true, true, 64, 15, true>("qd", 32, 32);
+  trace_run<dd, true, false, 64, 15, true>("dd", 64, 16);
+  trace_run<dd, false, false, 64, 15, true>("dd", 64, 16);
   trace_run<dd, false, false, 128, 15>("dd", 127, 16);
   trace_run<dd, false, false, 64, 15>("dd", 64, 16);
   trace_run<dd, true, false, 64, 15>("dd", 64, 16);
