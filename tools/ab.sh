@@ -3,7 +3,7 @@
 # setting, R rounds, printing iterations/s per run (bench args after the setting).
 #   bash tools/ab.sh "CLRSDP_NO_GRAPH=1" 3 --steps 600
 set -uo pipefail
-ENVB=$1; R=$2; shift 2
+ENVB=${1//,/ }; R=$2; shift 2  # (several settings: comma-separated)
 export TMPDIR=/tmp
 for r in $(seq 1 $R); do
   for v in A B; do
