@@ -29,18 +29,51 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+# the compiler's per-kernel resource remarks of the last build (VGPRs, scratch, occupancy), kept
+# beside the library for tests/test_build_resources.py (a kernel that starts spilling to scratch
+# is a silent slowdown: round 6 found schur_fused_f64 at 92 B/lane after an epilogue change)
+RESOURCES = os.path.join(HERE, "libclrsdp.resources.txt")
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and os.path.exists(OUT):
         t = os.path.getmtime(OUT)
         if all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d)):
             return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc] + HIPCC_FLAGS + ["-o", OUT + ".tmp", SRC]
+    cmd = [hipcc] + HIPCC_FLAGS + ["-Rpass-analysis=kernel-resource-usage", "-o", OUT + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+    with open(RESOURCES + ".tmp", "w") as f:
+        f.write(r.stderr)
+    if r.returncode != 0:
+        print("\n".join(ln for ln in r.stderr.splitlines() if "remark:" not in ln), file=sys.stderr)
+        raise subprocess.CalledProcessError(r.returncode, cmd)
+    os.replace(RESOURCES + ".tmp", RESOURCES)
     os.replace(OUT + ".tmp", OUT)
     return OUT
+
+
+def kernel_resources(path: str = RESOURCES) -> dict:
+    """{mangled kernel name: {"VGPRs": .., "ScratchSize": .., ...}} from the build's remarks."""
+    out, cur = {}, None
+    with open(path) as f:
+        for ln in f:
+            if "remark:" not in ln:
+                continue
+            body = ln.split("remark:", 1)[1].split("[-Rpass")[0].strip()
+            if body.startswith("Function Name:"):
+                cur = body.split(":", 1)[1].strip()
+                out[cur] = {}
+            elif cur is not None and ":" in body:
+                k, v = body.split(":", 1)
+                k = k.split("[")[0].strip()
+                try:
+                    out[cur][k] = int(v.strip())
+                except ValueError:
+                    pass
+    return out
 
 
 if __name__ == "__main__":

@@ -755,9 +755,15 @@ struct MatPlan : PlanBase {  // potrf / eigmin
       // idle (SKIP0, round 6: qd n = 51 138 -> 126 us, dd n = 64 63 -> 61 us)
       static const bool la = !env_off("CLRSDP_CHOL_LA");
       if (reg_potrf && la && nmax <= (std::is_same<T, mw::dd>::value ? 128 : 64)) {
-        if (std::is_same<T, mw::dd>::value && nmax > 64)
-          chol_lookahead<T, false, false, 128><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info, la_opts());
-        else if (std::is_same<T, mw::qd>::value && chol_ldl_on())
+        bool done = false;
+        if constexpr (std::is_same<T, mw::dd>::value) {  // (no quad-double instance: it would spill)
+          if (nmax > 64) {
+            chol_lookahead<T, false, false, 128><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info, la_opts());
+            done = true;
+          }
+        }
+        if (done) {
+        } else if (std::is_same<T, mw::qd>::value && chol_ldl_on())
           chol_lookahead<T, false, true, 64, 15, true><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info, la_opts());
         else
           chol_lookahead<T, false, false, 64, 15, true><<<(unsigned)h.size(), 1024, 0, s>>>(d, nullptr, d, info, la_opts());
@@ -1154,6 +1160,7 @@ struct Solver final : HandleBase {
   // schur_fused_f64 (every local block delta <= 128): V^T X^-1 formed on chip, one workgroup
   // per 64-row block; CLRSDP_SCHUR_FUSED=0 keeps the V^T X^-1 GEMM + schur_pairs_f64 pair
   bool schur_fused = false;
+  bool fused_grp2 = false;  // schur_fused_f64<.., .., true>: the rank-2 group-sum epilogue (every block grp = 2)
   bool fused_y = false;  // schur_fused_f64<0, true>: V^T Y on chip too (no p_ty); CLRSDP_SCHUR_FUSED_Y=0
   FusedPairDesc* d_fpd = nullptr;
   TileRef* d_fpt2d = nullptr;
@@ -1959,7 +1966,10 @@ struct Solver final : HandleBase {
         d_fpt2d = descs.own(ft2d);
         const char* efy = std::getenv("CLRSDP_SCHUR_FUSED_Y");
         fused_y = !(efy && efy[0] == '0');
-        for (const void* k : {(const void*)schur_fused_f64<0>, (const void*)schur_fused_f64<0, true>})
+        fused_grp2 = any_grp2;
+        for (const void* k : {(const void*)schur_fused_f64<0>, (const void*)schur_fused_f64<0, true>,
+                              (const void*)schur_fused_f64<0, false, true>,
+                              (const void*)schur_fused_f64<0, true, true>})
           HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)schur_fused::LDS));
       }
@@ -2410,8 +2420,12 @@ struct Solver final : HandleBase {
         static const bool force_full = env_on("CLRSDP_SCHUR_FULL");
         const bool full = force_full || !fac2 || n_gsum > 0 || lu_sq();
         s_lower = schur_fused && !full;
-        if (schur_fused && fused_y)
+        if (schur_fused && fused_y && fused_grp2)
+          schur_fused_f64<0, true, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
+        else if (schur_fused && fused_y)
           schur_fused_f64<0, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
+        else if (schur_fused && fused_grp2)
+          schur_fused_f64<0, false, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
         else if (schur_fused)
           schur_fused_f64<0><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
         else if (n_ptiles)

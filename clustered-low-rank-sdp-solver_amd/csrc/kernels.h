@@ -2220,7 +2220,10 @@ __device__ __forceinline__ int st_idx(int row, int col) { return row * 64 + (col
 // YV: phase 1 also forms TYt_a^T = Y V_a (sharing the V_a slab; one single-buffered image of
 // the three slabs), whose accumulators are written straight into the fragment-ordered TYt_a
 // region -- no V^T Y GEMM and no K x delta round trip through HBM for it either.
-template <int DBG = 0, bool YV = false>
+// GRP2 (every descriptor grp = 2): the rank-2 group-sum epilogue.  A template parameter, not a
+// branch on d.grp: the branch made the rank-1 (C3) instance spill 92 B/lane at 256 VGPRs
+// (63.7 against 57.3 us per launch, round 6).
+template <int DBG = 0, bool YV = false, bool GRP2 = false>
 __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __restrict__ descs,
                                                        const TileRef* __restrict__ t2d,
                                                        unsigned long long* stamp = nullptr,
@@ -2432,7 +2435,7 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     // (p, q) and its mirror (q, p) from the staging tile as 64-row column segments (lower
     // triangle only unless full: the tile whose row block is the larger one, and p >= q of a
     // diagonal tile)
-    if (d.grp == 2) {
+    if constexpr (GRP2) {
       // rank 2: the 32 x 32 tile of S at (a0 / 2, b0 / 2), each entry the sum of its 2 x 2 group
       // of the staged tile; the same triangle rules as below, in S's coordinates
       const int D = K >> 1, sa0 = a0 >> 1, sb0 = b0 >> 1;
