@@ -1628,6 +1628,7 @@ struct Solver final : HandleBase {
     d_blk = descs.own(bd);
     if (n_blk_m) d_blk_m = descs.own(bdm);
     d_ayd = descs.own(ayd);
+    build_ozaki();
     n_pair = (int)pd.size();
     // tuples <-> columns 1:1 in every local cluster (m = L = 1, every rank 1): fused trace_A
     trivial_tuples = n_pair > 0;
@@ -1869,6 +1870,84 @@ struct Solver final : HandleBase {
       t->finalize();
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q}) f->reg_potrf = true;
     for (MatPlan<T>* f : {&f_X, &f_Y, &f_S, &f_Q, &e_X, &e_Y}) f->finalize();
+  }
+
+  // ---- double-double Schur products on the int8 matrix cores (Ozaki scheme, oz_split / oz_gemm in
+  // kernels_dense.h; round 6): every block m = 1.  Four launches replace the four gemm_valu_ks
+  // launches of p_s1x, p_s1y, p_s2x, p_s2y: the digits of the rows of X^-1_b and Y_b and of the
+  // columns of V_b; TX_b = X^-1_b V_b and TY_b = Y_b V_b; the digits of the columns of TX_b, TY_b;
+  // BX_b = V_b^T TX_b and BY_b = V_b^T TY_b on their upper 16-tiles (the rows of V_b^T are the
+  // columns of V_b, so their digits serve twice).  CLRSDP_OZAKI=0 keeps the VALU products.
+  bool use_oz = false;
+  OzSplitDesc* d_ozs1 = nullptr;
+  OzSplitDesc* d_ozs2 = nullptr;
+  OzGemmDesc* d_ozg1 = nullptr;
+  OzGemmDesc* d_ozg2 = nullptr;
+  TileRef *d_ozs1t = nullptr, *d_ozs2t = nullptr, *d_ozg1t = nullptr, *d_ozg2t = nullptr;
+  int n_ozs1 = 0, n_ozs2 = 0, n_ozg1 = 0, n_ozg2 = 0;
+  void build_ozaki() {
+    use_oz = false;
+    if constexpr (std::is_same<T, mw::dd>::value) {
+      if (anyMgt1 || lb.empty() || env_off("CLRSDP_OZAKI")) return;
+      std::vector<OzSplitDesc> s1, s2;
+      std::vector<OzGemmDesc> g1, g2;
+      std::vector<TileRef> s1t, s2t, g1t, g2t;
+      auto pad = [](int v, int q) { return (v + q - 1) / q * q; };
+      auto digits = [&](int nv, int K) {
+        signed char* D = dmalloc<signed char>((size_t)OZ_S * pad(nv, 16) * pad(K, 64));
+        descs.owned_dev.push_back(D);
+        return D;
+      };
+      auto expo = [&](int nv) {
+        int* E = dmalloc<int>((size_t)pad(nv, 16));
+        descs.owned_dev.push_back(E);
+        return E;
+      };
+      auto add_split = [&](std::vector<OzSplitDesc>& v, std::vector<TileRef>& t, const T* X, long long sv,
+                           long long sk, int nv, int K, signed char* D, int* E) {
+        v.push_back(OzSplitDesc{X, sv, sk, D, E, nv, K, pad(nv, 16), pad(K, 64)});
+        for (int g = 0; g < cdiv(nv, 4); ++g) t.push_back(TileRef{(int)v.size() - 1, g});
+      };
+      auto add_gemm = [&](std::vector<OzGemmDesc>& v, std::vector<TileRef>& t, const signed char* DA,
+                          const int* EA, int RA, const signed char* DB, const int* EB, int RB, int Kp,
+                          T* C, int ldc, int M, int N, bool upper) {
+        const int tn = cdiv(N, 16);
+        v.push_back(OzGemmDesc{DA, EA, DB, EB, C, RA, RB, Kp, ldc, M, N, tn, 0});
+        for (int q = 0; q < cdiv(M, 16) * tn; ++q)
+          if (!upper || q / tn <= q % tn) t.push_back(TileRef{(int)v.size() - 1, q});
+      };
+      for (const LBlk& b : lb) {
+        const int n = b.n, del = b.del, K = b.K;
+        if (K <= 0 || del <= 0) continue;
+        signed char *Dx = digits(n, del), *Dy = digits(n, del), *Gv = digits(K, del);
+        signed char *Gtx = digits(K, del), *Gty = digits(K, del);
+        int *Ex = expo(n), *Ey = expo(n), *Fv = expo(K), *Ftx = expo(K), *Fty = expo(K);
+        // rows of X^-1_b, Y_b (n x n, ld n: row v, element k at v + k n); columns of V_b (del x K)
+        add_split(s1, s1t, Xinv + b.off, 1, n, n, del, Dx, Ex);
+        add_split(s1, s1t, Y + b.off, 1, n, n, del, Dy, Ey);
+        add_split(s1, s1t, V + b.voff, del, 1, K, del, Gv, Fv);
+        // columns of TX_b, TY_b (del x K, ld n)
+        add_split(s2, s2t, TX + b.toff, n, 1, K, del, Gtx, Ftx);
+        add_split(s2, s2t, TY + b.toff, n, 1, K, del, Gty, Fty);
+        const int Kp = pad(del, 64);
+        add_gemm(g1, g1t, Dx, Ex, pad(n, 16), Gv, Fv, pad(K, 16), Kp, TX + b.toff, n, n, K, false);
+        add_gemm(g1, g1t, Dy, Ey, pad(n, 16), Gv, Fv, pad(K, 16), Kp, TY + b.toff, n, n, K, false);
+        add_gemm(g2, g2t, Gv, Fv, pad(K, 16), Gtx, Ftx, pad(K, 16), Kp, BX + b.boff, K, K, K, mw_pair_upper);
+        add_gemm(g2, g2t, Gv, Fv, pad(K, 16), Gty, Fty, pad(K, 16), Kp, BY + b.boff, K, K, K, mw_pair_upper);
+      }
+      if (g1.empty()) return;
+      d_ozs1 = descs.own(s1); d_ozs2 = descs.own(s2); d_ozg1 = descs.own(g1); d_ozg2 = descs.own(g2);
+      d_ozs1t = descs.own(s1t); d_ozs2t = descs.own(s2t); d_ozg1t = descs.own(g1t); d_ozg2t = descs.own(g2t);
+      n_ozs1 = (int)s1t.size(); n_ozs2 = (int)s2t.size(); n_ozg1 = (int)g1t.size(); n_ozg2 = (int)g2t.size();
+      use_oz = true;
+    }
+  }
+  void launch_ozaki() {
+    oz_split<<<(unsigned)n_ozs1, 256, 0, stream>>>(d_ozs1, d_ozs1t);
+    oz_gemm<<<(unsigned)cdiv(n_ozg1, 4), 256, 0, stream>>>(d_ozg1, d_ozg1t, n_ozg1);
+    oz_split<<<(unsigned)n_ozs2, 256, 0, stream>>>(d_ozs2, d_ozs2t);
+    oz_gemm<<<(unsigned)cdiv(n_ozg2, 4), 256, 0, stream>>>(d_ozg2, d_ozg2t, n_ozg2);
+    HIPCHK(hipGetLastError());
   }
 
   bool schur_grp2 = !env_off("CLRSDP_SCHUR_GRP2");  // (per handle: tests switch it)
@@ -2438,10 +2517,14 @@ struct Solver final : HandleBase {
         return;
       }
     }
-    p_s1x.launch(stream, 1.0, 0.0);
-    p_s1y.launch(stream, 1.0, 0.0);
-    p_s2x.launch(stream, 1.0, 0.0);
-    p_s2y.launch(stream, 1.0, 0.0);
+    if (use_oz) {
+      launch_ozaki();
+    } else {
+      p_s1x.launch(stream, 1.0, 0.0);
+      p_s1y.launch(stream, 1.0, 0.0);
+      p_s2x.launch(stream, 1.0, 0.0);
+      p_s2y.launch(stream, 1.0, 0.0);
+    }
     if (nb()) extract_AY<T><<<nb(), 256, 0, stream>>>(d_ayd, BY, AY);
     if (n_pairs)
       schur_assemble<T><<<cdiv(n_pairs, 256), 256, 0, stream>>>(d_scd, nc(), d_sbd, rsums, lam, BX,

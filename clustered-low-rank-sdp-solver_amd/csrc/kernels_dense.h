@@ -822,6 +822,122 @@ __global__ __launch_bounds__(256) void potrf_blk_update(const BlkPotrfDesc<T>* _
 }
 
 // ------------------------------------------------------------------------------------------
+// Double-double GEMM on the int8 matrix cores (Ozaki scheme; round 6, the Schur products of
+// multi-word m = 1 blocks).  Every row of op(A) is scaled by 2^-E (|a| 2^-E < 1/2) and written as
+// OZ_S base-2^7 digits d_p in [-64, 64], each the rounded leading part of the exact double-double
+// remainder:  a = 2^E sum_{p < OZ_S} d_p 2^-7(p+1)  (every column of op(B) likewise, 2^F).  Then
+//     (op(A) op(B))_ij = 2^(E_i + F_j) sum_L 2^-7(L+2) sum_{p+q=L} (D_p G_q)_ij ,
+// every level-L sum of int8 products accumulates exactly in int32 (|.| <= 16 Kpad 64^2 < 2^31 for
+// Kpad < 2^15) on v_mfma_i32_16x16x64_i8 and converts exactly to fp64; the OZ_S levels are summed
+// in double-double, smallest first.  Levels L >= OZ_S are dropped: ~2^-7 OZ_S = 2^-112 relative
+// to 2^(E_i + F_j) K -- a row / column-normwise bound, where the VALU GEMM's is componentwise.
+// 136 int8 MFMAs per 16 x 16 tile and 64-k chunk against 64 double-double FMAs per output and k
+// on the VALU: 9.1 against 15.0 us for 16 products 64 x 64 @ 64 x 128, 15.1 against 43.0 us for
+// 64 (tools/micro/ozaki_dd_bench.hip, same accuracy against a host double-double reference).
+// Digit planes: D[(p * Rpad + v) * Kpad + k] (int8, zero-padded: the buffers are zeroed once and
+// the split writes only v < nv, k < K).
+// (Ozaki, Ogita, Oishi & Rump, Numer. Algorithms 59 (2012); integer slices as in Ootomo, Ozaki &
+// Yokota, IJHPCA 38 (2024).)
+// ------------------------------------------------------------------------------------------
+constexpr int OZ_S = 16;
+typedef int oz_v4i __attribute__((ext_vector_type(4)));
+struct OzSplitDesc {
+  const mw::dd* X;     // vector v, element k at X[v * sv + k * sk]
+  long long sv, sk;
+  signed char* D;      // digit planes, [OZ_S][Rpad][Kpad]
+  int* E;              // per-vector exponent
+  int nv, K, Rpad, Kpad;
+};
+// one wave per vector (4 per workgroup); t2d: TileRef{desc, group of 4 vectors}
+__global__ __launch_bounds__(256) void oz_split(const OzSplitDesc* __restrict__ descs,
+                                                const TileRef* __restrict__ t2d) {
+  const TileRef tr = t2d[blockIdx.x];
+  const OzSplitDesc d = descs[tr.p];
+  const int v = 4 * tr.t + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (v >= d.nv) return;
+  const mw::dd* x = d.X + (size_t)v * d.sv;
+  int ex = -1100;
+  for (int k = lane; k < d.K; k += 64) {
+    const double h = x[(size_t)k * d.sk].hi;
+    if (h != 0.0) ex = max(ex, ilogb(h));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ex = max(ex, __shfl_xor(ex, o));
+  const int E = ex + 2;  // |x| < 2^(ex+1) = 2^E / 2
+  for (int k = lane; k < d.K; k += 64) {
+    const mw::dd a = x[(size_t)k * d.sk];
+    double h = ldexp(a.hi, -E), l = ldexp(a.lo, -E);
+    signed char* out = d.D + (size_t)v * d.Kpad + k;
+#pragma unroll
+    for (int p = 0; p < OZ_S; ++p) {
+      h *= 128.0;
+      l *= 128.0;
+      const double dg = rint(h);
+      double e;
+      h = mw::two_sum(h - dg, l, e);  // (h - dg is exact: |h - dg| <= 1/2 on h's grid)
+      l = e;
+      out[(size_t)p * d.Rpad * d.Kpad] = (signed char)(int)dg;
+    }
+  }
+  if (lane == 0) d.E[v] = E;
+}
+struct OzGemmDesc {
+  const signed char* DA;  // rows of op(A): [OZ_S][RpadA][Kpad]
+  const int* EA;
+  const signed char* DB;  // columns of op(B): [OZ_S][RpadB][Kpad]
+  const int* EB;
+  mw::dd* C;              // M x N, ld ldc:  C = op(A) op(B)
+  int RpadA, RpadB, Kpad, ldc, M, N, tn, pad;
+};
+// one wave per 16 x 16 output tile (tile t: rows 16 (t / tn), columns 16 (t % tn)), 4 per
+// workgroup; t2d: TileRef{desc, tile} by groups of 4 consecutive entries per workgroup
+__global__ __launch_bounds__(256) void oz_gemm(const OzGemmDesc* __restrict__ descs,
+                                               const TileRef* __restrict__ t2d, int ntiles) {
+  const int wi = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (wi >= ntiles) return;
+  const TileRef tr = t2d[wi];
+  const OzGemmDesc d = descs[tr.p];
+  const int r0 = 16 * (tr.t / d.tn), c0 = 16 * (tr.t % d.tn);
+  const size_t pa = (size_t)d.RpadA * d.Kpad, pb = (size_t)d.RpadB * d.Kpad;
+  const signed char* ra = d.DA + (size_t)(r0 + (l & 15)) * d.Kpad + 16 * (l >> 4);
+  const signed char* rb = d.DB + (size_t)(c0 + (l & 15)) * d.Kpad + 16 * (l >> 4);
+  oz_v4i acc[OZ_S];
+#pragma unroll
+  for (int L = 0; L < OZ_S; ++L) acc[L] = oz_v4i{0, 0, 0, 0};
+  for (int k0 = 0; k0 < d.Kpad; k0 += 64) {
+    oz_v4i a[OZ_S], b[OZ_S];
+#pragma unroll
+    for (int p = 0; p < OZ_S; ++p) {
+      a[p] = *reinterpret_cast<const oz_v4i*>(ra + p * pa + k0);
+      b[p] = *reinterpret_cast<const oz_v4i*>(rb + p * pb + k0);
+    }
+#pragma unroll
+    for (int L = 0; L < OZ_S; ++L)
+#pragma unroll
+      for (int p = 0; p <= L; ++p) acc[L] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[p], b[L - p], acc[L], 0, 0, 0);
+  }
+  // C/D layout: column l & 15, row 4 (l >> 4) + r
+  const int col = c0 + (l & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double hi = 0.0, lo = 0.0;
+#pragma unroll
+    for (int L = OZ_S - 1; L >= 0; --L) {  // smallest level first; every term exact in fp64
+      double e;
+      hi = mw::two_sum(hi, ldexp((double)acc[L][r], -7 * (L + 2)), e);
+      lo += e;
+    }
+    const int row = r0 + 4 * (l >> 4) + r;
+    if (row < d.M && col < d.N) {
+      double e;
+      const double h = mw::quick_two_sum(hi, lo, e);
+      const int sc = d.EA[row] + d.EB[col];
+      d.C[row + (size_t)col * d.ldc] = mw::dd(ldexp(h, sc), ldexp(e, sc));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // eigmin_lds: smallest eigenvalue of a symmetric matrix (n <= NMAX), 512 threads.  The matrix
 // is symmetrised into LDS (ld = n), tridiagonalised by Householder reflections (full storage),
 // then one wave runs a 64-point Sturm multisection.

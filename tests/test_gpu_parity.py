@@ -244,7 +244,7 @@ def test_stage_parity_sphere_packing_shape_qd(pk, oracle):
     _stage_compare(pk, oracle, consm, ar.asarray(b), iters_before=3, words=4, ar=ar, tol=1e-45)
 
 
-@pytest.mark.parametrize("variant", ["default", "full-pairs", "one-cu-potrf"])
+@pytest.mark.parametrize("variant", ["default", "full-pairs", "one-cu-potrf", "valu-products"])
 @pytest.mark.parametrize("bits", [128, 256])
 def test_stage_parity_dd_c4_shape(pk, bits, variant, monkeypatch):
     """Config 4 at its own cluster shape (J = 2, delta = 64, rank 2, n_y = 64, dim_S = 127,
@@ -255,9 +255,12 @@ def test_stage_parity_dd_c4_shape(pk, bits, variant, monkeypatch):
     Schur pairings: only the upper tiles of V^T X^-1 V, V^T Y V with schur_assemble reading
     (min, max) (the m = 1 default, round 6) and the full products (CLRSDP_MW_PAIR_UPPER=0); both
     factorisations of S_j: the blocked potrf across workgroups (potrf_blk_*, the default above
-    n = 64, round 6) and the one-CU chol_lookahead (CLRSDP_POTRF_BLK=0)."""
+    n = 64, round 6) and the one-CU chol_lookahead (CLRSDP_POTRF_BLK=0); both forms of the four
+    Schur products: on the int8 matrix cores (Ozaki scheme, oz_split / oz_gemm, the double-double
+    default for m = 1, round 6) and on the VALU (gemm_valu_ks, CLRSDP_OZAKI=0)."""
     monkeypatch.setenv("CLRSDP_MW_PAIR_UPPER", "0" if variant == "full-pairs" else "1")
     monkeypatch.setenv("CLRSDP_POTRF_BLK", "0" if variant == "one-cu-potrf" else "1")
+    monkeypatch.setenv("CLRSDP_OZAKI", "0" if variant == "valu-products" else "1")
     _stage_compare_fixture(pk, "c4dd", 2, 1e-25, bits)
 
 
