@@ -1271,6 +1271,48 @@ __device__ inline mw::qd recip_fast<mw::qd>(const mw::qd& q) {
 #endif
 }
 
+// a (quad-double) x b (double-double): the truncated quad-double product with b's words 2, 3 zero
+// written out (the O(eps^3) terms a2 b1 + a3 b0 kept, as in operator*): ~70 operations against
+// ~115 for the full product
+__device__ inline mw::qd qd_mul_dd(const mw::qd& a, const mw::dd& b) {
+  MW_EXACT
+  double q0, q1, q2, q4, q5;
+  const double p0 = mw::two_prod(a.x[0], b.hi, q0);
+  double p1 = mw::two_prod(a.x[0], b.lo, q1);
+  double p2 = mw::two_prod(a.x[1], b.hi, q2);
+  const double p4 = mw::two_prod(a.x[1], b.lo, q4);
+  const double p5 = mw::two_prod(a.x[2], b.hi, q5);
+  mw::three_sum(p1, p2, q0);
+  mw::three_sum(p2, q1, q2);
+  double e4, t0, t1;
+  const double p3 = mw::two_sum(p4, p5, e4);
+  const double s0 = mw::two_sum(p2, p3, t0);
+  double s1 = mw::two_sum(q1, e4, t1);
+  double s2 = q2;
+  s1 = mw::two_sum(s1, t0, t0);
+  s2 += (t0 + t1);
+  s1 += a.x[2] * b.lo + a.x[3] * b.hi + q0 + q4 + q5;
+  return mw::qd_renorm(p0, p1, s0, s1, s2);
+}
+// 1/q at quad-double with ONE Newton step from the double-double reciprocal r (the LDL pivot of
+// chol_lookahead with opts bit 1, round 6 form): e = 1 - q r to double-double (|e| ~ 2^-104:
+// 1 - q0 r exact, the rest by two-sums, ~2^-210 absolute), then r + r e as the four words
+// (r.hi, r.lo, (r e).hi, (r e).lo) renormalised -- ~2^-208 relative as before, but ~160
+// operations on the serial pivot chain against ~330 (a quad-double product, two quad-double
+// additions)
+__device__ inline mw::qd recip_qd_newton1(const mw::qd& q) {
+  MW_EXACT
+  const mw::dd r = recip_fast(mw::dd(q.x[0], q.x[1]));
+  const mw::qd p = qd_mul_dd(q, r);
+  double e1, e2;
+  const double eh = mw::two_sum(1.0 - p.x[0], -p.x[1], e1);  // (1 - p0 exact: p0 = 1 to ~2^-104)
+  const double s = mw::two_sum(eh, -p.x[2], e2);
+  double el;
+  const double eq = mw::quick_two_sum(s, (e1 + e2) - p.x[3], el);
+  const mw::dd d = r * mw::dd(eq, el);
+  return mw::qd_renorm(r.hi, r.lo, d.hi, d.lo, 0.0);
+}
+
 template <class T, int NB, int NT = 256>
 __global__ __launch_bounds__(NT) void potrf_batched(const MatDesc<T>* __restrict__ descs,
                                                      int* __restrict__ info) {

@@ -529,9 +529,7 @@ __device__ __forceinline__ int chol_lookahead_body(const MatDesc<T>& d, const Ma
     if constexpr (LDL) {
       if constexpr (std::is_same<T, mw::qd>::value) {
         if (opts & 2) {
-          rs = T(recip_fast(mw::dd(dn.x[0], dn.x[1])));
-          const T e = T(1.0) - dn * rs;
-          rs = rs + T(mw::dd(rs.x[0], rs.x[1]) * mw::dd(e.x[0], e.x[1]));
+          rs = recip_qd_newton1(dn);
         } else {
           rs = recip_fast(dn);
         }
