@@ -45,6 +45,14 @@ HBM_PEAK_GBS = 8000.0
 # (tools/micro/mw_peak.hip -> profiles/r01_mw_peak.log: dd 1.868 T/s, qd 0.349 T/s; fp64 FMA
 # 30.2 T/s, so a dd multiply-add costs 16.2 and a qd one 86.5 fp64 FMA slots)
 MW_VALU_PEAK_TFLOPS = {2: 3.736, 4: 0.698}
+# double-double Schur products of m = 1 blocks on the int8 matrix cores (Ozaki scheme, round 6,
+# oz_gemm in kernels_dense.h): every double-double multiply-add of the product costs 136 int8
+# multiply-adds (16 digits per operand, the 136 digit pairs of levels 0..15).  Dense int8 MFMA
+# peak 5.0 POPS (2x the ~2.5 PF dense BF16 rate per clock, /opt/skills/guides/MI355X_MICROARCH.md
+# "Matrix cores"), so the stage's ceiling in double-double flops is 2 x 5.0e15 / 2 / 136.
+I8_MFMA_PEAK_TOPS = 5000.0
+OZAKI_DIGIT_PAIRS = 136
+OZAKI_DD_PEAK_TFLOPS = 2 * (I8_MFMA_PEAK_TOPS / 2) / OZAKI_DIGIT_PAIRS
 
 
 def env_on(name):
@@ -364,6 +372,12 @@ def main():
     issued, issued_src = schur_pmc_issued(args.config, args.precision, world, args.clusters)
     achieved = fl / sch_s / 1e12   # in flops of the word type (multi-word flops when w > 1)
     peak = FP64_MFMA_PEAK_TFLOPS if args.precision == 1 else MW_VALU_PEAK_TFLOPS[args.precision]
+    # the library takes the int8 (Ozaki) Schur products at double-double when every block has
+    # m = 1 (clrsdp.hip build_ozaki) unless CLRSDP_OZAKI=0
+    ozaki = (args.precision == 2 and not os.environ.get("CLRSDP_OZAKI", "1").startswith("0")
+             and all(mj == 1 for mj in bi.m))
+    if ozaki:
+        peak = OZAKI_DD_PEAK_TFLOPS
     # the library's default (clrsdp.hip use_graph / graph_ok): replay at world 1 unless
     # CLRSDP_NO_GRAPH, and at double-double / quad-double only with CLRSDP_GRAPH_MW; sharded only
     # with CLRSDP_GRAPH_RCCL on the native exchange
@@ -395,10 +409,13 @@ def main():
                                    f"C3-sized shard per GPU)" if weak else
                                    f"{cfg['J']} clusters sharded over {world} GPUs (strong)")
                                   if world > 1 else "1 GPU"},
-        "roofline": {"bound": "mfma" if args.precision == 1 else "valu",
+        "roofline": {"bound": "mfma" if args.precision == 1 or ozaki else "valu",
                      "kernel": "Schur assembly (stage SCHUR)",
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "peak_source": "MI355X fp64 matrix spec" if args.precision == 1 else
+                                    ("int8 matrix cores (Ozaki scheme): 5.0 POPS dense / %d int8 "
+                                     "multiply-adds per double-double multiply-add, in dd flops"
+                                     % OZAKI_DIGIT_PAIRS) if ozaki else
                                     "measured %s multiply-add ceiling x 2 (profiles/r01_mw_peak.log)"
                                     % DTYPES[args.precision],
                      "frac": achieved / peak,
