@@ -1160,6 +1160,7 @@ struct Solver final : HandleBase {
   // schur_fused_f64 (every local block delta <= 128): V^T X^-1 formed on chip, one workgroup
   // per 64-row block; CLRSDP_SCHUR_FUSED=0 keeps the V^T X^-1 GEMM + schur_pairs_f64 pair
   bool schur_fused = false;
+  bool fused_one = false;   // schur_fused_f64<.., .., .., true>: one column tile per workgroup (small batches)
   bool fused_grp2 = false;  // schur_fused_f64<.., .., true>: the rank-2 group-sum epilogue (every block grp = 2)
   bool fused_y = false;  // schur_fused_f64<0, true>: V^T Y on chip too (no p_ty); CLRSDP_SCHUR_FUSED_Y=0
   FusedPairDesc* d_fpd = nullptr;
@@ -2021,9 +2022,18 @@ struct Solver final : HandleBase {
       for (const PairTileDesc& t : ptd) {
         schur_fused = schur_fused && t.del <= 128;
         fwg += cdiv(t.K, 64);
-        if (!(ef && ef[0] == '1')) schur_fused = schur_fused && t.del > 64;
       }
-      if (!(ef && ef[0] == '1')) schur_fused = schur_fused && fwg >= 128;
+      // round 6: below half the CUs, with 64 < delta, the one-tile-per-workgroup form (ONE) is
+      // taken (8-cluster shard of C3: 1572-1601 -> 1607-1681 it/s against the unfused pair, three
+      // A/B pairs; at C2's delta = 64 it lost 2 %: 24.9 against 22.6 us)
+      // (CLRSDP_SCHUR_FUSED_ONE=0: never, =1: whenever the fused kernel runs)
+      fused_one = fwg < 128 && !env_off("CLRSDP_SCHUR_FUSED_ONE");
+      for (const PairTileDesc& t : ptd) fused_one = fused_one && t.del > 64;
+      if (env_on("CLRSDP_SCHUR_FUSED_ONE")) fused_one = true;
+      if (!(ef && ef[0] == '1') && !fused_one) {
+        for (const PairTileDesc& t : ptd) schur_fused = schur_fused && t.del > 64;
+        schur_fused = schur_fused && fwg >= 128;
+      }
       if (schur_fused) {
         std::vector<FusedPairDesc> fpd;
         std::vector<int> fnt;
@@ -2039,16 +2049,29 @@ struct Solver final : HandleBase {
           fpd.push_back(f);
           fnt.push_back(cdiv(b.K, 64));
         }
-        const std::vector<TileRef> ft2d = tile_major(fnt);
+        const char* efy = std::getenv("CLRSDP_SCHUR_FUSED_Y");
+        fused_y = !(efy && efy[0] == '0');
+        fused_one = fused_one && fused_y;  // (instantiated with V^T Y on chip only)
+        std::vector<TileRef> ft2d = tile_major(fnt);
+        if (fused_one) {  // every (row block a, tile s of its share): t = a + 64 s
+          std::vector<int> fnt1;
+          for (int nr : fnt) fnt1.push_back(64 * (nr / 2 + 1));
+          ft2d.clear();
+          for (const TileRef& r : tile_major(fnt1)) {
+            const int nr = fnt[r.p], a = r.t % 64, sidx = r.t / 64;
+            const int nbt = (nr % 2 == 0 && a >= nr / 2) ? nr / 2 : nr / 2 + 1;
+            if (a < nr && sidx < nbt) ft2d.push_back(r);
+          }
+        }
         n_fwg = (int)ft2d.size();
         d_fpd = descs.own(fpd);
         d_fpt2d = descs.own(ft2d);
-        const char* efy = std::getenv("CLRSDP_SCHUR_FUSED_Y");
-        fused_y = !(efy && efy[0] == '0');
         fused_grp2 = any_grp2;
         for (const void* k : {(const void*)schur_fused_f64<0>, (const void*)schur_fused_f64<0, true>,
                               (const void*)schur_fused_f64<0, false, true>,
-                              (const void*)schur_fused_f64<0, true, true>})
+                              (const void*)schur_fused_f64<0, true, true>,
+                              (const void*)schur_fused_f64<0, true, false, true>,
+                              (const void*)schur_fused_f64<0, true, true, true>})
           HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)schur_fused::LDS));
       }
@@ -2499,7 +2522,11 @@ struct Solver final : HandleBase {
         static const bool force_full = env_on("CLRSDP_SCHUR_FULL");
         const bool full = force_full || !fac2 || n_gsum > 0 || lu_sq();
         s_lower = schur_fused && !full;
-        if (schur_fused && fused_y && fused_grp2)
+        if (schur_fused && fused_one && fused_grp2)
+          schur_fused_f64<0, true, true, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
+        else if (schur_fused && fused_one)
+          schur_fused_f64<0, true, false, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
+        else if (schur_fused && fused_y && fused_grp2)
           schur_fused_f64<0, true, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
         else if (schur_fused && fused_y)
           schur_fused_f64<0, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);

@@ -2265,7 +2265,11 @@ __device__ __forceinline__ int st_idx(int row, int col) { return row * 64 + (col
 // GRP2 (every descriptor grp = 2): the rank-2 group-sum epilogue.  A template parameter, not a
 // branch on d.grp: the branch made the rank-1 (C3) instance spill 92 B/lane at 256 VGPRs
 // (63.7 against 57.3 us per launch, round 6).
-template <int DBG = 0, bool YV = false, bool GRP2 = false>
+// ONE (round 6, small batches): each workgroup forms TXt_a (and TYt_a) and then ONE column tile
+// s of row block a's share (tile ref t = a + 64 s) instead of all nb of them, so a batch with
+// few row blocks (C2: 16 clusters x 4 = 64 workgroups, the 8-cluster shard: 32) spreads over
+// 2.5x the workgroups at the price of recomputing phase 1 per tile.
+template <int DBG = 0, bool YV = false, bool GRP2 = false, bool ONE = false>
 __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __restrict__ descs,
                                                        const TileRef* __restrict__ t2d,
                                                        unsigned long long* stamp = nullptr,
@@ -2280,11 +2284,12 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
   auto P1 = [&](int img) { return sm_fused + (img ? VR : YR); };
   const TileRef tr = t2d[blockIdx.x];
   const FusedPairDesc d = descs[tr.p];
-  const int a = tr.t, K = d.K, D = d.del;
+  const int a = ONE ? tr.t % 64 : tr.t, K = d.K, D = d.del;
   const int T = (K + 63) / 64, a0 = 64 * a;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nt = w & 3, h = w >> 2, lr = lane & 15, lk = lane >> 4;
-  const int nb = (T % 2 == 0 && a >= T / 2) ? T / 2 : T / 2 + 1;  // tiles of this workgroup
+  const int nb = (T % 2 == 0 && a >= T / 2) ? T / 2 : T / 2 + 1;  // tiles of this row block
+  const int s_lo = ONE ? tr.t / 64 : 0, s_hi = ONE ? s_lo + 1 : nb;  // the ones of this workgroup
   // ---------------- phase 1: C' = X^-1 V_a (and Y V_a)
   d4 c1[4], c1y[YV ? 4 : 1];
 #pragma unroll
@@ -2391,7 +2396,7 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
   }
   // phase 2's first operands load during the swap of the K halves (through the V_b region)
   if constexpr (!YV) loady();
-  loadv(a);
+  loadv((a + s_lo) % T);
   __syncthreads();  // every wave is done with the last phase-1 image
   if constexpr (YV) {  // TYt_a fragments straight from the accumulators (tile (mt, nt), mt = 4h + q)
 #pragma unroll
@@ -2420,10 +2425,10 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
   __syncthreads();
   const double* yrow = Yf + nt * 32 * 64 + lane;     // chunk c at yrow[64 c]
   const double* vrow = Vf + 2 * h * 64 + lane;       // chunk c, tile 2h + u at vrow[256 c + 64 u]
-  for (int s = 0; s < nb; ++s) {
+  for (int s = s_lo; s < s_hi; ++s) {
     const int b = (a + s) % T, b0 = 64 * b;
     const bool diag = s == 0;
-    if (s + 1 < nb) loadv((a + s + 1) % T);
+    if (s + 1 < s_hi) loadv((a + s + 1) % T);
     // ---------------- phase 2: P_X, P_Y for the column tiles bt = 2h, 2h+1
     d4 px[2], py[2];
 #pragma unroll
@@ -2472,7 +2477,7 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int r = 0; r < 4; ++r) St[st_idx(16 * nt + 4 * r + lk, 16 * (2 * h + u) + lr)] = g[u][r];
-    if (s + 1 < nb) storev();
+    if (s + 1 < s_hi) storev();
     __syncthreads();
     // (p, q) and its mirror (q, p) from the staging tile as 64-row column segments (lower
     // triangle only unless full: the tile whose row block is the larger one, and p >= q of a

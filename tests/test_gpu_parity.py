@@ -152,15 +152,16 @@ def test_stage_parity_fp64_rank2_group_sums(pk, oracle, cfg, grp2, monkeypatch):
     _stage_compare(pk, oracle, cons, b)
 
 
-@pytest.mark.parametrize("fused", ["0", "1", "1-ty"])
+@pytest.mark.parametrize("fused", ["0", "1", "1-ty", "1-multi"])
 @pytest.mark.parametrize("cfg", CONFIGS_GPU[-4:-1], ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_stage_parity_fp64_schur_paths(pk, oracle, cfg, fused, monkeypatch):
-    """Every Schur path at every stage: schur_fused_f64 with V^T Y formed on chip ("1", the
-    default where the fused kernel is taken: when it fills half the CUs with 64 < delta <= 128,
-    so these small instances force it), the fused kernel reading V^T Y from the side-stream GEMM
-    ("1-ty"), and the V^T X^-1 GEMM + schur_pairs_f64 pair ("0")."""
+    """Every Schur path at every stage: schur_fused_f64 with V^T Y formed on chip, one column tile
+    per workgroup ("1": what these small batches take by default since round 6), the same with
+    all of a row block's tiles per workgroup ("1-multi", the C3 form), the fused kernel reading
+    V^T Y from the side-stream GEMM ("1-ty"), and the V^T X^-1 GEMM + schur_pairs_f64 pair ("0")."""
     monkeypatch.setenv("CLRSDP_SCHUR_FUSED", fused[0])
     monkeypatch.setenv("CLRSDP_SCHUR_FUSED_Y", "0" if fused == "1-ty" else "1")
+    monkeypatch.setenv("CLRSDP_SCHUR_FUSED_ONE", "0" if fused == "1-multi" else "1")
     cons, b = pk.synth(seed=3, **cfg)
     _stage_compare(pk, oracle, cons, b)
 
