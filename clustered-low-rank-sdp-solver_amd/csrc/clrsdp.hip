@@ -1161,6 +1161,7 @@ struct Solver final : HandleBase {
   // per 64-row block; CLRSDP_SCHUR_FUSED=0 keeps the V^T X^-1 GEMM + schur_pairs_f64 pair
   bool schur_fused = false;
   bool fused_one = false;   // schur_fused_f64<.., .., .., true>: one column tile per workgroup (small batches)
+  bool fused_d64 = false;   // schur_fused_f64<.., .., .., true, true>: the ONE form at delta <= 64
   bool fused_grp2 = false;  // schur_fused_f64<.., .., true>: the rank-2 group-sum epilogue (every block grp = 2)
   bool fused_y = false;  // schur_fused_f64<0, true>: V^T Y on chip too (no p_ty); CLRSDP_SCHUR_FUSED_Y=0
   FusedPairDesc* d_fpd = nullptr;
@@ -2013,8 +2014,8 @@ struct Solver final : HandleBase {
       if (n_ptiles) { d_ptd = descs.own(ptd); d_pt2d = descs.own(pt2d); }
       // the fused kernel: same blocks, one workgroup per 64-row block of each
       // Taken when it fills at least half the CUs with 64 < delta <= 128 (C3 and its 2-rank
-      // shards): with fewer row blocks (small cluster counts) or delta <= 64 (its 32 k-chunks
-      // half empty: C2) the unfused pair, with more and smaller workgroups, is faster.
+      // shards), and in its ONE form below half the CUs (small cluster counts; at delta <= 64, C2,
+      // the D64 instance).  Otherwise the unfused pair, with more and smaller workgroups.
       // CLRSDP_SCHUR_FUSED=0 / 1 forces either.
       const char* ef = std::getenv("CLRSDP_SCHUR_FUSED");
       schur_fused = !(ef && ef[0] == '0') && !ptd.empty();
@@ -2028,7 +2029,12 @@ struct Solver final : HandleBase {
       // A/B pairs; at C2's delta = 64 it lost 2 %: 24.9 against 22.6 us)
       // (CLRSDP_SCHUR_FUSED_ONE=0: never, =1: whenever the fused kernel runs)
       fused_one = fwg < 128 && !env_off("CLRSDP_SCHUR_FUSED_ONE");
-      for (const PairTileDesc& t : ptd) fused_one = fused_one && t.del > 64;
+      // (round 6, late: with every delta <= 64 the D64 instance of the ONE form -- half the MFMAs
+      // of the padded one -- replaces the unfused pair below half the CUs, C2;
+      // CLRSDP_SCHUR_FUSED_D64=0 keeps the padded instance wherever the fused kernel runs)
+      fused_d64 = !env_off("CLRSDP_SCHUR_FUSED_D64");
+      for (const PairTileDesc& t : ptd) fused_d64 = fused_d64 && t.del <= 64;
+      for (const PairTileDesc& t : ptd) fused_one = fused_one && (t.del > 64 || fused_d64);
       if (env_on("CLRSDP_SCHUR_FUSED_ONE")) fused_one = true;
       if (!(ef && ef[0] == '1') && !fused_one) {
         for (const PairTileDesc& t : ptd) schur_fused = schur_fused && t.del > 64;
@@ -2052,6 +2058,7 @@ struct Solver final : HandleBase {
         const char* efy = std::getenv("CLRSDP_SCHUR_FUSED_Y");
         fused_y = !(efy && efy[0] == '0');
         fused_one = fused_one && fused_y;  // (instantiated with V^T Y on chip only)
+        fused_d64 = fused_d64 && fused_one;   // (instantiated in the ONE form only)
         std::vector<TileRef> ft2d = tile_major(fnt);
         if (fused_one) {  // every (row block a, tile s of its share): t = a + 64 s
           std::vector<int> fnt1;
@@ -2071,7 +2078,9 @@ struct Solver final : HandleBase {
                               (const void*)schur_fused_f64<0, false, true>,
                               (const void*)schur_fused_f64<0, true, true>,
                               (const void*)schur_fused_f64<0, true, false, true>,
-                              (const void*)schur_fused_f64<0, true, true, true>})
+                              (const void*)schur_fused_f64<0, true, true, true>,
+                              (const void*)schur_fused_f64<0, true, false, true, true>,
+                              (const void*)schur_fused_f64<0, true, true, true, true>})
           HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)schur_fused::LDS));
       }
@@ -2522,7 +2531,11 @@ struct Solver final : HandleBase {
         static const bool force_full = env_on("CLRSDP_SCHUR_FULL");
         const bool full = force_full || !fac2 || n_gsum > 0 || lu_sq();
         s_lower = schur_fused && !full;
-        if (schur_fused && fused_one && fused_grp2)
+        if (schur_fused && fused_d64 && fused_grp2)
+          schur_fused_f64<0, true, true, true, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
+        else if (schur_fused && fused_d64)
+          schur_fused_f64<0, true, false, true, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
+        else if (schur_fused && fused_one && fused_grp2)
           schur_fused_f64<0, true, true, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);
         else if (schur_fused && fused_one)
           schur_fused_f64<0, true, false, true><<<n_fwg, 512, schur_fused::LDS, stream>>>(d_fpd, d_fpt2d, stamps + 4, full);

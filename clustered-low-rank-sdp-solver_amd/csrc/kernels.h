@@ -2269,7 +2269,11 @@ __device__ __forceinline__ int st_idx(int row, int col) { return row * 64 + (col
 // s of row block a's share (tile ref t = a + 64 s) instead of all nb of them, so a batch with
 // few row blocks (C2: 16 clusters x 4 = 64 workgroups, the 8-cluster shard: 32) spreads over
 // 2.5x the workgroups at the price of recomputing phase 1 per tile.
-template <int DBG = 0, bool YV = false, bool GRP2 = false, bool ONE = false>
+// D64 (every block delta <= 64: C2): rows 64..127 of C' and k-chunks 16..31 of phase 2 are zero,
+// so the waves of the upper half (h = 1) issue no phase-1 MFMAs (they share their SIMDs with the
+// h = 0 waves of the same nt) and phase 2 runs 16 chunks instead of 32: half the MFMAs of both
+// phases, the same sums over the nonzero terms in the same order.
+template <int DBG = 0, bool YV = false, bool GRP2 = false, bool ONE = false, bool D64 = false>
 __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __restrict__ descs,
                                                        const TileRef* __restrict__ t2d,
                                                        unsigned long long* stamp = nullptr,
@@ -2372,7 +2376,7 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     const double* S = P1(img);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      if (DBG == 2) break;
+      if (DBG == 2 || (D64 && h == 1)) break;
       const double bf = S[VOFF + (kk + lk) * LBV + 16 * nt + lr];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -2435,7 +2439,7 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
     for (int u = 0; u < 2; ++u) px[u] = py[u] = d4{0.0, 0.0, 0.0, 0.0};
     // fragment reads two chunks ahead of their MFMAs (a read an MFMA waits on exposes its
     // latency; the scheduling barriers keep the compiler from regrouping them)
-    constexpr int PD = 2;
+    constexpr int PD = 2, NCH = D64 ? 16 : 32;
     double fy[PD + 1], f0[PD + 1], f1[PD + 1];
 #pragma unroll
     for (int c = 0; c < PD; ++c) {
@@ -2444,9 +2448,9 @@ __global__ __launch_bounds__(512) void schur_fused_f64(const FusedPairDesc* __re
       f1[c] = vrow[256 * c + 64];
     }
 #pragma unroll
-    for (int c = 0; c < 32; ++c) {
+    for (int c = 0; c < NCH; ++c) {
       if (DBG == 1) break;
-      if (c + PD < 32) {
+      if (c + PD < NCH) {
         fy[(c + PD) % (PD + 1)] = yrow[64 * (c + PD)];
         f0[(c + PD) % (PD + 1)] = vrow[256 * (c + PD)];
         f1[(c + PD) % (PD + 1)] = vrow[256 * (c + PD) + 64];

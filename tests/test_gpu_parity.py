@@ -152,14 +152,17 @@ def test_stage_parity_fp64_rank2_group_sums(pk, oracle, cfg, grp2, monkeypatch):
     _stage_compare(pk, oracle, cons, b)
 
 
-@pytest.mark.parametrize("fused", ["0", "1", "1-ty", "1-multi"])
+@pytest.mark.parametrize("fused", ["0", "1", "1-ty", "1-multi", "1-pad"])
 @pytest.mark.parametrize("cfg", CONFIGS_GPU[-4:-1], ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_stage_parity_fp64_schur_paths(pk, oracle, cfg, fused, monkeypatch):
     """Every Schur path at every stage: schur_fused_f64 with V^T Y formed on chip, one column tile
     per workgroup ("1": what these small batches take by default since round 6), the same with
     all of a row block's tiles per workgroup ("1-multi", the C3 form), the fused kernel reading
-    V^T Y from the side-stream GEMM ("1-ty"), and the V^T X^-1 GEMM + schur_pairs_f64 pair ("0")."""
+    V^T Y from the side-stream GEMM ("1-ty"), and the V^T X^-1 GEMM + schur_pairs_f64 pair ("0").
+    At delta <= 64 (the delta-20 and C2-shape cases) "1" is the D64 instance of the one-tile form
+    (16 k-chunks) and "1-pad" the same form on the zero-padded 32 chunks."""
     monkeypatch.setenv("CLRSDP_SCHUR_FUSED", fused[0])
+    monkeypatch.setenv("CLRSDP_SCHUR_FUSED_D64", "0" if fused == "1-pad" else "1")
     monkeypatch.setenv("CLRSDP_SCHUR_FUSED_Y", "0" if fused == "1-ty" else "1")
     monkeypatch.setenv("CLRSDP_SCHUR_FUSED_ONE", "0" if fused == "1-multi" else "1")
     cons, b = pk.synth(seed=3, **cfg)
