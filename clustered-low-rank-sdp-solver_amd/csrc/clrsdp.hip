@@ -602,16 +602,23 @@ struct TrsmPlan : PlanBase {
     const int nc = vec ? ncv : narrow ? NCN : NCW;
     if constexpr (!std::is_same<T, double>::value) {
       if (vec) {  // (outside any graph capture)
-        static std::atomic<unsigned long long> attr_f{0}, attr_t{0};
-        static std::atomic<unsigned long long> attr_f16{0}, attr_t16{0}, a128[4];
+        static std::atomic<unsigned long long> a128[8], a64[8];
         lds_attr_once(a128[0], (const void*)trsv_wave128<T, true, NCV>, (int)trsv_wave128_lds<T>());
         lds_attr_once(a128[1], (const void*)trsv_wave128<T, false, NCV>, (int)trsv_wave128_lds<T>());
         lds_attr_once(a128[2], (const void*)trsv_wave128<T, true, NCV16>, (int)trsv_wave128_lds<T>());
         lds_attr_once(a128[3], (const void*)trsv_wave128<T, false, NCV16>, (int)trsv_wave128_lds<T>());
-        lds_attr_once(attr_t, (const void*)trsv_wave<T, true, NCV>, (int)trsv_wave_lds<T>());
-        lds_attr_once(attr_f, (const void*)trsv_wave<T, false, NCV>, (int)trsv_wave_lds<T>());
-        lds_attr_once(attr_t16, (const void*)trsv_wave<T, true, NCV16>, (int)trsv_wave_lds<T>());
-        lds_attr_once(attr_f16, (const void*)trsv_wave<T, false, NCV16>, (int)trsv_wave_lds<T>());
+        lds_attr_once(a128[4], (const void*)trsv_wave128<T, true, NCV, false>, (int)trsv_wave128_lds<T>());
+        lds_attr_once(a128[5], (const void*)trsv_wave128<T, false, NCV, false>, (int)trsv_wave128_lds<T>());
+        lds_attr_once(a128[6], (const void*)trsv_wave128<T, true, NCV16, false>, (int)trsv_wave128_lds<T>());
+        lds_attr_once(a128[7], (const void*)trsv_wave128<T, false, NCV16, false>, (int)trsv_wave128_lds<T>());
+        lds_attr_once(a64[0], (const void*)trsv_wave<T, true, NCV>, (int)trsv_wave_lds<T>());
+        lds_attr_once(a64[1], (const void*)trsv_wave<T, false, NCV>, (int)trsv_wave_lds<T>());
+        lds_attr_once(a64[2], (const void*)trsv_wave<T, true, NCV16>, (int)trsv_wave_lds<T>());
+        lds_attr_once(a64[3], (const void*)trsv_wave<T, false, NCV16>, (int)trsv_wave_lds<T>());
+        lds_attr_once(a64[4], (const void*)trsv_wave<T, true, NCV, false>, (int)trsv_wave_lds<T>());
+        lds_attr_once(a64[5], (const void*)trsv_wave<T, false, NCV, false>, (int)trsv_wave_lds<T>());
+        lds_attr_once(a64[6], (const void*)trsv_wave<T, true, NCV16, false>, (int)trsv_wave_lds<T>());
+        lds_attr_once(a64[7], (const void*)trsv_wave<T, false, NCV16, false>, (int)trsv_wave_lds<T>());
       }
     }
     t2d.clear();
@@ -621,6 +628,27 @@ struct TrsmPlan : PlanBase {
     }
     d = own(h);
     dt = own(t2d);
+  }
+  template <bool PF>
+  void launch_vec(hipStream_t s, bool trans, unsigned grid) const {
+    if constexpr (!std::is_same<T, double>::value) {
+      if (nmax > 64) {
+        const size_t l = trsv_wave128_lds<T>();
+        if (ncv == NCV16) {
+          if (trans) trsv_wave128<T, true, NCV16, PF><<<grid, 64 * NCV16, l, s>>>(d, dt);
+          else trsv_wave128<T, false, NCV16, PF><<<grid, 64 * NCV16, l, s>>>(d, dt);
+        } else {
+          if (trans) trsv_wave128<T, true, NCV, PF><<<grid, 64 * NCV, l, s>>>(d, dt);
+          else trsv_wave128<T, false, NCV, PF><<<grid, 64 * NCV, l, s>>>(d, dt);
+        }
+      } else if (ncv == NCV16) {
+        if (trans) trsv_wave<T, true, NCV16, PF><<<grid, 64 * NCV16, trsv_wave_lds<T>(), s>>>(d, dt);
+        else trsv_wave<T, false, NCV16, PF><<<grid, 64 * NCV16, trsv_wave_lds<T>(), s>>>(d, dt);
+      } else {
+        if (trans) trsv_wave<T, true, NCV, PF><<<grid, 64 * NCV, trsv_wave_lds<T>(), s>>>(d, dt);
+        else trsv_wave<T, false, NCV, PF><<<grid, 64 * NCV, trsv_wave_lds<T>(), s>>>(d, dt);
+      }
+    }
   }
   // mode (the LU fallback's factors): 0 = potrf's L; 1 = unit lower L of getrf; 2 = getrf's U,
   // read transposed (forward: U^T x = b; trans: U x = b)
@@ -632,22 +660,10 @@ struct TrsmPlan : PlanBase {
     const unsigned grid = (unsigned)t2d.size();
     if constexpr (!std::is_same<T, double>::value) {
       if (vec && mode == 0) {
-        if (nmax > 64) {
-          const size_t l = trsv_wave128_lds<T>();
-          if (ncv == NCV16) {
-            if (trans) trsv_wave128<T, true, NCV16><<<grid, 64 * NCV16, l, s>>>(d, dt);
-            else trsv_wave128<T, false, NCV16><<<grid, 64 * NCV16, l, s>>>(d, dt);
-          } else {
-            if (trans) trsv_wave128<T, true, NCV><<<grid, 64 * NCV, l, s>>>(d, dt);
-            else trsv_wave128<T, false, NCV><<<grid, 64 * NCV, l, s>>>(d, dt);
-          }
-        } else if (ncv == NCV16) {
-          if (trans) trsv_wave<T, true, NCV16><<<grid, 64 * NCV16, trsv_wave_lds<T>(), s>>>(d, dt);
-          else trsv_wave<T, false, NCV16><<<grid, 64 * NCV16, trsv_wave_lds<T>(), s>>>(d, dt);
-        } else {
-          if (trans) trsv_wave<T, true, NCV><<<grid, 64 * NCV, trsv_wave_lds<T>(), s>>>(d, dt);
-          else trsv_wave<T, false, NCV><<<grid, 64 * NCV, trsv_wave_lds<T>(), s>>>(d, dt);
-        }
+        // (CLRSDP_TRSV_PF=0: the staging loops that wait on each load of L in turn)
+        static const bool pf = !env_off("CLRSDP_TRSV_PF");
+        if (pf) launch_vec<true>(s, trans, grid);
+        else launch_vec<false>(s, trans, grid);
         HIPCHK(hipGetLastError());
         return;
       }

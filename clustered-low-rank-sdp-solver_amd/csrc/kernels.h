@@ -1536,8 +1536,55 @@ __device__ __forceinline__ T readlane_t(const T& v, int src) {  // src wave-unif
   for (int q = 0; q < (int)(sizeof(T) / 4); ++q) ti[q] = __builtin_amdgcn_readlane(vi[q], src);
   return t;
 }
+// one step's update v - c vq of the vector solves: double-double with fms_fast (one two-sum, the
+// low words added plainly: its absolute error ~2u^2(|v| + |c vq|) is the componentwise bound the
+// backward analysis of a triangular solve asks of each update, as for the factorisations' trailing
+// updates), the accurate operations otherwise
+template <class T> __device__ __forceinline__ T trsv_fms(const T& v, const T& c, const T& vq) {
+  return v - c * vq;
+}
+template <> __device__ __forceinline__ mw::dd trsv_fms(const mw::dd& v, const mw::dd& c, const mw::dd& vq) {
+  return mw::fms_fast(v, c, vq);
+}
+// two rows' fms_fast against one broadcast value with the two dependent chains interleaved
+// operation by operation (left to itself the scheduler issues one chain after the other, and a
+// lone chain waits out every fp64 latency); the same operations as mw::fms_fast per row
+template <class T>
+__device__ __forceinline__ void trsv_fms2(T& w0, const T& a0, const T& b0, T& w1, const T& a1,
+                                          const T& b1, const T& c) {
+  w0 = trsv_fms(a0, b0, c);
+  w1 = trsv_fms(a1, b1, c);
+}
+template <>
+__device__ __forceinline__ void trsv_fms2(mw::dd& w0, const mw::dd& a0, const mw::dd& b0, mw::dd& w1,
+                                          const mw::dd& a1, const mw::dd& b1, const mw::dd& c) {
+  MW_EXACT
+#define TSB __builtin_amdgcn_sched_barrier(0);
+  const double p1a = b0.hi * c.hi, p1b = b1.hi * c.hi;
+  TSB double p2a = fma(b0.hi, c.hi, -p1a), p2b = fma(b1.hi, c.hi, -p1b);
+  TSB p2a = fma(b0.hi, c.lo, p2a); p2b = fma(b1.hi, c.lo, p2b);
+  TSB p2a = fma(b0.lo, c.hi, p2a); p2b = fma(b1.lo, c.hi, p2b);
+  // two_sum(a.hi, -p1)
+  TSB const double sa = a0.hi + (-p1a), sb = a1.hi + (-p1b);
+  TSB const double ba = sa - a0.hi, bb = sb - a1.hi;
+  TSB const double ta = sa - ba, tb = sb - bb;
+  TSB const double ua = a0.hi - ta, ub = a1.hi - tb;
+  TSB const double va = (-p1a) - ba, vb = (-p1b) - bb;
+  TSB double ea = ua + va, eb = ub + vb;
+  TSB const double la = a0.lo - p2a, lb = a1.lo - p2b;
+  TSB ea = ea + la; eb = eb + lb;
+  // quick_two_sum(s, e)
+  TSB const double ra = sa + ea, rb = sb + eb;
+  TSB const double za = ra - sa, zb = rb - sb;
+  TSB w0 = mw::dd(ra, ea - za);
+  w1 = mw::dd(rb, eb - zb);
+#undef TSB
+}
 template <class T> constexpr size_t trsv_wave_lds() { return sizeof(T) * (64 * 64 + 64); }
-template <class T, bool TRANS, int NW = 4>
+// PF (round 6, late): the staging loads of L are all issued before the pivots' reciprocals and
+// before any of them is used (the loop with a runtime trip count waited on each load in turn:
+// ~n^2 / (128 NW) dependent global-load latencies); the values and their order are unchanged.
+template <class T, bool TRANS, int NW = 4, bool PF = true>
 __global__ __launch_bounds__(64 * NW) void trsv_wave(const TrsmDesc<T>* __restrict__ descs,
                                                      const int* __restrict__ t2d) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -1547,15 +1594,36 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave(const TrsmDesc<T>* __restri
   const int n = d.n, tid = threadIdx.x, lane = tid & 63;
   const T* L = d.L;
   const size_t ldl = d.ldl;
+  constexpr int NT = 64 * NW, IT = PF ? (64 * 64 + NT - 1) / NT : 1;
+  T lv[IT];
+  if constexpr (PF) {
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int e = tid + NT * u, i = e % n, j = e / n;
+      lv[u] = (e < n * n && i > j) ? L[i + (size_t)j * ldl] : T(0.0);
+    }
+  }
   if (tid < n) rdg[tid] = recip_fast(L[tid + (size_t)tid * ldl]);
   __syncthreads();
   // column q of L (rows > q) scaled by 1/l_qq; transposed: row q (columns < q), read as column
-  for (int e = tid; e < n * n; e += 64 * NW) {
-    const int i = e % n, j = e / n;  // coalesced: i runs over the rows of L
-    if (i > j) {
-      const T v = L[i + (size_t)j * ldl] * rdg[TRANS ? i : j];
-      if (TRANS) Ls[j + 64 * i] = v;
-      else Ls[i + 64 * j] = v;
+  if constexpr (PF) {
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int e = tid + NT * u, i = e % n, j = e / n;
+      if (e < n * n && i > j) {
+        const T v = lv[u] * rdg[TRANS ? i : j];
+        if (TRANS) Ls[j + 64 * i] = v;
+        else Ls[i + 64 * j] = v;
+      }
+    }
+  } else {
+    for (int e = tid; e < n * n; e += 64 * NW) {
+      const int i = e % n, j = e / n;  // coalesced: i runs over the rows of L
+      if (i > j) {
+        const T v = L[i + (size_t)j * ldl] * rdg[TRANS ? i : j];
+        if (TRANS) Ls[j + 64 * i] = v;
+        else Ls[i + 64 * j] = v;
+      }
     }
   }
   __syncthreads();
@@ -1564,7 +1632,32 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave(const TrsmDesc<T>* __restri
   T* B = d.B + (size_t)c * d.ldb;
   T v = T(0.0);
   if (lane < n) v = B[lane];
-  if (!TRANS) {
+  if constexpr (PF) {
+    // branch-free steps with the next step's coefficient read ahead of this step's arithmetic
+    // (the exec-masked form waited on each LDS read); inactive lanes keep v by a select, so
+    // every active lane runs the same operations in the same order
+    if (!TRANS) {
+      T c = Ls[lane];
+      for (int q = 0; q + 1 < n; ++q) {
+        T nx = c;
+        if (q + 2 < n) nx = Ls[lane + 64 * (q + 1)];
+        const T vq = readlane_t(v, q);
+        const T w = trsv_fms(v, c, vq);
+        v = sel(lane > q && lane < n, w, v);
+        c = nx;
+      }
+    } else {
+      T c = Ls[lane + 64 * (n - 1)];
+      for (int q = n - 1; q > 0; --q) {
+        T nx = c;
+        if (q > 1) nx = Ls[lane + 64 * (q - 1)];
+        const T vq = readlane_t(v, q);
+        const T w = trsv_fms(v, c, vq);
+        v = sel(lane < q, w, v);
+        c = nx;
+      }
+    }
+  } else if (!TRANS) {
     for (int q = 0; q + 1 < n; ++q) {
       const T vq = readlane_t(v, q);
       if (lane > q && lane < n) v = v - Ls[lane + 64 * q] * vq;
@@ -1582,7 +1675,10 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave(const TrsmDesc<T>* __restri
 // rows r and r + 64, and the scaled L passes through LDS in chunks of 32 steps (the whole matrix
 // would not fit), staged by the workgroup between two barriers per chunk.
 template <class T> constexpr size_t trsv_wave128_lds() { return sizeof(T) * (32 * 128 + 128); }
-template <class T, bool TRANS, int NW = 4>
+// PF (round 6, late): the next chunk's loads are issued into registers before the current
+// chunk's steps, so they arrive under its chain (the staging loop waited on each load in turn);
+// the values and their order are unchanged.
+template <class T, bool TRANS, int NW = 4, bool PF = true>
 __global__ __launch_bounds__(64 * NW) void trsv_wave128(const TrsmDesc<T>* __restrict__ descs,
                                                         const int* __restrict__ t2d) {
   constexpr int CH = 32;
@@ -1601,19 +1697,72 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave128(const TrsmDesc<T>* __res
   if (act && lane < n) v0 = B[lane];
   if (act && lane + 64 < n) v1 = B[lane + 64];
   const int nch = (n + CH - 1) / CH;
+  // (the register image of a chunk only where it fits beside the step loop's operands: not for
+  // quad-double at 1024 threads, 128 VGPRs)
+  constexpr bool SPF = PF && (sizeof(T) <= 16 || NW <= 4);
+  constexpr int NT = 64 * NW, IT = SPF ? (CH * 128 + NT - 1) / NT : 1;
+  T lv[IT];
+  auto loadc = [&](int ci) {  // chunk ci's entries of L into registers
+    const int q0 = (TRANS ? nch - 1 - ci : ci) * CH, qn = min(CH, n - q0);
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int e = tid + NT * u;
+      int i, qq;
+      if (TRANS) { qq = e % qn; i = e / qn; } else { i = e % n; qq = e / n; }
+      const int q = q0 + qq;
+      lv[u] = (e < qn * n && (TRANS ? i < q : i > q))
+                  ? (TRANS ? L[q + (size_t)i * ldl] : L[i + (size_t)q * ldl]) : T(0.0);
+    }
+  };
+  if constexpr (SPF) loadc(0);
   for (int ci = 0; ci < nch; ++ci) {
     const int q0 = (TRANS ? nch - 1 - ci : ci) * CH, qn = min(CH, n - q0);
     __syncthreads();  // the previous chunk is consumed (first pass: rdg is written)
-    for (int e = tid; e < qn * n; e += 64 * NW) {
-      int i, qq;
-      if (TRANS) { qq = e % qn; i = e / qn; } else { i = e % n; qq = e / n; }  // (coalesced)
-      const int q = q0 + qq;
-      T val = T(0.0);
-      if (TRANS ? i < q : i > q) val = (TRANS ? L[q + (size_t)i * ldl] : L[i + (size_t)q * ldl]) * rdg[q];
-      Ls[i + 128 * qq] = val;
+    if constexpr (SPF) {
+#pragma unroll
+      for (int u = 0; u < IT; ++u) {
+        const int e = tid + NT * u;
+        int i, qq;
+        if (TRANS) { qq = e % qn; i = e / qn; } else { i = e % n; qq = e / n; }
+        const int q = q0 + qq;
+        if (e < qn * n) Ls[i + 128 * qq] = (TRANS ? i < q : i > q) ? lv[u] * rdg[q] : T(0.0);
+      }
+    } else {
+      for (int e = tid; e < qn * n; e += 64 * NW) {
+        int i, qq;
+        if (TRANS) { qq = e % qn; i = e / qn; } else { i = e % n; qq = e / n; }  // (coalesced)
+        const int q = q0 + qq;
+        T val = T(0.0);
+        if (TRANS ? i < q : i > q) val = (TRANS ? L[q + (size_t)i * ldl] : L[i + (size_t)q * ldl]) * rdg[q];
+        Ls[i + 128 * qq] = val;
+      }
     }
     __syncthreads();
-    if (act) {
+    if constexpr (SPF) {
+      if (ci + 1 < nch) loadc(ci + 1);  // in flight under this chunk's chain
+    }
+    if (act && PF) {
+      // both rows of the lane every step, branch-free (their two chains interleave), with the
+      // next step's coefficients read ahead; inactive rows keep their value by a select
+      int qq = TRANS ? qn - 1 : 0;
+      T c0 = Ls[lane + 128 * qq], c1 = Ls[lane + 64 + 128 * qq];
+      for (int u = 0; u < qn; ++u) {
+        const int q = q0 + qq, qn1 = TRANS ? qq - 1 : qq + 1;
+        T n0 = c0, n1 = c1;
+        if (u + 1 < qn) {
+          n0 = Ls[lane + 128 * qn1];
+          n1 = Ls[lane + 64 + 128 * qn1];
+        }
+        const T vq = readlane_t(sel(q < 64, v0, v1), q & 63);
+        T w0, w1;
+        trsv_fms2(w0, v0, c0, w1, v1, c1, vq);
+        v0 = sel(TRANS ? lane < q : (lane > q && lane < n), w0, v0);
+        v1 = sel(TRANS ? lane + 64 < q : (lane + 64 > q && lane + 64 < n), w1, v1);
+        c0 = n0;
+        c1 = n1;
+        qq = qn1;
+      }
+    } else if (act) {
       for (int u = 0; u < qn; ++u) {
         const int qq = TRANS ? qn - 1 - u : u, q = q0 + qq;
         const T vq = readlane_t(sel(q < 64, v0, v1), q & 63);
