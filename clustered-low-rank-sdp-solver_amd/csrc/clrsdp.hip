@@ -577,13 +577,18 @@ struct TrsmPlan : PlanBase {
   bool vec = false;
   int ncv = NCV;
   bool four = false;  // four right-hand sides per workgroup whatever their number (latency first)
-  void add(const T* L, int ldl, T* B, int ldb, int n, int nrhs) {
+  // ident: the right-hand sides are the columns of the identity (L^-1 = L \ I); src: read them
+  // from src (ld ldb) and write the solution to B.  Both only in the vector-solve kernels
+  // (vec_rhs() after finalize); otherwise the caller fills B first.
+  void add(const T* L, int ldl, T* B, int ldb, int n, int nrhs, bool ident = false,
+           const T* src = nullptr) {
     if (n <= 0 || nrhs <= 0) return;
     rmax = std::max(rmax, nrhs);
     TrsmDesc<T> t;
     t.L = L; t.B = B; t.n = n; t.nrhs = nrhs; t.ldl = ldl; t.ldb = ldb;
     t.tile0 = 0;
-    t.pad = 0;
+    t.pad = ident ? 1 : 0;
+    t.src = src;
     h.push_back(t);
     nmax = std::max(nmax, n);
   }
@@ -621,6 +626,8 @@ struct TrsmPlan : PlanBase {
         lds_attr_once(a64[7], (const void*)trsv_wave<T, false, NCV16, false>, (int)trsv_wave_lds<T>());
       }
     }
+    if (!vec_rhs())
+      for (TrsmDesc<T>& t : h) { t.pad = 0; t.src = nullptr; }  // (the caller fills B)
     t2d.clear();
     for (size_t q = 0; q < h.size(); ++q) {
       h[q].tile0 = (int)t2d.size();
@@ -649,6 +656,12 @@ struct TrsmPlan : PlanBase {
         else trsv_wave<T, false, NCV, PF><<<grid, 64 * NCV, trsv_wave_lds<T>(), s>>>(d, dt);
       }
     }
+  }
+  // the vector-solve kernels take the identity / a separate source as right-hand sides
+  // (CLRSDP_TRSV_RHS=0: the caller copies them into B, as before round 6)
+  bool vec_rhs() const {
+    static const bool on = !env_off("CLRSDP_TRSV_RHS");
+    return on && vec && mode == 0 && !std::is_same<T, double>::value;
   }
   // mode (the LU fallback's factors): 0 = potrf's L; 1 = unit lower L of getrf; 2 = getrf's U,
   // read transposed (forward: U^T x = b; trans: U x = b)
@@ -1150,6 +1163,7 @@ struct Solver final : HandleBase {
   // L^-1 by four-wave triangular solves of the identity (S_j: on aux2, off the critical path),
   // then the same GEMV solves as the explicit-inverse path
   bool s_split = false, q_split = false, pending_sinv = false;
+  bool qf_fresh = false;  // sum_q_slabs wrote Qf = Q for this iteration's factor_q_
   int64_t s_len = 0;
   T *SLi = nullptr, *SLid = nullptr, *QLi = nullptr, *QLid = nullptr;  // L^-1 and identity images
   TrsmPlan<T> t_Sinv, t_Qinv;
@@ -1794,11 +1808,11 @@ struct Solver final : HandleBase {
         q_dx.add(Sc, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D, 1, D);
       }
       q_Wdy.add(Wc, D, dyv, (int)n_y, tvec + xo, D, tmpv + xo, D, D, 1, (int)n_y);
-      t_W.add(Sc, D, Wc, D, D, (int)n_y);
+      t_W.add(Sc, D, Wc, D, D, (int)n_y, false, Bc);
       t_t.add(Sc, D, tvec + xo, D, D, 1);
       if (s_split) {
         T* Li = SLi + c_Soff[c];
-        t_Sinv.add(Sc, D, Li, D, D, D);                                              // L^-1 = L \ I
+        t_Sinv.add(Sc, D, Li, D, D, D, true);                                        // L^-1 = L \ I
         q_t2.add(Li, D, rhs + xo, D, nullptr, 0, tvec + xo, D, D, 1, D);
         q_dx2.add(Li, D, tmpv + xo, D, nullptr, 0, dx + xo, D, D, 1, D);
       }
@@ -1846,7 +1860,7 @@ struct Solver final : HandleBase {
     q_qinv.add(Qf, (int)n_y, Qf, (int)n_y, nullptr, 0, Qinv, (int)n_y, (int)n_y, (int)n_y, (int)n_y);
     q_qdy.add(Qinv, (int)n_y, uvec, (int)n_y, nullptr, 0, dyv, (int)n_y, (int)n_y, 1, (int)n_y);
     if (q_split) {
-      t_Qinv.add(Qf, (int)n_y, QLi, (int)n_y, (int)n_y, (int)n_y);                  // L_Q^-1 = L_Q \ I
+      t_Qinv.add(Qf, (int)n_y, QLi, (int)n_y, (int)n_y, (int)n_y, true);            // L_Q^-1 = L_Q \ I
       q_qinv2.add(QLi, (int)n_y, QLi, (int)n_y, nullptr, 0, Qinv, (int)n_y, (int)n_y, (int)n_y, (int)n_y);
     }
     {
@@ -2679,7 +2693,8 @@ struct Solver final : HandleBase {
           HIPCHK(hipEventRecord(ev_sp, stream));
           HIPCHK(hipStreamWaitEvent(ls, ev_sp, 0));
         }
-        HIPCHK(hipMemcpyAsync(SLi, SLid, (size_t)s_len * sizeof(T), hipMemcpyDeviceToDevice, ls));
+        if (!t_Sinv.vec_rhs())
+          HIPCHK(hipMemcpyAsync(SLi, SLid, (size_t)s_len * sizeof(T), hipMemcpyDeviceToDevice, ls));
         t_Sinv.launch(ls, false);
         if (ls != stream) {
           HIPCHK(hipEventRecord(ev_sinv, ls));
@@ -2687,7 +2702,7 @@ struct Solver final : HandleBase {
         }
       }
       seg(CLRSDP_INNER_CINVB, [&] {
-        vlin(Wm, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
+        if (!t_W.vec_rhs()) vlin(Wm, Bm, 1.0, nullptr, 0, nullptr, 0, nB);
         t_W.launch(stream, false);            // W_j = L_j^-1 B_j
       });
     }
@@ -2699,13 +2714,18 @@ struct Solver final : HandleBase {
   // Q = sum_j slab_j (all-gathered over the ranks)
   void sum_q_slabs() {
     const int64_t q2 = n_y * n_y;
+    // (potrf factors Q in place in Qf: the slab sum writes that copy too, one launch fewer on the
+    // critical path; CLRSDP_Q_DUAL=0 keeps the separate copy)
+    static const bool dual_on = !env_off("CLRSDP_Q_DUAL");
+    T* q_dual = dual_on && !reg_Q && Qf ? Qf : nullptr;
+    qf_fresh = q_dual != nullptr;
     if (world == 1 && nc()) {
-      slab_sum4<T><<<cdiv(q2, 64), 256, 0, stream>>>(Qslab, nc(), q2, q2, Q);
+      slab_sum4<T><<<cdiv(q2, 64), 256, 0, stream>>>(Qslab, nc(), q2, q2, Q, nullptr, 0.0, 1.0, q_dual);
     } else {
       if (nc()) slab_sum4<T><<<cdiv(q2, 64), 256, 0, stream>>>(Qslab, nc(), q2, q2, xsend);
       else fill(xsend, 0.0, q2);
       exchange(2, q2);
-      slab_sum4<T><<<cdiv(q2, 64), 256, 0, stream>>>(xrecv, world, q2, q2, Q);
+      slab_sum4<T><<<cdiv(q2, 64), 256, 0, stream>>>(xrecv, world, q2, q2, Q, nullptr, 0.0, 1.0, q_dual);
     }
   }
   void factor_q() {
@@ -2713,8 +2733,10 @@ struct Solver final : HandleBase {
   }
   void factor_q_() {
     const int64_t q2 = n_y * n_y;
+    const bool fresh = qf_fresh;  // Qf = Q written by this iteration's slab sum
+    qf_fresh = false;
     if (lu_sq()) {                            // approx_lu!(perm, Q) (MPMP.jl:1499-1505)
-      vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
+      if (!fresh) vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
       lu_Q.launch(stream, info + info_Q0);
       return;
     }
@@ -2722,10 +2744,11 @@ struct Solver final : HandleBase {
       ci_Q.launch(stream, info + info_Q0);    // Qf = L_Q^-1
       q_qinv.launch(stream, 1.0, 0.0);        // Q^-1 = L_Q^-T L_Q^-1
     } else {
-      vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
+      if (!fresh) vlin(Qf, Q, 1.0, nullptr, 0, nullptr, 0, q2);
       f_Q.potrf(stream, info + info_Q0);
       if (q_split) {  // Q^-1 = L_Q^-T L_Q^-1 with L_Q^-1 = L_Q \ I
-        HIPCHK(hipMemcpyAsync(QLi, QLid, (size_t)q2 * sizeof(T), hipMemcpyDeviceToDevice, stream));
+        if (!t_Qinv.vec_rhs())
+          HIPCHK(hipMemcpyAsync(QLi, QLid, (size_t)q2 * sizeof(T), hipMemcpyDeviceToDevice, stream));
         t_Qinv.launch(stream, false);
         q_qinv2.launch(stream, 1.0, 0.0);
       }

@@ -55,8 +55,15 @@ template <class T> struct TrsmDesc {
   T* B;
   int n, nrhs, ldl, ldb;
   int tile0;  // first column-tile index of this problem in the launch
-  int pad;
+  int pad;    // trsv_wave / trsv_wave128: 1 = the right-hand sides are the identity's columns
+  const T* src;  // trsv_wave / trsv_wave128: right-hand sides read from here (ld ldb), not B
 };
+// the right-hand side entry (row, column c) of a vector solve: the identity, src, or B in place
+template <class T>
+__device__ __forceinline__ T trsv_rhs(const TrsmDesc<T>& d, const T* B, int row, int c) {
+  if (d.pad == 1) return T(row == c ? 1.0 : 0.0);
+  return d.src ? d.src[row + (size_t)c * d.ldb] : B[row];
+}
 
 // Load through an explicitly global pointer.  A pointer read from a descriptor is generic, and
 // hipcc then emits flat_load, which also counts on lgkmcnt: the first LDS wait of the MFMA loop
@@ -1631,7 +1638,7 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave(const TrsmDesc<T>* __restri
   if (c >= d.nrhs) return;  // (whole waves; no barrier follows)
   T* B = d.B + (size_t)c * d.ldb;
   T v = T(0.0);
-  if (lane < n) v = B[lane];
+  if (lane < n) v = trsv_rhs(d, B, lane, c);
   if constexpr (PF) {
     // branch-free steps with the next step's coefficient read ahead of this step's arithmetic
     // (the exec-masked form waited on each LDS read); inactive lanes keep v by a select, so
@@ -1694,8 +1701,8 @@ __global__ __launch_bounds__(64 * NW) void trsv_wave128(const TrsmDesc<T>* __res
   const bool act = c < d.nrhs;  // (wave-uniform; every wave stays for the barriers)
   T* B = d.B + (size_t)(act ? c : 0) * d.ldb;
   T v0 = T(0.0), v1 = T(0.0);
-  if (act && lane < n) v0 = B[lane];
-  if (act && lane + 64 < n) v1 = B[lane + 64];
+  if (act && lane < n) v0 = trsv_rhs(d, B, lane, c);
+  if (act && lane + 64 < n) v1 = trsv_rhs(d, B, lane + 64, c);
   const int nch = (n + CH - 1) / CH;
   // (the register image of a chunk only where it fits beside the step loop's operands: not for
   // quad-double at 1024 threads, 128 VGPRs)
@@ -3017,7 +3024,7 @@ __device__ __forceinline__ T slab_chunk_sum(const T* in, int i0, int i1, long lo
 template <class T>
 __global__ __launch_bounds__(256) void slab_sum4(const T* in, int cnt, long long stride, long long n,
                                                  T* out, const T* base = nullptr, double cbase = 0.0,
-                                                 double csum = 1.0) {
+                                                 double csum = 1.0, T* out2 = nullptr) {
   __shared__ T part[4][64];
   const int el = threadIdx.x & 63, ch = threadIdx.x >> 6;
   const long long e = (long long)blockIdx.x * 64 + el;
@@ -3028,6 +3035,7 @@ __global__ __launch_bounds__(256) void slab_sum4(const T* in, int cnt, long long
   T acc = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
   if (base) acc = base[e] * T(cbase) + acc * T(csum);
   out[e] = acc;
+  if (out2) out2[e] = acc;
 }
 
 // dy = Q^-1 r with r = cbase*base + csum*sum_{i<cnt} in[i*stride + .] (slab_sum's order): the

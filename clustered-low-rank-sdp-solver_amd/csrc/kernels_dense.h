@@ -3420,14 +3420,35 @@ __global__ __launch_bounds__(TRI ? 576 : 512) void eigmin_mx(const MatDesc<T>* _
     unsigned long long* masks = reinterpret_cast<unsigned long long*>(sc + 64);  // 8
     T* xv = reinterpret_cast<T*>(masks + 8);           // n   the eigenvector estimate
     T* part = xv + n;                                  // 8 x n  row partials of A_s x
-    // (1) leading words of the symmetrised block, then the fp64 tridiagonalisation
-    for (int j = w; j < n && w < NW; j += NW)
-      for (int i = lane; i < n; i += 64) {
-        if (i < j) continue;
-        const T s = (d.A[i + (size_t)j * d.lda] + d.A[j + (size_t)i * d.lda]) * T(0.5);
-        A[i + (size_t)j * ld] = Num<T>::hi(s);
-        A[j + (size_t)i * ld] = Num<T>::hi(s);
+    // the symmetrised entries (row lane, columns j = w + NW u) of the lane, every load issued
+    // before any is used (a loop over j waited on each strided load in turn, ~n / NW global
+    // latencies per pass; n <= 64 so one row per lane and at most JM columns per wave)
+    // (quad-double: in two halves of JH columns, registers)
+    constexpr int JM = 64 / NW, JH = sizeof(T) > 16 ? JM / 2 : JM;
+    auto load_sym = [&](T* sv, int u0) {
+#pragma unroll
+      for (int u = 0; u < JH; ++u) {
+        const int j = w + NW * (u0 + u), jc = min(j, n - 1), ic = min(lane, n - 1);
+        const T a1 = d.A[ic + (size_t)jc * d.lda], a2 = d.A[jc + (size_t)ic * d.lda];
+        sv[u] = (a1 + a2) * T(0.5);
       }
+    };
+    // (1) leading words of the symmetrised block, then the fp64 tridiagonalisation
+    if (w < NW && lane < n) {
+#pragma unroll
+      for (int u0 = 0; u0 < JM; u0 += JH) {
+        T sv[JH];
+        load_sym(sv, u0);
+#pragma unroll
+        for (int u = 0; u < JH; ++u) {
+          const int j = w + NW * (u0 + u);
+          if (j < n && lane >= j) {
+            A[lane + (size_t)j * ld] = Num<T>::hi(sv[u]);
+            A[j + (size_t)lane * ld] = Num<T>::hi(sv[u]);
+          }
+        }
+      }
+    }
     __syncthreads();
     stamp(0);
     int ex0 = 0;  // (TRI 1: T comes out scaled by 2^-ex0)
@@ -3582,9 +3603,15 @@ __global__ __launch_bounds__(TRI ? 576 : 512) void eigmin_mx(const MatDesc<T>* _
         // row partials of y = A_s x: row lane, columns j = w (mod 8)
         if (lane < n && w < NW) {
           T acc = T(0.0);
-          for (int j = w; j < n; j += NW) {
-            const T s = (d.A[lane + (size_t)j * d.lda] + d.A[j + (size_t)lane * d.lda]) * T(0.5);
-            acc = acc + s * xv[j];
+#pragma unroll
+          for (int u0 = 0; u0 < JM; u0 += JH) {
+            T sv[JH];
+            load_sym(sv, u0);
+#pragma unroll
+            for (int u = 0; u < JH; ++u) {
+              const int j = w + NW * (u0 + u);
+              if (j < n) acc = acc + sv[u] * xv[j];
+            }
           }
           part[w * n + lane] = acc;
         }
